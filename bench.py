@@ -1,0 +1,349 @@
+"""Benchmark: device-resident RS(4+2) encode + 2-erasure reconstruct on MI355X.
+
+Metric (BASELINE.json): "GiB/s device-resident RS(4+2) encode + 2-erasure
+reconstruct, batched stripes".  One *step* = one pass of the hot path over one
+batch: encode the batch (configs[1]: 65 536 objects x 4 KiB stripe, RS(4+2),
+S = 1 024) and then reconstruct two erased shards per stripe with a seeded random
+pattern per stripe (configs[2], 2-missing case).  User data per step =
+2 x N x K x S bytes; `value` = user-data GiB/s over all ranks.
+
+Inputs are resident in HBM before the timed region; batches rotate over >= 2 GiB
+so the 256 MiB Infinity Cache cannot serve them.  Multi-GPU: one process per GPU,
+each with its own stripe batches (objects are independent: weak scaling, no
+data-path collective); the only collectives are the timing barrier / max-reduce.
+
+Roofline: the dominant kernel's algorithmic bytes per launch (encode N.S.(K+M),
+reconstruct N.S.(K+e)) / its average launch time measured with HIP
+events on the launch stream, against 8.0 TB/s (MI355X_MICROARCH.md).
+cpu_baseline: oracle/rs_cpu_baseline.c (AVX-512 GFNI / AVX2 split-nibble C
+restatement of klauspost's CPU kernels -- a port, not the Go reference, which is
+absent) on the host cores of this box, same workload, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import itertools
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--stripes", type=int, default=65536)
+    p.add_argument("--stripe-kib", type=int, default=4)
+    p.add_argument("--k", type=int, default=4)
+    p.add_argument("--m", type=int, default=2)
+    p.add_argument("--rotate-gib", type=float, default=2.0)
+    p.add_argument("--no-extras", action="store_true")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--json-out", default="")
+    return p.parse_args()
+
+
+def two_erasure_masks(rng, n, t):
+    pairs = np.array(list(itertools.combinations(range(t), 2)))
+    ch = pairs[rng.integers(0, len(pairs), n)]
+    full = (1 << t) - 1
+    return (full & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32)
+
+
+def make_batches(torch, eng, n_batches, N, t, P, S, seed):
+    bufs = []
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    for _ in range(n_batches):
+        b = torch.randint(0, 256, (N, t, P), dtype=torch.uint8, device="cuda", generator=g)
+        bufs.append(b)
+    return bufs
+
+
+class KernelTimer:
+    """HIP events around each launch on the launch stream."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.pairs = {}
+
+    def start(self):
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, name, e0):
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.pairs.setdefault(name, []).append((e0, e1))
+
+    def avg_ms(self):
+        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in self.pairs.items()}
+
+
+def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, kernel_timer=True):
+    """Returns dict with step time and per-kernel averages for encode + 2-erasure
+    reconstruct (seeded per-stripe pattern, device-resident masks)."""
+    from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
+
+    t = k + m
+    P = shard_pitch_for(S)
+    batch_bytes = N * t * P
+    nb = max(2, int(np.ceil(rotate_bytes / batch_bytes)))
+    bufs = make_batches(torch, eng, nb, N, t, P, S, seed)
+    rng = np.random.default_rng(0x5EED0003)
+    masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(nb)]
+    timer = KernelTimer(torch)
+
+    def step(i, timed):
+        b = bufs[i % nb]
+        e0 = timer.start() if timed else None
+        eng.encode_unified(b, S, P, N)
+        if timed:
+            timer.stop("encode", e0)
+            e0 = timer.start()
+        eng.reconstruct_unified_devmask(b, S, P, N, masks[i % nb])
+        if timed:
+            timer.stop("reconstruct", e0)
+
+    for i in range(warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i, kernel_timer)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    eng.sync()
+    # correctness at full size: reconstructed slots hold the encoded bytes again
+    ok = True
+    for i in range(min(nb, 2)):
+        b = bufs[i]
+        chk = b[:64].clone()
+        eng.encode_unified(chk, S, P, 64)
+        torch.cuda.synchronize()
+        ok &= bool(torch.equal(chk[:, :, :S], b[:64, :, :S]))
+    km = timer.avg_ms() if kernel_timer else {}
+    del bufs, masks
+    torch.cuda.empty_cache()
+    return {"dt": dt, "steps": steps, "kernel_ms": km, "batch_bytes": batch_bytes, "n_batches": nb, "ok": ok}
+
+
+def cpu_baseline(k, m, S, N_sample, seconds):
+    from oracle import rs_oracle
+
+    t = k + m
+    P = S  # host layout: contiguous shards
+    buf = np.random.default_rng(1).integers(0, 256, N_sample * t * P, dtype=np.uint8)
+    try:
+        threads = len(os.sched_getaffinity(0))
+    except AttributeError:
+        threads = os.cpu_count() or 1
+    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads))))
+    mat = rs_oracle.build_matrix(k, m)
+    surv, miss, rows = rs_oracle.decode_rows(k, m, [0, 0] + [1] * (t - 2))
+    level = 0
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        level = rs_oracle.baseline_apply_batch(k, mat[k:], list(range(k)), list(range(k, t)), buf, t * P, P, S,
+                                               N_sample, threads)
+        rs_oracle.baseline_apply_batch(k, rows, surv, miss, buf, t * P, P, S, N_sample, threads)
+        done += 1
+    dt = time.perf_counter() - t0
+    gibs = done * 2 * N_sample * k * S / dt / GiB
+    simd = {0: "scalar", 2: "avx2-vpshufb", 3: "avx512-gfni"}.get(level, str(level))
+    return {
+        "value": round(gibs, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{done} passes x (encode + 2-erasure reconstruct) of {N_sample} x {k * S // 1024} KiB "
+                  f"RS({k}+{m}) stripes, {simd}, one stripe per task, {threads} threads "
+                  f"(C restatement of klauspost's CPU kernels; Go reference absent)",
+    }
+
+
+def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    a.fill_(1)
+    for _ in range(3):
+        eng.device_copy(b, a)
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        eng.device_copy(b, a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def host_e2e(torch, eng, k, m, S, N):
+    """Pinned host -> H2D -> kernel -> D2H, encode then 1-erasure reconstruct."""
+    t = k + m
+    P = S
+    host = np.random.default_rng(2).integers(0, 256, N * t * P, dtype=np.uint8).reshape(N, t, P)
+    eng.host_register(host)
+    try:
+        eng.encode_host(host, S, P, N)
+        t0 = time.perf_counter()
+        eng.encode_host(host, S, P, N)
+        t_enc = time.perf_counter() - t0
+        mask = ((1 << t) - 1) & ~1
+        t0 = time.perf_counter()
+        eng.reconstruct_host(host, S, P, N, mask)
+        t_rec = time.perf_counter() - t0
+    finally:
+        eng.host_unregister(host)
+    return {"encode_GiBps": round(N * k * S / t_enc / GiB, 2), "reconstruct1_GiBps": round(N * k * S / t_rec / GiB, 2),
+            "bytes_user": N * k * S}
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+
+    from replication_erasurecoding_object_store_amd.batch import BatchEngine
+
+    k, m = args.k, args.m
+    S = args.stripe_kib * 1024 // k
+    N = args.stripes
+    eng = BatchEngine(k, m, torch.cuda.current_device())
+    rotate = int(args.rotate_gib * GiB)
+
+    if world > 1:
+        dist.barrier()
+    res = measure_rs(torch, eng, k, m, S, N, args.steps, args.warmup, rotate, seed=0x5EED0002 + rank)
+    dt = res["dt"]
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        okt = torch.tensor([1 if res["ok"] else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        res["ok"] = bool(okt.item())
+    user_bytes_per_step = 2 * N * k * S
+    value = world * args.steps * user_bytes_per_step / dt / GiB
+    ms_step = dt / args.steps * 1e3
+
+    km = res["kernel_ms"]
+    alg = {"encode": N * S * (k + m), "reconstruct": N * S * (k + 2)}
+    dom = max(km, key=km.get) if km else "reconstruct"
+    achieved = alg[dom] / (km.get(dom, float("nan")) * 1e-3) / 1e9 if km else None
+    traffic = None
+    pmc = pmc_traffic()
+    if pmc and pmc.get("workload") == f"rs{k}{m}_{args.stripe_kib}KiB_N{N}":
+        traffic = pmc.get("hbm_bytes_per_launch", {}).get(dom)
+
+    out = {
+        "metric": "GiB/s device-resident RS(4+2) encode + 2-erasure reconstruct, batched stripes",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: uniform random bytes (torch on-device RNG), seeded per-stripe 2-erasure patterns "
+                "(seed 0x5EED0003)",
+        "config": {
+            "workload": f"RS({k}+{m}) encode + 2-erasure reconstruct, {N} objects x {args.stripe_kib} KiB stripe "
+                        f"(S={S}) per GPU, device-resident, {res['n_batches']} rotating batches "
+                        f"({res['n_batches'] * res['batch_bytes'] / GiB:.2f} GiB)",
+            "k": k, "m": m, "shard_len": S, "stripes_per_gpu": N,
+            "parallelism": f"dp{world} (independent stripes per GPU, no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": f"apply_kernel<{k},{m}> ({dom})",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "kernel_ms": {kk: round(v, 5) for kk, v in km.items()},
+            "alg_bytes_per_launch": alg,
+        },
+        "parity_check_full_size": res["ok"],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_extras:
+        extras = {"copy_kernel_peak_GBps": round(copy_peak(torch, eng), 1)}
+        sweep = {}
+        for kk, mm in [(4, 2), (8, 4), (10, 4)]:
+            e2 = BatchEngine(kk, mm, 0)
+            SS = -(-65536 // kk)
+            NN = 16384
+            r = measure_rs(torch, e2, kk, mm, SS, NN, 10, 2, rotate, seed=0x5EED0004)
+            kms = r["kernel_ms"]
+            sweep[f"rs{kk}{mm}_64KiB"] = {
+                "shard_len": SS, "stripes": NN,
+                "encode_GiBps": round(NN * kk * SS / (kms["encode"] * 1e-3) / GiB, 1),
+                "reconstruct2_GiBps": round(NN * kk * SS / (kms["reconstruct"] * 1e-3) / GiB, 1),
+                "encode_hbm_frac": round(NN * SS * (kk + mm) / (kms["encode"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "reconstruct2_hbm_frac": round(NN * SS * (kk + 2) / (kms["reconstruct"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                               4),
+                "ok": r["ok"],
+            }
+            e2.close()
+        extras["kmsweep_64KiB_device"] = sweep
+        extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 16384)
+        out["extras"] = extras
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,139 @@
+/*
+ * rsgpu.h -- C-ABI of the MI355X Reed-Solomon engine (librsgpu.so).
+ *
+ * Drop-in boundary for the reference's codec package internal/ec
+ * (internal/ec/ec.go:15-61) behind interfaces.IEcDriver
+ * (internal/interfaces/interfaces.go:41-52).  A cgo shim keeps the
+ * Go surface NewService / Split / Encode / Reconstruct and calls these entry points;
+ * the codec arithmetic that klauspost/reedsolomon v1.12.1 did on the CPU
+ * (go.mod:16) runs in hand-written gfx950 HIP kernels.
+ *
+ * Conventions
+ *  - Plain C types only: pointers, sizes, ints.  No torch / HIP types in signatures
+ *    (streams are passed as void* = hipStream_t, NULL = the context's own stream).
+ *  - Return value: RS_OK (0) or an RS_ERR_* code; rs_strerror() gives the message.
+ *    Codes 1..7 carry klauspost's sentinel messages (errors.go) so that a Go shim
+ *    can return errors whose %v text matches the reference's.
+ *  - Thread safety: every function may be called concurrently on one context
+ *    (the reference shares one IEcDriver across all request goroutines and the
+ *    healer's workers: cmd/api/main.go:206, cmd/healer/main.go:42, poller.go:49).
+ *  - No CPU fallback: rs_create fails with RS_ERR_NO_DEVICE when no gfx950 GPU is
+ *    visible.  The library never computes parity on the host.
+ */
+#ifndef RSGPU_H
+#define RSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes ------------------------------------------------------- */
+#define RS_OK 0
+#define RS_ERR_INV_SHARD_NUM 1  /* klauspost ErrInvShardNum  */
+#define RS_ERR_MAX_SHARD_NUM 2  /* klauspost ErrMaxShardNum  */
+#define RS_ERR_TOO_FEW_SHARDS 3 /* klauspost ErrTooFewShards "too few shards given" */
+#define RS_ERR_SHARD_NO_DATA 4  /* klauspost ErrShardNoData "no shard data" */
+#define RS_ERR_SHARD_SIZE 5     /* klauspost ErrShardSize "shard sizes do not match" */
+#define RS_ERR_SHORT_DATA 6     /* klauspost ErrShortData */
+#define RS_ERR_SINGULAR 7       /* klauspost errSingular "matrix is singular" */
+#define RS_ERR_INVALID_ARG 16   /* pointer / layout contract violated */
+#define RS_ERR_NO_DEVICE 17     /* no usable GPU */
+#define RS_ERR_DEVICE 18        /* HIP runtime failure */
+#define RS_ERR_NOT_SUPPORTED 19 /* klauspost ErrNotSupported "operation not supported" */
+
+/* memory kinds for the batched entry points */
+#define RS_MEM_DEVICE 0 /* pointers are device memory; call is asynchronous on `stream` */
+#define RS_MEM_HOST 1   /* pointers are host memory (pinned or pageable); synchronous */
+
+typedef struct rs_ctx rs_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------
+ * Replaces reedsolomon.New(config.K, config.M, WithAutoGoroutines(NumCPU))
+ * at internal/ec/ec.go:26.  k >= 1, m >= 0, k+m <= 256 (klauspost limits; the GPU
+ * engine additionally needs k <= 32, m <= 16, k+m <= 32).  device = HIP ordinal.
+ */
+int rs_create(int k, int m, int device, int flags, rs_ctx **out);
+void rs_destroy(rs_ctx *ctx);
+int rs_data_shards(const rs_ctx *ctx);
+int rs_parity_shards(const rs_ctx *ctx);
+int rs_device(const rs_ctx *ctx);
+/* Description of the backend for NewService's log line (ec.go:32-41). */
+const char *rs_backend(const rs_ctx *ctx);
+const char *rs_strerror(int code);
+/* Copy the (k+m) x k encode matrix (row-major) into out. */
+int rs_encode_matrix(const rs_ctx *ctx, uint8_t *out);
+
+/* ---- per-object API, host memory (IEcDriver drop-in) --------------------
+ * Split  (ec.go:48-50): host-only, no arithmetic -> the shim keeps it in Go; this
+ *         gives perShard = ceil(len/k) (0 if len == 0 -> ErrShortData).
+ * Encode (ec.go:54-56): shards[k+m], lens[k+m]; all lens equal and nonzero, else
+ *         RS_ERR_SHARD_SIZE / RS_ERR_SHARD_NO_DATA.  Parity written in place.
+ * Reconstruct (ec.go:59-61): lens[i] == 0 marks a missing shard (Go: len==0); the
+ *         caller supplies writable storage of >= S bytes for each missing shard in
+ *         shards[i].  Every missing shard (data AND parity) is filled and its
+ *         lens[i] set to S.  Fewer than k present -> RS_ERR_TOO_FEW_SHARDS.
+ * Verify: *ok = 1 iff the parity shards match the data shards.
+ */
+size_t rs_shard_size(const rs_ctx *ctx, size_t data_len);
+int rs_encode(rs_ctx *ctx, uint8_t *const *shards, const size_t *lens);
+int rs_reconstruct(rs_ctx *ctx, uint8_t *const *shards, size_t *lens);
+int rs_reconstruct_data(rs_ctx *ctx, uint8_t *const *shards, size_t *lens);
+int rs_verify(rs_ctx *ctx, uint8_t *const *shards, const size_t *lens, int *ok);
+
+/* ---- batched API: the throughput path -----------------------------------
+ * A batch holds n_stripes independent stripes (objects).  Shard s of stripe i is
+ * at  base + i*stripe_pitch + s*shard_pitch,  shard_len (S) bytes.
+ *
+ * RS_MEM_DEVICE: shard_pitch and stripe_pitch must be multiples of 16 and
+ *   shard_pitch >= round_up(S, 16), the base 16-B aligned (the kernels read whole
+ *   16-B columns; the bytes of a slot past S may be read, never written).
+ *   The call enqueues on `stream` and returns; synchronise with hipStreamSynchronize
+ *   or rs_sync.
+ * RS_MEM_HOST: any pitches; the engine stages through pinned buffers with
+ *   H2D / kernel / D2H overlapped on several streams, and returns when the
+ *   outputs are in host memory.
+ *
+ * rs_encode_batch: reads data shards 0..k-1 of each stripe from `data`
+ *   (data_stripe_pitch), writes parity 0..m-1 into `parity` (parity_stripe_pitch).
+ *   For the unified K+M-slot layout pass parity = data + k*shard_pitch and equal
+ *   stripe pitches.
+ * rs_reconstruct_batch: unified layout (k+m slots per stripe), in place.
+ *   present_masks: host array of n_masks uint32 (bit s set = shard s present);
+ *   n_masks == 1 applies one pattern to every stripe, n_masks == n_stripes gives a
+ *   pattern per stripe.  Missing shards (data and parity) are written.  Any mask
+ *   with < k present -> RS_ERR_TOO_FEW_SHARDS and nothing is modified.
+ */
+int rs_encode_batch(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch, uint8_t *parity,
+                    size_t parity_stripe_pitch, size_t shard_pitch, size_t shard_len,
+                    size_t n_stripes, int mem, void *stream);
+int rs_reconstruct_batch(rs_ctx *ctx, uint8_t *shards, size_t stripe_pitch, size_t shard_pitch,
+                         size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
+                         size_t n_masks, int mem, void *stream);
+/* Device-resident masks (RS_MEM_DEVICE only, k+m <= 16): present_masks_dev is a
+ * device array of n_stripes uint32.  Stripes with < k present are skipped and
+ * reported by the next rs_sync on that stream as RS_ERR_TOO_FEW_SHARDS. */
+int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *shards, size_t stripe_pitch,
+                                 size_t shard_pitch, size_t shard_len, size_t n_stripes,
+                                 const uint32_t *present_masks_dev, void *stream);
+/* Wait for `stream` and return any deferred device-side error. */
+int rs_sync(rs_ctx *ctx, void *stream);
+
+/* ---- host memory helpers ------------------------------------------------ */
+int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin for async DMA */
+int rs_host_unregister(rs_ctx *ctx, void *ptr);
+
+/* ---- measurement helpers (bench.py) ------------------------------------- */
+/* Name of the kernel the last batched call on this context launched. */
+const char *rs_last_kernel(const rs_ctx *ctx);
+/* Streaming device copy, the measured HBM ceiling beside the RS kernels. */
+int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
+/* Tuning knob: workgroups per CU for the batched kernels (0 = default). */
+int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSGPU_H */

@@ -1,0 +1,91 @@
+/*
+ * rs_oracle.h -- CPU restatement of the reference's Reed-Solomon path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the HIP engine in
+ * replication_erasurecoding_object_store_amd/.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product library (librsgpu.so)
+ * never links, loads or calls anything in oracle/.
+ *
+ * What it restates: the reference's codec path internal/ec/ec.go:21-61, which
+ * wraps github.com/klauspost/reedsolomon v1.12.1 (go.mod:16, go.sum:81-82).  That
+ * module is NOT vendored under /root/reference, so the arithmetic below follows
+ * the library's published algorithm (galois.go, matrix.go, reedsolomon.go,
+ * errors.go) and is pinned on its published known-answer tests (galois_test.go,
+ * reedsolomon_test.go TestOneEncode) -- see tests/test_oracle.py.
+ */
+#ifndef RS_ORACLE_H
+#define RS_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Error codes: same meaning/messages as klauspost's sentinels (errors.go). */
+enum {
+    RSO_OK = 0,
+    RSO_ERR_INV_SHARD_NUM = 1,  /* "cannot create Encoder with less than one data shard or less than zero parity shards" */
+    RSO_ERR_MAX_SHARD_NUM = 2,  /* "cannot create Encoder with more than 256 data+parity shards" */
+    RSO_ERR_TOO_FEW_SHARDS = 3, /* "too few shards given" */
+    RSO_ERR_SHARD_NO_DATA = 4,  /* "no shard data" */
+    RSO_ERR_SHARD_SIZE = 5,     /* "shard sizes do not match" */
+    RSO_ERR_SHORT_DATA = 6,     /* "not enough data to fill the number of requested shards" */
+    RSO_ERR_SINGULAR = 7        /* "matrix is singular" */
+};
+
+/* GF(2^8), poly 0x11d, generator 2 [upstream galois.go]. */
+uint8_t rso_gf_mul(uint8_t a, uint8_t b);
+uint8_t rso_gf_exp(uint8_t a, int n);
+uint8_t rso_gf_inv(uint8_t a);
+
+/* Encode matrix = vandermonde(K+M, K) * inv(top K x K) [upstream matrix.go buildMatrix].
+ * out: (k+m) x k bytes, row-major.  Returns RSO_* code. */
+int rso_build_matrix(int k, int m, uint8_t *out);
+
+/* Gauss-Jordan inverse of an n x n matrix over GF(2^8) [upstream matrix.go Invert]. */
+int rso_invert(int n, const uint8_t *in, uint8_t *out);
+
+/* Split: per-shard size ceil(len/k) [upstream reedsolomon.go Split]. 0 if len == 0. */
+size_t rso_shard_size(int k, size_t len);
+
+/* Encode: parity[p][b] = XOR_c mul(P[p][c], data[c][b])  [upstream Encode/codeSomeShards].
+ * shards: k+m pointers, lens: per-shard lengths (0 == nil).  Writes parity in place. */
+int rso_encode(int k, int m, uint8_t *const *shards, const size_t *lens);
+
+/* Reconstruct: fills every shard with lens[i]==0, two-phase like upstream
+ * reconstruct(shards, dataOnly=false, required=nil).  The caller provides
+ * storage of size S for missing shards (shards[i] != NULL); lens[i] is updated
+ * to S for every filled shard. */
+int rso_reconstruct(int k, int m, uint8_t *const *shards, size_t *lens);
+
+/* Verify: recompute parity and compare [upstream Verify]. *ok = 1 if consistent. */
+int rso_verify(int k, int m, uint8_t *const *shards, const size_t *lens, int *ok);
+
+/* Composed reconstruct coefficients: for the present mask (k+m bytes, 1=present),
+ * pick the first k present shards in index order (survivors, k entries) and the
+ * missing indices (n_missing entries, data then parity, in index order), and the
+ * n_missing x k matrix that maps survivors straight to each missing shard. */
+int rso_decode_rows(int k, int m, const uint8_t *present, int *survivors,
+                    int *missing, int *n_missing, uint8_t *rows);
+
+/* Batched layout helpers (test/baseline only).  Stripe i's shard c lives at
+ * base + i*stripe_pitch + c*shard_pitch, S bytes.  Encode reads shards 0..k-1
+ * and writes k..k+m-1 of each stripe; single-threaded scalar. */
+void rso_encode_batch_scalar(int k, int m, uint8_t *base, size_t stripe_pitch,
+                             size_t shard_pitch, size_t S, size_t N);
+
+/* CPU baseline (rs_cpu_baseline.c): SIMD split-nibble (AVX2 VPSHUFB, the same
+ * algorithm class as klauspost's amd64 galMulAVX2 kernels), one stripe per task,
+ * `threads` worker threads.  Layout as above; rows = e x k coefficient matrix,
+ * in_idx = k input shard indices, out_idx = e output shard indices (the same for
+ * every stripe).  Returns the SIMD level used: 0 scalar, 2 avx2, 3 gfni. */
+int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_idx,
+                             const int *out_idx, uint8_t *base, size_t stripe_pitch,
+                             size_t shard_pitch, size_t S, size_t N, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

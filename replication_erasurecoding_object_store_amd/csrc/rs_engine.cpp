@@ -1,0 +1,854 @@
+// rs_engine.cpp -- librsgpu.so: the C-ABI in include/rsgpu.h.
+//
+// Host runtime around the gfx950 kernels in rs_kernels.hip:
+//   * encode matrix and per-erasure-pattern decode plans (the analogue of
+//     klauspost's inversion_tree.go cache, [upstream reedsolomon.go reconstruct]),
+//     built once per pattern and kept resident in HBM;
+//   * for k+m <= 16 every pattern with 1..m erasures is precomputed at rs_create and
+//     indexed by a dense missing-mask -> plan LUT, so a batch may carry a different
+//     erasure pattern per stripe with no host work per stripe;
+//   * per-object host calls (the IEcDriver drop-in: ec.go:54-61) run on a pool of
+//     "lanes" (stream + pinned staging + device buffers) so concurrent goroutines do
+//     not serialise on one stream;
+//   * host-resident batches are pipelined H2D -> kernel -> D2H over 3 streams.
+// No CPU arithmetic path exists: every parity / reconstructed byte comes from a
+// HIP kernel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "gf256.hpp"
+#include "rs_plan.hpp"
+
+namespace {
+
+using rs::Matrix;
+
+#define RS_HIP(expr)                                    \
+  do {                                                  \
+    if ((expr) != hipSuccess) return RS_ERR_DEVICE;     \
+  } while (0)
+
+size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// ---- plan construction -----------------------------------------------------
+// 3-chunk v_perm tables for coefficient f (see rs_kernels.hip):
+//   A[v] = f*v (v<8), B[v] = f*(v<<3) (v<8), C[v] = f*(v<<6) (v<4).
+void perm_tables(uint8_t f, uint32_t* t) {
+  const rs::Field& F = rs::field();
+  auto pack4 = [&](int base, int shift) {
+    uint32_t w = 0;
+    for (int j = 0; j < 4; ++j) w |= static_cast<uint32_t>(F.mul(f, static_cast<uint8_t>((base + j) << shift))) << (8 * j);
+    return w;
+  };
+  t[0] = pack4(0, 0);
+  t[1] = pack4(4, 0);
+  t[2] = pack4(0, 3);
+  t[3] = pack4(4, 3);
+  t[4] = pack4(0, 6);
+}
+
+// rows: n_out x k coefficient matrix (row-major).
+std::vector<uint8_t> make_plan(int k, int m, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+                               const std::vector<uint8_t>& rows) {
+  std::vector<uint8_t> p(rs::plan_stride(k, m), 0);
+  const uint32_t n_out = static_cast<uint32_t>(out_idx.size());
+  std::memcpy(p.data(), &n_out, 4);
+  uint32_t* ii = reinterpret_cast<uint32_t*>(p.data() + 8);
+  for (int c = 0; c < k; ++c) ii[c] = static_cast<uint32_t>(in_idx[c]);
+  for (size_t r = 0; r < out_idx.size(); ++r) ii[k + r] = static_cast<uint32_t>(out_idx[r]);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
+  for (size_t r = 0; r < out_idx.size(); ++r)
+    for (int c = 0; c < k; ++c) perm_tables(rows[r * k + c], tab + (r * k + c) * 5);
+  return p;
+}
+
+// Composed reconstruct plan for a present-shard mask over k+m shards.
+// Survivors = first k present shards in index order [upstream reconstruct];
+// a missing data shard d is row d of inv(sub) (phase 1); a missing parity shard p
+// is P[p] x inv(sub) (phase 2 over the recovered data, folded into one pass).
+int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool data_only,
+                     std::vector<uint8_t>* out) {
+  const rs::Field& F = rs::field();
+  const int t = k + m;
+  std::vector<int> surv, miss;
+  for (int i = 0; i < t; ++i) {
+    if ((present >> i) & 1u) {
+      if (static_cast<int>(surv.size()) < k) surv.push_back(i);
+    } else if (!data_only || i < k) {
+      miss.push_back(i);
+    }
+  }
+  if (static_cast<int>(surv.size()) < k) return RS_ERR_TOO_FEW_SHARDS;
+  Matrix sub(k, k), dec;
+  for (int r = 0; r < k; ++r)
+    for (int c = 0; c < k; ++c) sub.at(r, c) = enc.at(surv[r], c);
+  if (!rs::invert(sub, &dec)) return RS_ERR_SINGULAR;
+  std::vector<uint8_t> rows(miss.size() * k);
+  for (size_t r = 0; r < miss.size(); ++r) {
+    const int s = miss[r];
+    for (int c = 0; c < k; ++c) {
+      uint8_t v;
+      if (s < k) {
+        v = dec.at(s, c);
+      } else {
+        v = 0;
+        for (int d = 0; d < k; ++d) v ^= F.mul(enc.at(s, d), dec.at(d, c));
+      }
+      rows[r * k + c] = v;
+    }
+  }
+  *out = make_plan(k, m, surv, miss, rows);
+  return RS_OK;
+}
+
+// ---- per-call resources ------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= n) return RS_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return RS_ERR_DEVICE;
+    n = bytes;
+    return RS_OK;
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= n) return RS_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return RS_ERR_DEVICE;
+    n = bytes;
+    return RS_OK;
+  }
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+// A lane serves one synchronous host call at a time.
+struct Lane {
+  hipStream_t stream = nullptr;
+  DevBuf dev;
+  PinnedBuf host;
+};
+
+// Upload slot for per-stripe masks passed in host memory (async device calls).
+struct UploadSlot {
+  PinnedBuf host;
+  DevBuf dev;
+  hipEvent_t done = nullptr;
+  bool used = false;
+};
+
+}  // namespace
+
+struct rs_ctx {
+  int k = 0, m = 0, device = 0, cu_count = 0;
+  int blocks_per_cu_override = 0;
+  bool force_generic = false;
+  std::string backend;
+  Matrix enc;
+  hipStream_t stream = nullptr;  // default stream for device calls with stream == NULL
+
+  // encode plan (device, uniform)
+  DevBuf d_enc_plan;
+  // eager all-pattern plans + LUT (k+m <= 16)
+  DevBuf d_plans, d_lut;
+  uint32_t n_plans = 0;
+  std::vector<uint16_t> h_lut;          // missing mask -> plan index
+  bool have_lut = false;
+  // uniform-pattern plans built on demand (k+m > 16), keyed by (present, data_only)
+  std::mutex plan_mu;
+  std::unordered_map<uint64_t, std::unique_ptr<DevBuf>> plan_cache;
+
+  // device status word for devmask calls
+  DevBuf d_status;
+  PinnedBuf h_status;
+
+  // lanes for synchronous host calls
+  std::mutex lane_mu;
+  std::condition_variable lane_cv;
+  std::vector<std::unique_ptr<Lane>> lanes;
+  std::vector<Lane*> free_lanes;
+  int max_lanes = 8;
+
+  std::mutex upload_mu;
+  std::vector<UploadSlot> uploads;
+  size_t upload_next = 0;
+
+  std::atomic<const char*> last_kernel{"none"};
+
+  ~rs_ctx() {
+    for (auto& s : uploads)
+      if (s.done) (void)hipEventDestroy(s.done);
+    for (auto& l : lanes)
+      if (l->stream) (void)hipStreamDestroy(l->stream);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+uint32_t grid_for(rs_ctx* c, uint64_t ntasks, bool per_stripe) {
+  const int bpc = c->blocks_per_cu_override > 0 ? c->blocks_per_cu_override
+                                                : rs::apply_kernel_max_blocks_per_cu(c->k, c->m, per_stripe);
+  const uint64_t cap = static_cast<uint64_t>(c->cu_count) * static_cast<uint64_t>(bpc);
+  const uint64_t need = (ntasks + 3) / 4;  // 4 waves per 256-thread block, one task per wave
+  return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(cap, need)));
+}
+
+rs::KernelArgs base_args(rs_ctx* c, size_t S, size_t N) {
+  rs::KernelArgs a{};
+  a.shard_len = static_cast<uint32_t>(S);
+  a.n_stripes = static_cast<uint32_t>(N);
+  a.blocks_per_stripe = static_cast<uint32_t>((round_up(S, 16) / 16 + 63) / 64);
+  a.k = c->k;
+  a.m = c->m;
+  a.full_mask = (c->k + c->m >= 32) ? 0xFFFFFFFFu : ((1u << (c->k + c->m)) - 1u);
+  a.plan_bytes = rs::plan_stride(c->k, c->m);
+  return a;
+}
+
+int launch(rs_ctx* c, const rs::KernelArgs& a, bool per_stripe, hipStream_t s) {
+  if (a.n_stripes == 0 || a.shard_len == 0) return RS_OK;
+  const uint64_t ntasks = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  const char* name = rs::launch_apply(a, per_stripe, grid_for(c, ntasks, per_stripe), s, c->force_generic);
+  c->last_kernel.store(name);
+  RS_HIP(hipGetLastError());
+  return RS_OK;
+}
+
+// Device pointer of the uniform plan for `present` (k+m <= 16: the eager table).
+int uniform_plan(rs_ctx* c, uint64_t present, bool data_only, const uint8_t** plan_dev) {
+  const int t = c->k + c->m;
+  if (__builtin_popcountll(present) < c->k) return RS_ERR_TOO_FEW_SHARDS;
+  const uint64_t full = (t >= 64) ? ~0ull : ((1ull << t) - 1);
+  if (c->have_lut && !data_only) {
+    const uint32_t missing = static_cast<uint32_t>(~present & full);
+    const uint16_t pid = c->h_lut[missing];
+    if (pid == rs::kPlanInvalid) return RS_ERR_TOO_FEW_SHARDS;
+    *plan_dev = static_cast<const uint8_t*>(c->d_plans.p) + static_cast<size_t>(pid) * rs::plan_stride(c->k, c->m);
+    return RS_OK;
+  }
+  const uint64_t key = (present & full) | (data_only ? (1ull << 63) : 0ull);
+  std::lock_guard<std::mutex> g(c->plan_mu);
+  auto it = c->plan_cache.find(key);
+  if (it == c->plan_cache.end()) {
+    std::vector<uint8_t> plan;
+    int rc = make_decode_plan(c->k, c->m, c->enc, present, data_only, &plan);
+    if (rc) return rc;
+    auto buf = std::make_unique<DevBuf>();
+    if (buf->ensure(plan.size())) return RS_ERR_DEVICE;
+    RS_HIP(hipMemcpy(buf->p, plan.data(), plan.size(), hipMemcpyHostToDevice));
+    it = c->plan_cache.emplace(key, std::move(buf)).first;
+  }
+  *plan_dev = static_cast<const uint8_t*>(it->second->p);
+  return RS_OK;
+}
+
+// RAII lane checkout.
+struct LaneGuard {
+  rs_ctx* c;
+  Lane* lane = nullptr;
+  int rc = RS_OK;
+  explicit LaneGuard(rs_ctx* ctx) : c(ctx) {
+    std::unique_lock<std::mutex> g(c->lane_mu);
+    if (c->free_lanes.empty() && static_cast<int>(c->lanes.size()) < c->max_lanes) {
+      auto l = std::make_unique<Lane>();
+      if (hipSetDevice(c->device) != hipSuccess ||
+          hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) {
+        rc = RS_ERR_DEVICE;
+        return;
+      }
+      c->free_lanes.push_back(l.get());
+      c->lanes.push_back(std::move(l));
+    }
+    c->lane_cv.wait(g, [&] { return !c->free_lanes.empty(); });
+    lane = c->free_lanes.back();
+    c->free_lanes.pop_back();
+  }
+  ~LaneGuard() {
+    if (!lane) return;
+    std::lock_guard<std::mutex> g(c->lane_mu);
+    c->free_lanes.push_back(lane);
+    c->lane_cv.notify_one();
+  }
+};
+
+// [upstream reedsolomon.go checkShards(shards, nilok)] + shardSize.
+int check_shards(int n, const size_t* lens, bool nilok, size_t* S) {
+  size_t s = 0;
+  for (int i = 0; i < n; ++i)
+    if (lens[i]) {
+      s = lens[i];
+      break;
+    }
+  if (s == 0) return RS_ERR_SHARD_NO_DATA;
+  for (int i = 0; i < n; ++i)
+    if (lens[i] != s && (lens[i] != 0 || !nilok)) return RS_ERR_SHARD_SIZE;
+  *S = s;
+  return RS_OK;
+}
+
+// One object through a lane: pack inputs into pinned staging, H2D, one kernel,
+// D2H of the outputs, unpack.  in/out slots are shard indices into `shards`.
+int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+               uint8_t* const* shards, size_t S) {
+  LaneGuard lg(c);
+  if (lg.rc) return lg.rc;
+  Lane* L = lg.lane;
+  const int t = c->k + c->m;
+  const size_t P = round_up(S, 64);
+  const size_t bytes = P * static_cast<size_t>(t);
+  if (L->dev.ensure(bytes) || L->host.ensure(bytes)) return RS_ERR_DEVICE;
+  uint8_t* h = static_cast<uint8_t*>(L->host.p);
+  uint8_t* d = static_cast<uint8_t*>(L->dev.p);
+  // inputs: copy each used slot (pad bytes of the slot are never written back)
+  for (int s : in_idx) std::memcpy(h + static_cast<size_t>(s) * P, shards[s], S);
+  // contiguous H2D of the slots that carry inputs
+  int lo = *std::min_element(in_idx.begin(), in_idx.end());
+  int hi = *std::max_element(in_idx.begin(), in_idx.end());
+  RS_HIP(hipMemcpyAsync(d + lo * P, h + lo * P, (hi - lo + 1) * P, hipMemcpyHostToDevice, L->stream));
+  rs::KernelArgs a = base_args(c, S, 1);
+  a.in = d;
+  a.out = d;
+  a.in_stripe_pitch = a.out_stripe_pitch = bytes;
+  a.shard_pitch = P;
+  a.plans = plan_dev;
+  int rc = launch(c, a, false, L->stream);
+  if (rc) return rc;
+  for (int s : out_idx)
+    RS_HIP(hipMemcpyAsync(h + static_cast<size_t>(s) * P, d + static_cast<size_t>(s) * P, S, hipMemcpyDeviceToHost,
+                          L->stream));
+  RS_HIP(hipStreamSynchronize(L->stream));
+  for (int s : out_idx) std::memcpy(shards[s], h + static_cast<size_t>(s) * P, S);
+  return RS_OK;
+}
+
+int reconstruct_impl(rs_ctx* c, uint8_t* const* shards, size_t* lens, bool data_only) {
+  if (!c || !shards || !lens) return RS_ERR_INVALID_ARG;
+  const int t = c->k + c->m;
+  size_t S = 0;
+  int rc = check_shards(t, lens, true, &S);
+  if (rc) return rc;
+  uint64_t present = 0;
+  int np = 0, data_present = 0;
+  for (int i = 0; i < t; ++i)
+    if (lens[i]) {
+      present |= 1ull << i;
+      ++np;
+      if (i < c->k) ++data_present;
+    }
+  if (np == t || (data_only && data_present == c->k)) return RS_OK;
+  if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
+  std::vector<int> surv, miss;
+  for (int i = 0; i < t; ++i) {
+    if (lens[i]) {
+      if (static_cast<int>(surv.size()) < c->k) surv.push_back(i);
+    } else if (!data_only || i < c->k) {
+      if (!shards[i]) return RS_ERR_INVALID_ARG;
+      miss.push_back(i);
+    }
+  }
+  const uint8_t* plan = nullptr;
+  rc = uniform_plan(c, present, data_only, &plan);
+  if (rc) return rc;
+  rc = run_object(c, plan, surv, miss, shards, S);
+  if (rc) return rc;
+  for (int s : miss) lens[s] = S;
+  return RS_OK;
+}
+
+hipStream_t pick_stream(rs_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+
+bool device_layout_ok(const void* base, size_t stripe_pitch, size_t shard_pitch, size_t S) {
+  return (reinterpret_cast<uintptr_t>(base) % 16 == 0) && stripe_pitch % 16 == 0 && shard_pitch % 16 == 0 &&
+         shard_pitch >= round_up(S, 16);
+}
+
+// ---- host batch pipeline -------------------------------------------------------
+// Chunks of stripes flow H2D -> kernel -> D2H on kStreams streams; each stream has
+// its own device slab, so chunk j+1's copy overlaps chunk j's kernel and D2H.
+constexpr int kStreams = 3;
+
+struct HostPipe {
+  hipStream_t st[kStreams] = {};
+  DevBuf buf[kStreams];
+  ~HostPipe() {
+    for (auto& s : st)
+      if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+// Copies `rows` rows of `width` bytes with independent pitches.
+hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                  hipMemcpyKind kind, hipStream_t s) {
+  if (rows == 0 || width == 0) return hipSuccess;
+  return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
+}
+
+// Host-resident batch: for each chunk, copy the in-slots of every stripe (H2D),
+// run the kernel, copy the out-slots back (D2H).
+int host_batch(rs_ctx* c, const uint8_t* in_host, size_t in_sp, const std::vector<int>& in_slots, uint8_t* out_host,
+               size_t out_sp, const std::vector<int>& out_slots, size_t shard_pitch, size_t S, size_t N,
+               const uint8_t* plan_dev, const uint32_t* masks_host /* per-stripe or null */) {
+  const int t = c->k + c->m;
+  const size_t P = round_up(S, 64);
+  const size_t dev_stripe = P * static_cast<size_t>(t);
+  const size_t target = size_t(64) << 20;
+  size_t chunk = std::max<size_t>(1, target / dev_stripe);
+  chunk = std::min(chunk, N);
+  HostPipe pipe;
+  for (int i = 0; i < kStreams; ++i) {
+    RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
+    if (pipe.buf[i].ensure(chunk * dev_stripe + (masks_host ? chunk * 4 + 256 : 0))) return RS_ERR_DEVICE;
+  }
+  rs::KernelArgs a = base_args(c, S, 0);
+  a.in_stripe_pitch = a.out_stripe_pitch = dev_stripe;
+  a.shard_pitch = P;
+  a.plans = plan_dev;
+  if (masks_host) {
+    a.lut = static_cast<const uint16_t*>(c->d_lut.p);
+    a.status = static_cast<uint32_t*>(c->d_status.p);
+  }
+  int j = 0;
+  for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
+    const size_t n = std::min(chunk, N - s0);
+    hipStream_t st = pipe.st[j % kStreams];
+    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kStreams].p);
+    // H2D: slot s of stripes [s0, s0+n): rows of S bytes, pitch in_sp -> dev_stripe
+    for (int slot : in_slots)
+      RS_HIP(copy2d(d + static_cast<size_t>(slot) * P, dev_stripe, in_host + s0 * in_sp + slot * shard_pitch, in_sp, S,
+                    n, hipMemcpyHostToDevice, st));
+    rs::KernelArgs aa = a;
+    aa.in = d;
+    aa.out = d;
+    aa.n_stripes = static_cast<uint32_t>(n);
+    if (masks_host) {
+      uint32_t* dm = reinterpret_cast<uint32_t*>(d + round_up(chunk * dev_stripe, 256));
+      RS_HIP(hipMemcpyAsync(dm, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
+      aa.present_masks = dm;
+    }
+    int rc = launch(c, aa, masks_host != nullptr, st);
+    if (rc) return rc;
+    for (int slot : out_slots)
+      RS_HIP(copy2d(out_host + s0 * out_sp + slot * shard_pitch, out_sp, d + static_cast<size_t>(slot) * P, dev_stripe, S,
+                    n, hipMemcpyDeviceToHost, st));
+  }
+  for (int i = 0; i < kStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
+  return RS_OK;
+}
+
+int upload_masks(rs_ctx* c, const uint32_t* masks, size_t n, hipStream_t s, const uint32_t** dev) {
+  std::lock_guard<std::mutex> g(c->upload_mu);
+  if (c->uploads.empty()) c->uploads.resize(4);
+  UploadSlot& u = c->uploads[c->upload_next++ % c->uploads.size()];
+  if (!u.done) RS_HIP(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
+  if (u.used) RS_HIP(hipEventSynchronize(u.done));
+  if (u.host.ensure(n * 4) || u.dev.ensure(n * 4)) return RS_ERR_DEVICE;
+  std::memcpy(u.host.p, masks, n * 4);
+  RS_HIP(hipMemcpyAsync(u.dev.p, u.host.p, n * 4, hipMemcpyHostToDevice, s));
+  RS_HIP(hipEventRecord(u.done, s));
+  u.used = true;
+  *dev = static_cast<const uint32_t*>(u.dev.p);
+  return RS_OK;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+const char* rs_strerror(int code) {
+  switch (code) {
+    case RS_OK: return "ok";
+    case RS_ERR_INV_SHARD_NUM:
+      return "cannot create Encoder with less than one data shard or less than zero parity shards";
+    case RS_ERR_MAX_SHARD_NUM: return "cannot create Encoder with more than 256 data+parity shards";
+    case RS_ERR_TOO_FEW_SHARDS: return "too few shards given";
+    case RS_ERR_SHARD_NO_DATA: return "no shard data";
+    case RS_ERR_SHARD_SIZE: return "shard sizes do not match";
+    case RS_ERR_SHORT_DATA: return "not enough data to fill the number of requested shards";
+    case RS_ERR_SINGULAR: return "matrix is singular";
+    case RS_ERR_INVALID_ARG: return "rsgpu: invalid argument or layout";
+    case RS_ERR_NO_DEVICE: return "rsgpu: no usable GPU device";
+    case RS_ERR_DEVICE: return "rsgpu: HIP runtime error";
+    case RS_ERR_NOT_SUPPORTED: return "operation not supported";
+    default: return "rsgpu: unknown error";
+  }
+}
+
+int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
+  (void)flags;
+  if (!out) return RS_ERR_INVALID_ARG;
+  *out = nullptr;
+  // [upstream reedsolomon.go New] argument checks, same order and sentinels.
+  if (k <= 0 || m < 0) return RS_ERR_INV_SHARD_NUM;
+  if (k + m > 256) return RS_ERR_MAX_SHARD_NUM;
+  if (k > rs::kMaxK || m > rs::kMaxM || k + m > 32) return RS_ERR_NOT_SUPPORTED;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RS_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return RS_ERR_NO_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return RS_ERR_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RS_ERR_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RS_ERR_NO_DEVICE;
+
+  auto c = std::make_unique<rs_ctx>();
+  c->k = k;
+  c->m = m;
+  c->device = device;
+  c->cu_count = prop.multiProcessorCount;
+  c->enc = rs::build_encode_matrix(k, m);
+  if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = std::atoi(e);
+  if (const char* e = std::getenv("RSGPU_FORCE_GENERIC")) c->force_generic = std::atoi(e) != 0;
+  char name[160];
+  std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
+  c->backend = name;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return RS_ERR_DEVICE;
+
+  // encode plan: in = data 0..k-1, out = parity slots k..k+m-1 (unified layout);
+  // rs_encode_batch remaps outputs for a separate parity buffer via out_idx - k.
+  {
+    std::vector<int> in_idx(k), out_idx(m);
+    for (int i = 0; i < k; ++i) in_idx[i] = i;
+    for (int p = 0; p < m; ++p) out_idx[p] = k + p;
+    std::vector<uint8_t> rows(static_cast<size_t>(m) * k);
+    for (int p = 0; p < m; ++p)
+      for (int i = 0; i < k; ++i) rows[p * k + i] = c->enc.at(k + p, i);
+    // two encode plans back to back: [0] unified (out slots k..), [1] separate parity buffer (out slots 0..)
+    std::vector<uint8_t> p0 = make_plan(k, m, in_idx, out_idx, rows);
+    for (int p = 0; p < m; ++p) out_idx[p] = p;
+    std::vector<uint8_t> p1 = make_plan(k, m, in_idx, out_idx, rows);
+    p0.insert(p0.end(), p1.begin(), p1.end());
+    if (c->d_enc_plan.ensure(p0.size())) return RS_ERR_DEVICE;
+    if (hipMemcpy(c->d_enc_plan.p, p0.data(), p0.size(), hipMemcpyHostToDevice) != hipSuccess) return RS_ERR_DEVICE;
+  }
+  // eager all-pattern plans + LUT for k+m <= 16
+  const int t = k + m;
+  if (t <= 16 && m > 0) {
+    const uint32_t full = (1u << t) - 1u;
+    c->h_lut.assign(size_t(1) << t, static_cast<uint16_t>(rs::kPlanInvalid));
+    std::vector<uint8_t> all;
+    uint32_t count = 0;
+    // plan 0: no missing shard (n_out = 0)
+    {
+      std::vector<int> in_idx(k), none;
+      for (int i = 0; i < k; ++i) in_idx[i] = i;
+      std::vector<uint8_t> p = make_plan(k, m, in_idx, none, {});
+      all.insert(all.end(), p.begin(), p.end());
+      c->h_lut[0] = 0;
+      count = 1;
+    }
+    bool ok = true;
+    for (uint32_t missing = 1; missing <= full && ok; ++missing) {
+      if (__builtin_popcount(missing) > m) continue;
+      std::vector<uint8_t> p;
+      if (make_decode_plan(k, m, c->enc, full & ~missing, false, &p) != RS_OK) continue;
+      if (count >= 0xFFFE || all.size() > (size_t(64) << 20)) {
+        ok = false;
+        break;
+      }
+      all.insert(all.end(), p.begin(), p.end());
+      c->h_lut[missing] = static_cast<uint16_t>(count++);
+    }
+    if (ok) {
+      if (c->d_plans.ensure(all.size()) || c->d_lut.ensure(c->h_lut.size() * 2)) return RS_ERR_DEVICE;
+      if (hipMemcpy(c->d_plans.p, all.data(), all.size(), hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(c->d_lut.p, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+        return RS_ERR_DEVICE;
+      c->n_plans = count;
+      c->have_lut = true;
+    }
+  }
+  if (c->d_status.ensure(256) || c->h_status.ensure(256)) return RS_ERR_DEVICE;
+  if (hipMemset(c->d_status.p, 0, 256) != hipSuccess) return RS_ERR_DEVICE;
+  *out = c.release();
+  return RS_OK;
+}
+
+void rs_destroy(rs_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ctx;
+}
+
+int rs_data_shards(const rs_ctx* c) { return c ? c->k : 0; }
+int rs_parity_shards(const rs_ctx* c) { return c ? c->m : 0; }
+int rs_device(const rs_ctx* c) { return c ? c->device : -1; }
+const char* rs_backend(const rs_ctx* c) { return c ? c->backend.c_str() : "none"; }
+const char* rs_last_kernel(const rs_ctx* c) { return c ? c->last_kernel.load() : "none"; }
+
+int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
+  if (!c || !out) return RS_ERR_INVALID_ARG;
+  std::memcpy(out, c->enc.a.data(), c->enc.a.size());
+  return RS_OK;
+}
+
+size_t rs_shard_size(const rs_ctx* c, size_t len) {
+  if (!c || len == 0) return 0;
+  return (len + static_cast<size_t>(c->k) - 1) / static_cast<size_t>(c->k);
+}
+
+int rs_encode(rs_ctx* c, uint8_t* const* shards, const size_t* lens) {
+  if (!c || !shards || !lens) return RS_ERR_INVALID_ARG;
+  size_t S = 0;
+  int rc = check_shards(c->k + c->m, lens, false, &S);
+  if (rc) return rc;
+  if (c->m == 0) return RS_OK;
+  for (int i = 0; i < c->k + c->m; ++i)
+    if (!shards[i]) return RS_ERR_INVALID_ARG;
+  std::vector<int> in_idx(c->k), out_idx(c->m);
+  for (int i = 0; i < c->k; ++i) in_idx[i] = i;
+  for (int p = 0; p < c->m; ++p) out_idx[p] = c->k + p;
+  return run_object(c, static_cast<const uint8_t*>(c->d_enc_plan.p), in_idx, out_idx, shards, S);
+}
+
+int rs_reconstruct(rs_ctx* c, uint8_t* const* shards, size_t* lens) { return reconstruct_impl(c, shards, lens, false); }
+int rs_reconstruct_data(rs_ctx* c, uint8_t* const* shards, size_t* lens) {
+  return reconstruct_impl(c, shards, lens, true);
+}
+
+// [upstream reedsolomon.go Verify]: recompute parity on the GPU into scratch and
+// compare on the host against the caller's parity shards.
+int rs_verify(rs_ctx* c, uint8_t* const* shards, const size_t* lens, int* ok) {
+  if (!c || !shards || !lens || !ok) return RS_ERR_INVALID_ARG;
+  size_t S = 0;
+  int rc = check_shards(c->k + c->m, lens, false, &S);
+  if (rc) return rc;
+  *ok = 1;
+  if (c->m == 0) return RS_OK;
+  std::vector<std::vector<uint8_t>> tmp(c->m, std::vector<uint8_t>(S));
+  std::vector<uint8_t*> view(shards, shards + c->k + c->m);
+  for (int p = 0; p < c->m; ++p) view[c->k + p] = tmp[p].data();
+  std::vector<int> in_idx(c->k), out_idx(c->m);
+  for (int i = 0; i < c->k; ++i) in_idx[i] = i;
+  for (int p = 0; p < c->m; ++p) out_idx[p] = c->k + p;
+  rc = run_object(c, static_cast<const uint8_t*>(c->d_enc_plan.p), in_idx, out_idx, view.data(), S);
+  if (rc) return rc;
+  for (int p = 0; p < c->m; ++p)
+    if (std::memcmp(tmp[p].data(), shards[c->k + p], S) != 0) *ok = 0;
+  return RS_OK;
+}
+
+int rs_encode_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
+                    size_t shard_pitch, size_t S, size_t N, int mem, void* stream) {
+  if (!c || !data || !parity) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || shard_pitch < S) return RS_ERR_INVALID_ARG;
+  if (c->m == 0) return RS_OK;
+  (void)hipSetDevice(c->device);
+  const uint8_t* plan_sep = static_cast<const uint8_t*>(c->d_enc_plan.p) + rs::plan_stride(c->k, c->m);
+  if (mem == RS_MEM_DEVICE) {
+    if (!device_layout_ok(data, data_sp, shard_pitch, S) || !device_layout_ok(parity, parity_sp, shard_pitch, S))
+      return RS_ERR_INVALID_ARG;
+    rs::KernelArgs a = base_args(c, S, N);
+    a.in = data;
+    a.out = parity;
+    a.in_stripe_pitch = data_sp;
+    a.out_stripe_pitch = parity_sp;
+    a.shard_pitch = shard_pitch;
+    a.plans = plan_sep;
+    return launch(c, a, false, pick_stream(c, stream));
+  }
+  if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
+  // host: stage data slots 0..k-1 in, parity slots k..k+m-1 out (unified device slab)
+  std::vector<int> in_slots(c->k), out_slots;
+  for (int i = 0; i < c->k; ++i) in_slots[i] = i;
+  const uint8_t* plan_uni = static_cast<const uint8_t*>(c->d_enc_plan.p);
+  // out rows: parity p of stripe i -> parity + i*parity_sp + p*shard_pitch.  host_batch
+  // addresses out slots as out_host + slot*shard_pitch, so shift the base by -k slots.
+  const int t = c->k + c->m;
+  const size_t P = round_up(S, 64);
+  const size_t dev_stripe = P * static_cast<size_t>(t);
+  // run per chunk with explicit copies (parity buffer is separate from data buffer)
+  const size_t target = size_t(64) << 20;
+  const size_t chunk = std::min(N, std::max<size_t>(1, target / dev_stripe));
+  HostPipe pipe;
+  for (int i = 0; i < kStreams; ++i) {
+    RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
+    if (pipe.buf[i].ensure(chunk * dev_stripe)) return RS_ERR_DEVICE;
+  }
+  rs::KernelArgs a = base_args(c, S, 0);
+  a.in_stripe_pitch = a.out_stripe_pitch = dev_stripe;
+  a.shard_pitch = P;
+  a.plans = plan_uni;
+  int j = 0;
+  for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
+    const size_t n = std::min(chunk, N - s0);
+    hipStream_t st = pipe.st[j % kStreams];
+    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kStreams].p);
+    for (int slot = 0; slot < c->k; ++slot)
+      RS_HIP(copy2d(d + slot * P, dev_stripe, data + s0 * data_sp + slot * shard_pitch, data_sp, S, n,
+                    hipMemcpyHostToDevice, st));
+    rs::KernelArgs aa = a;
+    aa.in = aa.out = d;
+    aa.n_stripes = static_cast<uint32_t>(n);
+    int rc = launch(c, aa, false, st);
+    if (rc) return rc;
+    for (int p = 0; p < c->m; ++p)
+      RS_HIP(copy2d(parity + s0 * parity_sp + p * shard_pitch, parity_sp, d + (c->k + p) * P, dev_stripe, S, n,
+                    hipMemcpyDeviceToHost, st));
+  }
+  for (int i = 0; i < kStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
+  (void)out_slots;
+  return RS_OK;
+}
+
+int rs_reconstruct_batch(rs_ctx* c, uint8_t* shards, size_t sp, size_t shard_pitch, size_t S, size_t N,
+                         const uint32_t* masks, size_t n_masks, int mem, void* stream) {
+  if (!c || !shards || !masks) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || shard_pitch < S) return RS_ERR_INVALID_ARG;
+  if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
+  const int t = c->k + c->m;
+  const uint32_t full = (t >= 32) ? 0xFFFFFFFFu : ((1u << t) - 1u);
+  for (size_t i = 0; i < n_masks; ++i)
+    if (__builtin_popcount(masks[i] & full) < c->k) return RS_ERR_TOO_FEW_SHARDS;
+  (void)hipSetDevice(c->device);
+  if (n_masks == 1) {
+    const uint32_t present = masks[0] & full;
+    if (present == full) return RS_OK;
+    const uint8_t* plan = nullptr;
+    int rc = uniform_plan(c, present, false, &plan);
+    if (rc) return rc;
+    if (mem == RS_MEM_DEVICE) {
+      if (!device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
+      rs::KernelArgs a = base_args(c, S, N);
+      a.in = a.out = shards;
+      a.in_stripe_pitch = a.out_stripe_pitch = sp;
+      a.shard_pitch = shard_pitch;
+      a.plans = plan;
+      return launch(c, a, false, pick_stream(c, stream));
+    }
+    if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
+    std::vector<int> in_slots, out_slots;
+    for (int i = 0; i < t; ++i) {
+      if ((present >> i) & 1u) {
+        if (static_cast<int>(in_slots.size()) < c->k) in_slots.push_back(i);
+      } else {
+        out_slots.push_back(i);
+      }
+    }
+    return host_batch(c, shards, sp, in_slots, shards, sp, out_slots, shard_pitch, S, N, plan, nullptr);
+  }
+  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
+  if (mem == RS_MEM_DEVICE) {
+    if (!device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
+    hipStream_t s = pick_stream(c, stream);
+    const uint32_t* dm = nullptr;
+    int rc = upload_masks(c, masks, N, s, &dm);
+    if (rc) return rc;
+    rs::KernelArgs a = base_args(c, S, N);
+    a.in = a.out = shards;
+    a.in_stripe_pitch = a.out_stripe_pitch = sp;
+    a.shard_pitch = shard_pitch;
+    a.plans = static_cast<const uint8_t*>(c->d_plans.p);
+    a.present_masks = dm;
+    a.lut = static_cast<const uint16_t*>(c->d_lut.p);
+    a.status = static_cast<uint32_t*>(c->d_status.p);
+    return launch(c, a, true, s);
+  }
+  if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
+  // host, per-stripe patterns: every slot travels both ways (present slots come back
+  // unchanged); selective copies per pattern are a later optimisation.
+  std::vector<int> all(t);
+  for (int i = 0; i < t; ++i) all[i] = i;
+  return host_batch(c, shards, sp, all, shards, sp, all, shard_pitch, S, N, static_cast<const uint8_t*>(c->d_plans.p),
+                    masks);
+}
+
+int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* shards, size_t sp, size_t shard_pitch, size_t S, size_t N,
+                                 const uint32_t* masks_dev, void* stream) {
+  if (!c || !shards || !masks_dev) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
+  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || !device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  rs::KernelArgs a = base_args(c, S, N);
+  a.in = a.out = shards;
+  a.in_stripe_pitch = a.out_stripe_pitch = sp;
+  a.shard_pitch = shard_pitch;
+  a.plans = static_cast<const uint8_t*>(c->d_plans.p);
+  a.present_masks = masks_dev;
+  a.lut = static_cast<const uint16_t*>(c->d_lut.p);
+  a.status = static_cast<uint32_t*>(c->d_status.p);
+  return launch(c, a, true, pick_stream(c, stream));
+}
+
+int rs_sync(rs_ctx* c, void* stream) {
+  if (!c) return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  RS_HIP(hipMemcpyAsync(c->h_status.p, c->d_status.p, 4, hipMemcpyDeviceToHost, s));
+  RS_HIP(hipStreamSynchronize(s));
+  uint32_t st = *static_cast<uint32_t*>(c->h_status.p);
+  if (st) {
+    RS_HIP(hipMemsetAsync(c->d_status.p, 0, 4, s));
+    RS_HIP(hipStreamSynchronize(s));
+    return RS_ERR_TOO_FEW_SHARDS;
+  }
+  return RS_OK;
+}
+
+int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
+  if (!c || !ptr) return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  RS_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  return RS_OK;
+}
+
+int rs_host_unregister(rs_ctx* c, void* ptr) {
+  if (!c || !ptr) return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  RS_HIP(hipHostUnregister(ptr));
+  return RS_OK;
+}
+
+int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!c || !dst || !src || bytes % 16 || reinterpret_cast<uintptr_t>(dst) % 16 ||
+      reinterpret_cast<uintptr_t>(src) % 16)
+    return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  const uint32_t grid = static_cast<uint32_t>(
+      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(c->cu_count) * 8, (bytes / 16 + 255) / 256)));
+  rs::launch_copy(src, dst, bytes, grid, pick_stream(c, stream));
+  c->last_kernel.store("copy_kernel");
+  RS_HIP(hipGetLastError());
+  return RS_OK;
+}
+
+int rs_set_blocks_per_cu(rs_ctx* c, int bpc) {
+  if (!c || bpc < 0) return RS_ERR_INVALID_ARG;
+  c->blocks_per_cu_override = bpc;
+  return RS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// rs_plan.hpp -- device-visible coefficient plans and kernel arguments.
+//
+// A plan is one coefficient matrix C[e x K] in the form the kernels consume,
+// plus the shard slots it reads and writes:
+//   encode       : in = data shards 0..K-1, out = parity 0..M-1   (rows K..K+M-1 of
+//                  the encode matrix, [upstream reedsolomon.go Encode])
+//   reconstruct  : in = first K present shards in index order, out = every missing
+//                  shard (data then parity, index order), C = composed decode rows
+//                  ([upstream reedsolomon.go reconstruct] phases 1+2 folded).
+// Byte layout (plan_bytes = plan_stride(K, M), 16-B aligned):
+//   u32 n_out; u32 reserved; u32 in_idx[K]; u32 out_idx[M]; pad to 16;
+//   u32 tab[M][K][5]   -- per coefficient f: 3-chunk v_perm tables
+//                         {A_lo, A_hi, B_lo, B_hi, C_lo} (see rs_kernels.hip).
+#pragma once
+
+#include <stdint.h>
+
+
+namespace rs {
+
+constexpr int kMaxK = 32;
+constexpr int kMaxM = 16;
+constexpr uint32_t kPlanInvalid = 0xFFFFu;
+
+__host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
+  return (8u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
+}
+__host__ __device__ constexpr uint32_t plan_stride(int k, int m) {
+  return (plan_tab_offset(k, m) + 20u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) &
+         ~15u;
+}
+
+// Plans, masks and LUT are written by the host before a launch and never by a
+// kernel, so device code reads them through the constant address space: uniform
+// addresses then lower to scalar (s_load) reads into SGPRs.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RS_CONST __attribute__((address_space(4)))
+#else
+#define RS_CONST
+#endif
+template <typename T>
+__host__ __device__ inline const RS_CONST T* as_const(const void* p) {
+  return (const RS_CONST T*)(p);
+}
+
+struct PlanView {
+  const uint8_t* p;
+  int k, m;
+  __host__ __device__ PlanView(const uint8_t* plan, int kk, int mm) : p(plan), k(kk), m(mm) {}
+  __host__ __device__ uint32_t n_out() const { return *as_const<uint32_t>(p); }
+  __host__ __device__ uint32_t in_idx(int c) const { return as_const<uint32_t>(p + 8)[c]; }
+  __host__ __device__ uint32_t out_idx(int r) const { return as_const<uint32_t>(p + 8 + 4 * k)[r]; }
+  __host__ __device__ const RS_CONST uint32_t* tab(int r, int c) const {
+    return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (r * k + c) * 5;
+  }
+};
+
+struct KernelArgs {
+  const uint8_t* in;
+  uint8_t* out;
+  uint64_t in_stripe_pitch;
+  uint64_t out_stripe_pitch;
+  uint64_t shard_pitch;
+  uint32_t shard_len;
+  uint32_t n_stripes;
+  uint32_t blocks_per_stripe;  // ceil(ceil(S/16) / 64)
+  int32_t k, m;
+  uint32_t full_mask;          // (1 << (k+m)) - 1
+  uint32_t plan_bytes;
+  const uint8_t* plans;            // uniform plan, or plan array (PER_STRIPE)
+  const uint32_t* present_masks;   // PER_STRIPE: bit s = shard s present
+  const uint16_t* lut;             // PER_STRIPE: missing mask -> plan index
+  uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards
+};
+
+// Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
+const char* launch_apply(const KernelArgs& a, bool per_stripe, uint32_t grid_blocks,
+                         hipStream_t s, bool force_generic);
+void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
+int apply_kernel_max_blocks_per_cu(int k, int m, bool per_stripe);
+
+}  // namespace rs

@@ -1,0 +1,157 @@
+"""Host-side mirror of the reference's ``internal/ec`` package over librsgpu.so.
+
+Reference surface (kept name-for-name so tests read like the reference's):
+  internal/ec/ec.go:15-17   type Service struct { driver reedsolomon.Encoder }
+  internal/ec/ec.go:21-44   func NewService() interfaces.IEcDriver
+  internal/ec/ec.go:48-50   func (s *Service) Split(data []byte) ([][]byte, error)
+  internal/ec/ec.go:54-56   func (s *Service) Encode(shards [][]byte) error
+  internal/ec/ec.go:59-61   func (s *Service) Reconstruct(shards [][]byte) error
+  internal/interfaces/interfaces.go:41-52  IEcDriver
+  internal/config/config.go:20-23          K = 4, M = 2
+
+Go's ``[][]byte`` maps to a Python list whose entries are ``bytearray`` (or
+``None``/empty for a nil shard); Go's ``error`` maps to :class:`ECError`, whose
+message is klauspost's sentinel text.  Every parity / reconstructed byte is
+computed by the HIP kernels behind the C-ABI; this module only marshals.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+from . import _lib
+
+K = 4  # internal/config/config.go:21
+M = 2  # internal/config/config.go:22
+
+
+class ECError(Exception):
+    """A codec error; ``str(e)`` is the klauspost sentinel message."""
+
+    def __init__(self, code: int):
+        self.code = code
+        super().__init__(_lib.strerror(code))
+
+
+# klauspost v1.12.1 errors.go: Split's sentinel is produced on the host.
+ErrShortData = _lib.RS_ERR_SHORT_DATA
+ErrTooFewShards = _lib.RS_ERR_TOO_FEW_SHARDS
+ErrShardNoData = _lib.RS_ERR_SHARD_NO_DATA
+ErrShardSize = _lib.RS_ERR_SHARD_SIZE
+
+
+def _check(rc: int) -> None:
+    if rc != _lib.RS_OK:
+        raise ECError(rc)
+
+
+def _shard_array(shards: Sequence[Optional[bytearray]], S: int, fill_missing: bool):
+    """Build (u8** ptrs, size_t* lens, keepalive) for a K+M shard list."""
+    n = len(shards)
+    ptrs = (_lib._u8p * n)()
+    lens = (ctypes.c_size_t * n)()
+    keep = []
+    for i, sh in enumerate(shards):
+        if sh is None or len(sh) == 0:
+            lens[i] = 0
+            if fill_missing:
+                buf = (ctypes.c_uint8 * max(S, 1))()
+                keep.append(buf)
+                ptrs[i] = ctypes.cast(buf, _lib._u8p)
+            continue
+        if not isinstance(sh, bytearray):
+            raise TypeError("shards must be bytearray (mutable, like Go []byte) or None")
+        buf = (ctypes.c_uint8 * len(sh)).from_buffer(sh)
+        keep.append(buf)
+        ptrs[i] = ctypes.cast(buf, _lib._u8p)
+        lens[i] = len(sh)
+    return ptrs, lens, keep
+
+
+class Service:
+    """IEcDriver implementation on the MI355X engine (internal/ec/ec.go:15-17)."""
+
+    def __init__(self, k: int = K, m: int = M, device: int = 0):
+        handle = ctypes.c_void_p()
+        _check(_lib.lib().rs_create(k, m, device, 0, ctypes.byref(handle)))
+        self._ctx = handle
+        self.k, self.m = k, m
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            _lib.lib().rs_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ctx(self) -> ctypes.c_void_p:
+        return self._ctx
+
+    def backend(self) -> str:
+        return _lib.lib().rs_backend(self._ctx).decode()
+
+    def encode_matrix(self) -> List[List[int]]:
+        t = self.k + self.m
+        out = (ctypes.c_uint8 * (t * self.k))()
+        _check(_lib.lib().rs_encode_matrix(self._ctx, out))
+        return [list(out[r * self.k:(r + 1) * self.k]) for r in range(t)]
+
+    # ---- IEcDriver -------------------------------------------------------------
+    def Split(self, data: bytes) -> List[bytearray]:
+        """[upstream reedsolomon.go Split]: perShard = ceil(len/K); data shards hold
+        the payload zero-padded to K*perShard; parity shards are zeroed.  Go's
+        aliasing of ``data`` cannot be expressed for Python ``bytes``; the byte
+        contents are identical."""
+        if len(data) == 0:
+            raise ECError(ErrShortData)
+        S = int(_lib.lib().rs_shard_size(self._ctx, len(data)))
+        padded = bytes(data) + bytes(self.k * S - len(data))
+        out = [bytearray(padded[i * S:(i + 1) * S]) for i in range(self.k)]
+        out += [bytearray(S) for _ in range(self.m)]
+        return out
+
+    def Encode(self, shards: List[Optional[bytearray]]) -> None:
+        if len(shards) != self.k + self.m:
+            raise ECError(ErrTooFewShards)
+        ptrs, lens, keep = _shard_array(shards, 0, fill_missing=False)
+        _check(_lib.lib().rs_encode(self._ctx, ptrs, lens))
+        del keep
+
+    def _reconstruct(self, shards: List[Optional[bytearray]], data_only: bool) -> None:
+        if len(shards) != self.k + self.m:
+            raise ECError(ErrTooFewShards)
+        S = next((len(s) for s in shards if s is not None and len(s) > 0), 0)
+        ptrs, lens, keep = _shard_array(shards, S, fill_missing=True)
+        fn = _lib.lib().rs_reconstruct_data if data_only else _lib.lib().rs_reconstruct
+        _check(fn(self._ctx, ptrs, lens))
+        for i, sh in enumerate(shards):
+            if (sh is None or len(sh) == 0) and lens[i] == S and S > 0:
+                shards[i] = bytearray(ctypes.string_at(ptrs[i], S))
+        del keep
+
+    def Reconstruct(self, shards: List[Optional[bytearray]]) -> None:
+        """Fills every nil/empty entry (data and parity), as readservice.go:285 and
+        poller.go:282 rely on."""
+        self._reconstruct(shards, data_only=False)
+
+    def ReconstructData(self, shards: List[Optional[bytearray]]) -> None:
+        self._reconstruct(shards, data_only=True)
+
+    def Verify(self, shards: List[bytearray]) -> bool:
+        if len(shards) != self.k + self.m:
+            raise ECError(ErrTooFewShards)
+        ptrs, lens, keep = _shard_array(shards, 0, fill_missing=False)
+        ok = ctypes.c_int(0)
+        _check(_lib.lib().rs_verify(self._ctx, ptrs, lens, ctypes.byref(ok)))
+        del keep
+        return bool(ok.value)
+
+
+def NewService(k: int = K, m: int = M, device: int = 0) -> Service:
+    """internal/ec/ec.go:21 NewService(): RS(K=4, M=2) on the GPU engine."""
+    return Service(k, m, device)
