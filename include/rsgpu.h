@@ -10,7 +10,7 @@
  *
  * Conventions
  *  - Plain C types only: pointers, sizes, ints.  No torch / HIP types in signatures
- *    (streams are passed as void* = hipStream_t, NULL = the context's own stream).
+ *    (streams are passed as void* = hipStream_t, NULL = the HIP null stream).
  *  - Return value: RS_OK (0) or an RS_ERR_* code; rs_strerror() gives the message.
  *    Codes 1..7 carry klauspost's sentinel messages (errors.go) so that a Go shim
  *    can return errors whose %v text matches the reference's.

@@ -171,7 +171,6 @@ struct rs_ctx {
   bool force_generic = false;
   std::string backend;
   Matrix enc;
-  hipStream_t stream = nullptr;  // default stream for device calls with stream == NULL
 
   // encode plan (device, uniform)
   DevBuf d_enc_plan;
@@ -206,7 +205,6 @@ struct rs_ctx {
       if (s.done) (void)hipEventDestroy(s.done);
     for (auto& l : lanes)
       if (l->stream) (void)hipStreamDestroy(l->stream);
-    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -382,7 +380,9 @@ int reconstruct_impl(rs_ctx* c, uint8_t* const* shards, size_t* lens, bool data_
   return RS_OK;
 }
 
-hipStream_t pick_stream(rs_ctx* c, void* s) { return s ? static_cast<hipStream_t>(s) : c->stream; }
+// NULL = the HIP null stream (as in HIP's own APIs), so torch's default stream and
+// the engine order against each other.
+hipStream_t pick_stream(rs_ctx*, void* s) { return static_cast<hipStream_t>(s); }
 
 bool device_layout_ok(const void* base, size_t stripe_pitch, size_t shard_pitch, size_t S) {
   return (reinterpret_cast<uintptr_t>(base) % 16 == 0) && stripe_pitch % 16 == 0 && shard_pitch % 16 == 0 &&
@@ -528,7 +528,6 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
   char name[160];
   std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
   c->backend = name;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return RS_ERR_DEVICE;
 
   // encode plan: in = data 0..k-1, out = parity slots k..k+m-1 (unified layout);
   // rs_encode_batch remaps outputs for a separate parity buffer via out_idx - k.
