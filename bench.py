@@ -62,82 +62,80 @@ def two_erasure_masks(rng, n, t):
     return (full & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32)
 
 
-def make_batches(torch, eng, n_batches, N, t, P, S, seed):
-    bufs = []
+def make_batches(torch, n_batches, N, k, m, P, seed):
+    """Split layout (the fast device layout): data [N, K, P] + parity [N, M, P]."""
     g = torch.Generator(device="cuda").manual_seed(seed)
+    out = []
     for _ in range(n_batches):
-        b = torch.randint(0, 256, (N, t, P), dtype=torch.uint8, device="cuda", generator=g)
-        bufs.append(b)
-    return bufs
+        d = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+        p = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+        out.append((d, p))
+    return out
 
 
-class KernelTimer:
-    """HIP events around each launch on the launch stream."""
-
-    def __init__(self, torch):
-        self.torch = torch
-        self.pairs = {}
-
-    def start(self):
-        e = self.torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
-
-    def stop(self, name, e0):
-        e1 = self.torch.cuda.Event(enable_timing=True)
-        e1.record()
-        self.pairs.setdefault(name, []).append((e0, e1))
-
-    def avg_ms(self):
-        return {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in self.pairs.items()}
-
-
-def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, kernel_timer=True):
-    """Returns dict with step time and per-kernel averages for encode + 2-erasure
-    reconstruct (seeded per-stripe pattern, device-resident masks)."""
+def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofline_reps=20):
+    """Step = encode the batch + reconstruct 2 erased shards per stripe (seeded
+    per-stripe pattern, device-resident masks).  Returns the step time, and each
+    kernel's average launch duration from `roofline_reps` back-to-back launches
+    bracketed by one HIP event pair on the launch stream (torch's current stream,
+    which the engine launches on)."""
     from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
 
     t = k + m
     P = shard_pitch_for(S)
     batch_bytes = N * t * P
     nb = max(2, int(np.ceil(rotate_bytes / batch_bytes)))
-    bufs = make_batches(torch, eng, nb, N, t, P, S, seed)
+    bufs = make_batches(torch, nb, N, k, m, P, seed)
     rng = np.random.default_rng(0x5EED0003)
     masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(nb)]
-    timer = KernelTimer(torch)
+    for d, p in bufs:  # make every batch a codeword before timing
+        eng.encode(d, p, S, N)
 
-    def step(i, timed):
-        b = bufs[i % nb]
-        e0 = timer.start() if timed else None
-        eng.encode_unified(b, S, P, N)
-        if timed:
-            timer.stop("encode", e0)
-            e0 = timer.start()
-        eng.reconstruct_unified_devmask(b, S, P, N, masks[i % nb])
-        if timed:
-            timer.stop("reconstruct", e0)
+    def enc(i):
+        d, p = bufs[i % nb]
+        eng.encode(d, p, S, N)
+
+    def rec(i):
+        d, p = bufs[i % nb]
+        eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
 
     for i in range(warmup):
-        step(i, False)
+        enc(i)
+        rec(i)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
-        step(i, kernel_timer)
+        enc(i)
+        rec(i)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     eng.sync()
-    # correctness at full size: reconstructed slots hold the encoded bytes again
+    kernel_ms = {}
+    kernel_names = {}
+    for name, fn in (("encode", enc), ("reconstruct", rec)):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(roofline_reps):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        kernel_ms[name] = e0.elapsed_time(e1) / roofline_reps
+        kernel_names[name] = eng.last_kernel()
+    eng.sync()
+    # full-size property check: after encode + reconstruct the batch is still a
+    # codeword, i.e. re-encoding a sample reproduces the stored parity
     ok = True
     for i in range(min(nb, 2)):
-        b = bufs[i]
-        chk = b[:64].clone()
-        eng.encode_unified(chk, S, P, 64)
+        d, p = bufs[i]
+        chk = torch.empty_like(p[:256])
+        eng.encode(d[:256], chk, S, 256)
         torch.cuda.synchronize()
-        ok &= bool(torch.equal(chk[:, :, :S], b[:64, :, :S]))
-    km = timer.avg_ms() if kernel_timer else {}
+        ok &= bool(torch.equal(chk[:, :, :S], p[:256, :, :S]))
     del bufs, masks
     torch.cuda.empty_cache()
-    return {"dt": dt, "steps": steps, "kernel_ms": km, "batch_bytes": batch_bytes, "n_batches": nb, "ok": ok}
+    return {"dt": dt, "steps": steps, "kernel_ms": kernel_ms, "batch_bytes": batch_bytes, "n_batches": nb, "ok": ok,
+            "kernels": kernel_names}
 
 
 def cpu_baseline(k, m, S, N_sample, seconds):
@@ -196,22 +194,24 @@ def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
 
 
 def host_e2e(torch, eng, k, m, S, N):
-    """Pinned host -> H2D -> kernel -> D2H, encode then 1-erasure reconstruct."""
-    t = k + m
-    P = S
-    host = np.random.default_rng(2).integers(0, 256, N * t * P, dtype=np.uint8).reshape(N, t, P)
-    eng.host_register(host)
+    """Pinned host -> H2D -> kernel -> D2H (split layout, shards back to back as
+    Split produces them): encode, then 1-erasure reconstruct."""
+    data = np.random.default_rng(2).integers(0, 256, (N, k, S), dtype=np.uint8)
+    parity = np.zeros((N, m, S), np.uint8)
+    eng.host_register(data)
+    eng.host_register(parity)
     try:
-        eng.encode_host(host, S, P, N)
+        eng.encode_host(data, parity, S, N)
         t0 = time.perf_counter()
-        eng.encode_host(host, S, P, N)
+        eng.encode_host(data, parity, S, N)
         t_enc = time.perf_counter() - t0
-        mask = ((1 << t) - 1) & ~1
+        mask = ((1 << (k + m)) - 1) & ~1
         t0 = time.perf_counter()
-        eng.reconstruct_host(host, S, P, N, mask)
+        eng.reconstruct_host(data, parity, S, N, mask)
         t_rec = time.perf_counter() - t0
     finally:
-        eng.host_unregister(host)
+        eng.host_unregister(data)
+        eng.host_unregister(parity)
     return {"encode_GiBps": round(N * k * S / t_enc / GiB, 2), "reconstruct1_GiBps": round(N * k * S / t_rec / GiB, 2),
             "bytes_user": N * k * S}
 
@@ -298,7 +298,9 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": f"apply_kernel<{k},{m}> ({dom})",
+            "kernel": f"{res['kernels'].get(dom)} ({dom}; rocprof name rs::apply_kernel<{k}, {m}, 2, "
+                      f"{'true' if dom == 'reconstruct' else 'false'}>)",
+            "timing": "HIP events around 20 back-to-back launches on the launch stream",
             "achieved": round(achieved, 1) if achieved else None,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -318,7 +320,7 @@ def main():
             e2 = BatchEngine(kk, mm, 0)
             SS = -(-65536 // kk)
             NN = 16384
-            r = measure_rs(torch, e2, kk, mm, SS, NN, 10, 2, rotate, seed=0x5EED0004)
+            r = measure_rs(torch, e2, kk, mm, SS, NN, 5, 2, rotate, seed=0x5EED0004, roofline_reps=10)
             kms = r["kernel_ms"]
             sweep[f"rs{kk}{mm}_64KiB"] = {
                 "shard_len": SS, "stripes": NN,

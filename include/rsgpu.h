@@ -84,39 +84,41 @@ int rs_reconstruct_data(rs_ctx *ctx, uint8_t *const *shards, size_t *lens);
 int rs_verify(rs_ctx *ctx, uint8_t *const *shards, const size_t *lens, int *ok);
 
 /* ---- batched API: the throughput path -----------------------------------
- * A batch holds n_stripes independent stripes (objects).  Shard s of stripe i is
- * at  base + i*stripe_pitch + s*shard_pitch,  shard_len (S) bytes.
+ * A batch holds n_stripes independent stripes (objects) in a SPLIT layout (the
+ * reference's shard order: shards[0..k) data, shards[k..k+m) parity):
+ *   data shard s  (s < k)  of stripe i:  data   + i*data_stripe_pitch   + s*shard_pitch
+ *   parity shard p (p < m) of stripe i:  parity + i*parity_stripe_pitch + p*shard_pitch
+ * each shard_len (S) bytes.  A unified K+M-slot layout is the special case
+ * parity = data + k*shard_pitch with equal stripe pitches.
  *
- * RS_MEM_DEVICE: shard_pitch and stripe_pitch must be multiples of 16 and
- *   shard_pitch >= round_up(S, 16), the base 16-B aligned (the kernels read whole
- *   16-B columns; the bytes of a slot past S may be read, never written).
- *   The call enqueues on `stream` and returns; synchronise with hipStreamSynchronize
- *   or rs_sync.
- * RS_MEM_HOST: any pitches; the engine stages through pinned buffers with
- *   H2D / kernel / D2H overlapped on several streams, and returns when the
- *   outputs are in host memory.
+ * RS_MEM_DEVICE: pitches must be multiples of 16 and shard_pitch >= round_up(S, 16),
+ *   bases 16-B aligned (the kernels read whole 16-B columns; bytes of a slot past S
+ *   may be read, never written).  The call enqueues on `stream` and returns;
+ *   synchronise with hipStreamSynchronize or rs_sync.
+ * RS_MEM_HOST: any pitches; the engine stages through pinned device slabs with
+ *   H2D / kernel / D2H overlapped on several streams and returns when the outputs
+ *   are in host memory (pin the buffers with rs_host_register for full speed).
  *
- * rs_encode_batch: reads data shards 0..k-1 of each stripe from `data`
- *   (data_stripe_pitch), writes parity 0..m-1 into `parity` (parity_stripe_pitch).
- *   For the unified K+M-slot layout pass parity = data + k*shard_pitch and equal
- *   stripe pitches.
- * rs_reconstruct_batch: unified layout (k+m slots per stripe), in place.
- *   present_masks: host array of n_masks uint32 (bit s set = shard s present);
- *   n_masks == 1 applies one pattern to every stripe, n_masks == n_stripes gives a
- *   pattern per stripe.  Missing shards (data and parity) are written.  Any mask
- *   with < k present -> RS_ERR_TOO_FEW_SHARDS and nothing is modified.
+ * rs_encode_batch: reads data shards, writes every parity shard.
+ * rs_reconstruct_batch: in place.  present_masks: host array of n_masks uint32
+ *   (bit s set = shard s present); n_masks == 1 applies one pattern to every
+ *   stripe, n_masks == n_stripes gives a pattern per stripe (k+m <= 16).  Every
+ *   missing shard (data and parity) is written.  Any mask with < k present ->
+ *   RS_ERR_TOO_FEW_SHARDS and nothing is modified.
  */
 int rs_encode_batch(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch, uint8_t *parity,
                     size_t parity_stripe_pitch, size_t shard_pitch, size_t shard_len,
                     size_t n_stripes, int mem, void *stream);
-int rs_reconstruct_batch(rs_ctx *ctx, uint8_t *shards, size_t stripe_pitch, size_t shard_pitch,
-                         size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
-                         size_t n_masks, int mem, void *stream);
+int rs_reconstruct_batch(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch, uint8_t *parity,
+                         size_t parity_stripe_pitch, size_t shard_pitch, size_t shard_len,
+                         size_t n_stripes, const uint32_t *present_masks, size_t n_masks, int mem,
+                         void *stream);
 /* Device-resident masks (RS_MEM_DEVICE only, k+m <= 16): present_masks_dev is a
- * device array of n_stripes uint32.  Stripes with < k present are skipped and
- * reported by the next rs_sync on that stream as RS_ERR_TOO_FEW_SHARDS. */
-int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *shards, size_t stripe_pitch,
-                                 size_t shard_pitch, size_t shard_len, size_t n_stripes,
+ * device array of n_stripes uint32.  Stripes with < k present are left untouched
+ * and reported by the next rs_sync on that stream as RS_ERR_TOO_FEW_SHARDS. */
+int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch,
+                                 uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
+                                 size_t shard_len, size_t n_stripes,
                                  const uint32_t *present_masks_dev, void *stream);
 /* Wait for `stream` and return any deferred device-side error. */
 int rs_sync(rs_ctx *ctx, void *stream);
@@ -130,7 +132,8 @@ int rs_host_unregister(rs_ctx *ctx, void *ptr);
 const char *rs_last_kernel(const rs_ctx *ctx);
 /* Streaming device copy, the measured HBM ceiling beside the RS kernels. */
 int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
-/* Tuning knob: workgroups per CU for the batched kernels (0 = default). */
+/* Tuning knob: workgroups (256 threads) per CU for the batched kernels
+ * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
 
 #ifdef __cplusplus

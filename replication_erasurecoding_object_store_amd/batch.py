@@ -1,12 +1,14 @@
-"""Batched device-resident API over librsgpu.so (the throughput path).
+"""Batched API over librsgpu.so (the throughput path).
 
 torch provides device memory and the stream (plumbing only): tensors are passed to
-the C-ABI as raw pointers, kernels run on torch's *current* stream so that
+the C-ABI as raw pointers and kernels run on torch's *current* stream, so
 ``torch.cuda.Event`` brackets them exactly.
 
-Layout (unified, SURVEY.md 8d "shard-major per stripe"): a uint8 tensor viewed as
-[n_stripes, k+m, shard_pitch]; shard s of stripe i is row (i, s); the first
-shard_len bytes of each row are the shard, the rest is padding.
+Layouts (include/rsgpu.h):
+  split   data [N, K, P] + parity [N, M, P]  -- the fast device layout (two
+          sequential streams; object i's K data shards contiguous = its Split view)
+  unified one buffer [N, K+M, P]             -- parity = data + K*P
+P (shard pitch) >= S rounded up to 16; :func:`shard_pitch_for` picks 64-B multiples.
 """
 from __future__ import annotations
 
@@ -36,16 +38,45 @@ def _stream_handle(stream=None) -> ctypes.c_void_p:
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def _masks(present_masks) -> np.ndarray:
+    return np.ascontiguousarray(np.atleast_1d(np.asarray(present_masks, dtype=np.uint32)))
+
+
+def _u32p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))
+
+
 class BatchEngine(Service):
     """Service plus the batched entry points (rs_*_batch)."""
 
-    def encode_batch(self, data, parity, shard_len: int, shard_pitch: int, n_stripes: int,
-                     data_stripe_pitch: int, parity_stripe_pitch: int, stream=None) -> None:
-        """data/parity: device tensors (uint8).  Asynchronous on `stream`."""
-        _check(_lib.lib().rs_encode_batch(self.ctx, data.data_ptr(), data_stripe_pitch, parity.data_ptr(),
-                                          parity_stripe_pitch, shard_pitch, shard_len, n_stripes,
-                                          _lib.RS_MEM_DEVICE, _stream_handle(stream)))
+    # ---- device-resident, split layout --------------------------------------------
+    def encode(self, data, parity, shard_len: int, n_stripes: int, shard_pitch: Optional[int] = None,
+               data_stripe_pitch: Optional[int] = None, parity_stripe_pitch: Optional[int] = None,
+               stream=None) -> None:
+        """data [N, K, P] / parity [N, M, P] uint8 device tensors.  Asynchronous."""
+        P = shard_pitch or data.shape[-1]
+        dsp = data_stripe_pitch or self.k * P
+        psp = parity_stripe_pitch or self.m * P
+        _check(_lib.lib().rs_encode_batch(self.ctx, data.data_ptr(), dsp, parity.data_ptr(), psp, P, shard_len,
+                                          n_stripes, _lib.RS_MEM_DEVICE, _stream_handle(stream)))
 
+    def reconstruct(self, data, parity, shard_len: int, n_stripes: int, present_masks,
+                    shard_pitch: Optional[int] = None, stream=None) -> None:
+        """present_masks: int (one pattern) or host uint32 array (one per stripe)."""
+        P = shard_pitch or data.shape[-1]
+        m = _masks(present_masks)
+        _check(_lib.lib().rs_reconstruct_batch(self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(), self.m * P,
+                                               P, shard_len, n_stripes, _u32p(m), m.size, _lib.RS_MEM_DEVICE,
+                                               _stream_handle(stream)))
+
+    def reconstruct_devmask(self, data, parity, shard_len: int, n_stripes: int, masks_dev,
+                            shard_pitch: Optional[int] = None, stream=None) -> None:
+        P = shard_pitch or data.shape[-1]
+        _check(_lib.lib().rs_reconstruct_batch_devmask(self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(),
+                                                       self.m * P, P, shard_len, n_stripes, masks_dev.data_ptr(),
+                                                       _stream_handle(stream)))
+
+    # ---- device-resident, unified layout ------------------------------------------
     def encode_unified(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, stream=None) -> None:
         """buf: [n_stripes, k+m, shard_pitch] uint8 device tensor; fills parity slots."""
         sp = (self.k + self.m) * shard_pitch
@@ -55,37 +86,53 @@ class BatchEngine(Service):
 
     def reconstruct_unified(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, present_masks,
                             stream=None) -> None:
-        """present_masks: int or host array of uint32 (one per stripe)."""
-        masks = np.ascontiguousarray(np.atleast_1d(np.asarray(present_masks, dtype=np.uint32)))
+        m = _masks(present_masks)
         sp = (self.k + self.m) * shard_pitch
-        _check(_lib.lib().rs_reconstruct_batch(
-            self.ctx, buf.data_ptr(), sp, shard_pitch, shard_len, n_stripes,
-            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), masks.size, _lib.RS_MEM_DEVICE,
-            _stream_handle(stream)))
+        base = buf.data_ptr()
+        _check(_lib.lib().rs_reconstruct_batch(self.ctx, base, sp, base + self.k * shard_pitch, sp, shard_pitch,
+                                               shard_len, n_stripes, _u32p(m), m.size, _lib.RS_MEM_DEVICE,
+                                               _stream_handle(stream)))
 
     def reconstruct_unified_devmask(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, masks_dev,
                                     stream=None) -> None:
         sp = (self.k + self.m) * shard_pitch
-        _check(_lib.lib().rs_reconstruct_batch_devmask(self.ctx, buf.data_ptr(), sp, shard_pitch, shard_len,
-                                                       n_stripes, masks_dev.data_ptr(), _stream_handle(stream)))
+        base = buf.data_ptr()
+        _check(_lib.lib().rs_reconstruct_batch_devmask(self.ctx, base, sp, base + self.k * shard_pitch, sp,
+                                                       shard_pitch, shard_len, n_stripes, masks_dev.data_ptr(),
+                                                       _stream_handle(stream)))
 
     def sync(self, stream=None) -> None:
         _check(_lib.lib().rs_sync(self.ctx, _stream_handle(stream)))
 
-    # ---- host-resident batches (synchronous, pipelined H2D/kernel/D2H) ---------
-    def encode_host(self, buf: np.ndarray, shard_len: int, shard_pitch: int, n_stripes: int) -> None:
+    # ---- host-resident (synchronous, pipelined H2D / kernel / D2H) -------------------
+    def encode_host(self, data: np.ndarray, parity: np.ndarray, shard_len: int, n_stripes: int,
+                    shard_pitch: Optional[int] = None) -> None:
+        """data [N, K, P] / parity [N, M, P] host uint8 arrays."""
+        P = shard_pitch or data.shape[-1]
+        _check(_lib.lib().rs_encode_batch(self.ctx, data.ctypes.data, self.k * P, parity.ctypes.data, self.m * P, P,
+                                          shard_len, n_stripes, _lib.RS_MEM_HOST, None))
+
+    def reconstruct_host(self, data: np.ndarray, parity: np.ndarray, shard_len: int, n_stripes: int,
+                         present_masks, shard_pitch: Optional[int] = None) -> None:
+        P = shard_pitch or data.shape[-1]
+        m = _masks(present_masks)
+        _check(_lib.lib().rs_reconstruct_batch(self.ctx, data.ctypes.data, self.k * P, parity.ctypes.data,
+                                               self.m * P, P, shard_len, n_stripes, _u32p(m), m.size,
+                                               _lib.RS_MEM_HOST, None))
+
+    def encode_host_unified(self, buf: np.ndarray, shard_len: int, shard_pitch: int, n_stripes: int) -> None:
         sp = (self.k + self.m) * shard_pitch
         base = buf.ctypes.data
         _check(_lib.lib().rs_encode_batch(self.ctx, base, sp, base + self.k * shard_pitch, sp, shard_pitch,
                                           shard_len, n_stripes, _lib.RS_MEM_HOST, None))
 
-    def reconstruct_host(self, buf: np.ndarray, shard_len: int, shard_pitch: int, n_stripes: int,
-                         present_masks) -> None:
-        masks = np.ascontiguousarray(np.atleast_1d(np.asarray(present_masks, dtype=np.uint32)))
+    def reconstruct_host_unified(self, buf: np.ndarray, shard_len: int, shard_pitch: int, n_stripes: int,
+                                 present_masks) -> None:
+        m = _masks(present_masks)
         sp = (self.k + self.m) * shard_pitch
-        _check(_lib.lib().rs_reconstruct_batch(
-            self.ctx, buf.ctypes.data, sp, shard_pitch, shard_len, n_stripes,
-            masks.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), masks.size, _lib.RS_MEM_HOST, None))
+        base = buf.ctypes.data
+        _check(_lib.lib().rs_reconstruct_batch(self.ctx, base, sp, base + self.k * shard_pitch, sp, shard_pitch,
+                                               shard_len, n_stripes, _u32p(m), m.size, _lib.RS_MEM_HOST, None))
 
     def host_register(self, arr: np.ndarray) -> None:
         _check(_lib.lib().rs_host_register(self.ctx, arr.ctypes.data, arr.nbytes))
@@ -93,6 +140,7 @@ class BatchEngine(Service):
     def host_unregister(self, arr: np.ndarray) -> None:
         _check(_lib.lib().rs_host_unregister(self.ctx, arr.ctypes.data))
 
+    # ---- measurement helpers ----------------------------------------------------------
     def device_copy(self, dst, src, nbytes: Optional[int] = None, stream=None) -> None:
         n = nbytes if nbytes is not None else src.numel() * src.element_size()
         _check(_lib.lib().rs_device_copy(self.ctx, dst.data_ptr(), src.data_ptr(), n, _stream_handle(stream)))

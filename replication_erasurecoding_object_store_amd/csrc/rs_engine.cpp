@@ -8,7 +8,7 @@
 //     indexed by a dense missing-mask -> plan LUT, so a batch may carry a different
 //     erasure pattern per stripe with no host work per stripe;
 //   * per-object host calls (the IEcDriver drop-in: ec.go:54-61) run on a pool of
-//     "lanes" (stream + pinned staging + device buffers) so concurrent goroutines do
+//     "lanes" (stream + pinned staging + device slab) so concurrent goroutines do
 //     not serialise on one stream;
 //   * host-resident batches are pipelined H2D -> kernel -> D2H over 3 streams.
 // No CPU arithmetic path exists: every parity / reconstructed byte comes from a
@@ -35,12 +35,19 @@ namespace {
 
 using rs::Matrix;
 
-#define RS_HIP(expr)                                    \
-  do {                                                  \
-    if ((expr) != hipSuccess) return RS_ERR_DEVICE;     \
+#define RS_HIP(expr)                                \
+  do {                                              \
+    if ((expr) != hipSuccess) return RS_ERR_DEVICE; \
   } while (0)
 
 size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// Default workgroups (256 threads) per CU for the batched kernels, measured with
+// tools/ab_bench.py on MI355X (profiles/r01_ab_occupancy.log): the streaming
+// pattern wants few waves (tools/hbm_probe2.hip: 1-2 WG/CU beat higher occupancy)
+// until the per-byte VALU work (K*E lookups) needs more waves to hide latency.
+constexpr int kDefaultBlocksPerCu = 0;  // 0 = pick by shape
+int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
 
 // ---- plan construction -----------------------------------------------------
 // 3-chunk v_perm tables for coefficient f (see rs_kernels.hip):
@@ -49,7 +56,8 @@ void perm_tables(uint8_t f, uint32_t* t) {
   const rs::Field& F = rs::field();
   auto pack4 = [&](int base, int shift) {
     uint32_t w = 0;
-    for (int j = 0; j < 4; ++j) w |= static_cast<uint32_t>(F.mul(f, static_cast<uint8_t>((base + j) << shift))) << (8 * j);
+    for (int j = 0; j < 4; ++j)
+      w |= static_cast<uint32_t>(F.mul(f, static_cast<uint8_t>((base + j) << shift))) << (8 * j);
     return w;
   };
   t[0] = pack4(0, 0);
@@ -113,7 +121,7 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
   return RS_OK;
 }
 
-// ---- per-call resources ------------------------------------------------------
+// ---- buffers -------------------------------------------------------------------
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
@@ -163,31 +171,40 @@ struct UploadSlot {
   bool used = false;
 };
 
+// Split shard layout shared by host and device buffers (see rs_plan.hpp).
+struct Layout {
+  uint8_t* data;
+  size_t data_sp;
+  uint8_t* parity;
+  size_t parity_sp;
+  size_t pitch;
+  uint8_t* slot(int k, size_t stripe, int s) const {
+    return s < k ? data + stripe * data_sp + static_cast<size_t>(s) * pitch
+                 : parity + stripe * parity_sp + static_cast<size_t>(s - k) * pitch;
+  }
+  size_t stripe_pitch(int k, int s) const { return s < k ? data_sp : parity_sp; }
+};
+
 }  // namespace
 
 struct rs_ctx {
   int k = 0, m = 0, device = 0, cu_count = 0;
-  int blocks_per_cu_override = 0;
+  int blocks_per_cu = kDefaultBlocksPerCu;
   bool force_generic = false;
   std::string backend;
   Matrix enc;
 
-  // encode plan (device, uniform)
-  DevBuf d_enc_plan;
-  // eager all-pattern plans + LUT (k+m <= 16)
-  DevBuf d_plans, d_lut;
+  DevBuf d_enc_plan;              // encode plan (uniform)
+  DevBuf d_plans, d_lut;          // eager all-pattern plans + LUT (k+m <= 16)
   uint32_t n_plans = 0;
-  std::vector<uint16_t> h_lut;          // missing mask -> plan index
+  std::vector<uint32_t> h_lut;    // missing mask -> plan index
   bool have_lut = false;
-  // uniform-pattern plans built on demand (k+m > 16), keyed by (present, data_only)
-  std::mutex plan_mu;
+  std::mutex plan_mu;             // uniform plans built on demand (k+m > 16 / data-only)
   std::unordered_map<uint64_t, std::unique_ptr<DevBuf>> plan_cache;
 
-  // device status word for devmask calls
-  DevBuf d_status;
+  DevBuf d_status, d_scratch;     // device status word (per-stripe calls); store sink
   PinnedBuf h_status;
 
-  // lanes for synchronous host calls
   std::mutex lane_mu;
   std::condition_variable lane_cv;
   std::vector<std::unique_ptr<Lane>> lanes;
@@ -210,48 +227,56 @@ struct rs_ctx {
 
 namespace {
 
-uint32_t grid_for(rs_ctx* c, uint64_t ntasks, bool per_stripe) {
-  const int bpc = c->blocks_per_cu_override > 0 ? c->blocks_per_cu_override
-                                                : rs::apply_kernel_max_blocks_per_cu(c->k, c->m, per_stripe);
-  const uint64_t cap = static_cast<uint64_t>(c->cu_count) * static_cast<uint64_t>(bpc);
-  const uint64_t need = (ntasks + 3) / 4;  // 4 waves per 256-thread block, one task per wave
-  return static_cast<uint32_t>(std::max<uint64_t>(1, std::min(cap, need)));
-}
-
-rs::KernelArgs base_args(rs_ctx* c, size_t S, size_t N) {
+rs::KernelArgs make_args(rs_ctx* c, const Layout& L, size_t S, size_t N) {
   rs::KernelArgs a{};
+  a.data = L.data;
+  a.parity = L.parity;
+  a.data_sp = L.data_sp;
+  a.parity_sp = L.parity_sp;
+  a.shard_pitch = L.pitch;
   a.shard_len = static_cast<uint32_t>(S);
   a.n_stripes = static_cast<uint32_t>(N);
   a.blocks_per_stripe = static_cast<uint32_t>((round_up(S, 16) / 16 + 63) / 64);
+  a.full_cols = static_cast<uint32_t>(S / 16);
+  a.blocks_full = (a.full_cols + 63u) / 64u;
   a.k = c->k;
   a.m = c->m;
   a.full_mask = (c->k + c->m >= 32) ? 0xFFFFFFFFu : ((1u << (c->k + c->m)) - 1u);
   a.plan_bytes = rs::plan_stride(c->k, c->m);
+  a.scratch = static_cast<uint8_t*>(c->d_scratch.p);
+  a.status = static_cast<uint32_t*>(c->d_status.p);
+  a.lut = static_cast<const uint32_t*>(c->d_lut.p);
   return a;
 }
 
-int launch(rs_ctx* c, const rs::KernelArgs& a, bool per_stripe, hipStream_t s) {
-  if (a.n_stripes == 0 || a.shard_len == 0) return RS_OK;
-  const uint64_t ntasks = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
-  const char* name = rs::launch_apply(a, per_stripe, grid_for(c, ntasks, per_stripe), s, c->force_generic);
+// e = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
+// #missing for per-stripe patterns).
+int launch(rs_ctx* c, const rs::KernelArgs& a, int e, bool per_stripe, hipStream_t s) {
+  if (a.n_stripes == 0 || a.shard_len == 0 || e <= 0) return RS_OK;
+  const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, e);
+  const char* name = rs::launch_apply(a, e, per_stripe, static_cast<uint32_t>(bpc),
+                                      static_cast<uint32_t>(c->cu_count), s, c->force_generic);
+  if (!name) return RS_ERR_DEVICE;
   c->last_kernel.store(name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
 
-// Device pointer of the uniform plan for `present` (k+m <= 16: the eager table).
+uint64_t full_mask64(int t) { return (t >= 64) ? ~0ull : ((1ull << t) - 1); }
+
+// Device pointer of the plan for one erasure pattern (cached).
 int uniform_plan(rs_ctx* c, uint64_t present, bool data_only, const uint8_t** plan_dev) {
   const int t = c->k + c->m;
+  present &= full_mask64(t);
   if (__builtin_popcountll(present) < c->k) return RS_ERR_TOO_FEW_SHARDS;
-  const uint64_t full = (t >= 64) ? ~0ull : ((1ull << t) - 1);
   if (c->have_lut && !data_only) {
-    const uint32_t missing = static_cast<uint32_t>(~present & full);
-    const uint16_t pid = c->h_lut[missing];
+    const uint32_t missing = static_cast<uint32_t>(~present & full_mask64(t));
+    const uint32_t pid = c->h_lut[missing];
     if (pid == rs::kPlanInvalid) return RS_ERR_TOO_FEW_SHARDS;
     *plan_dev = static_cast<const uint8_t*>(c->d_plans.p) + static_cast<size_t>(pid) * rs::plan_stride(c->k, c->m);
     return RS_OK;
   }
-  const uint64_t key = (present & full) | (data_only ? (1ull << 63) : 0ull);
+  const uint64_t key = present | (data_only ? (1ull << 63) : 0ull);
   std::lock_guard<std::mutex> g(c->plan_mu);
   auto it = c->plan_cache.find(key);
   if (it == c->plan_cache.end()) {
@@ -315,6 +340,7 @@ int check_shards(int n, const size_t* lens, bool nilok, size_t* S) {
 // D2H of the outputs, unpack.  in/out slots are shard indices into `shards`.
 int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
                uint8_t* const* shards, size_t S) {
+  if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   LaneGuard lg(c);
   if (lg.rc) return lg.rc;
   Lane* L = lg.lane;
@@ -324,19 +350,14 @@ int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_id
   if (L->dev.ensure(bytes) || L->host.ensure(bytes)) return RS_ERR_DEVICE;
   uint8_t* h = static_cast<uint8_t*>(L->host.p);
   uint8_t* d = static_cast<uint8_t*>(L->dev.p);
-  // inputs: copy each used slot (pad bytes of the slot are never written back)
   for (int s : in_idx) std::memcpy(h + static_cast<size_t>(s) * P, shards[s], S);
-  // contiguous H2D of the slots that carry inputs
-  int lo = *std::min_element(in_idx.begin(), in_idx.end());
-  int hi = *std::max_element(in_idx.begin(), in_idx.end());
+  const int lo = *std::min_element(in_idx.begin(), in_idx.end());
+  const int hi = *std::max_element(in_idx.begin(), in_idx.end());
   RS_HIP(hipMemcpyAsync(d + lo * P, h + lo * P, (hi - lo + 1) * P, hipMemcpyHostToDevice, L->stream));
-  rs::KernelArgs a = base_args(c, S, 1);
-  a.in = d;
-  a.out = d;
-  a.in_stripe_pitch = a.out_stripe_pitch = bytes;
-  a.shard_pitch = P;
+  const Layout dl{d, bytes, d + static_cast<size_t>(c->k) * P, bytes, P};
+  rs::KernelArgs a = make_args(c, dl, S, 1);
   a.plans = plan_dev;
-  int rc = launch(c, a, false, L->stream);
+  int rc = launch(c, a, static_cast<int>(out_idx.size()), false, L->stream);
   if (rc) return rc;
   for (int s : out_idx)
     RS_HIP(hipMemcpyAsync(h + static_cast<size_t>(s) * P, d + static_cast<size_t>(s) * P, S, hipMemcpyDeviceToHost,
@@ -382,16 +403,24 @@ int reconstruct_impl(rs_ctx* c, uint8_t* const* shards, size_t* lens, bool data_
 
 // NULL = the HIP null stream (as in HIP's own APIs), so torch's default stream and
 // the engine order against each other.
-hipStream_t pick_stream(rs_ctx*, void* s) { return static_cast<hipStream_t>(s); }
+hipStream_t as_stream(void* s) { return static_cast<hipStream_t>(s); }
 
-bool device_layout_ok(const void* base, size_t stripe_pitch, size_t shard_pitch, size_t S) {
-  return (reinterpret_cast<uintptr_t>(base) % 16 == 0) && stripe_pitch % 16 == 0 && shard_pitch % 16 == 0 &&
-         shard_pitch >= round_up(S, 16);
+bool device_layout_ok(const Layout& L, int m, size_t S) {
+  auto al = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  return al(L.data) && (m == 0 || al(L.parity)) && L.data_sp % 16 == 0 && L.parity_sp % 16 == 0 &&
+         L.pitch % 16 == 0 && L.pitch >= round_up(S, 16);
+}
+
+bool batch_sizes_ok(size_t S, size_t N, size_t pitch) {
+  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || pitch < S) return false;
+  const uint64_t cols = round_up(S, 16) / 16;
+  return N * ((cols + 63) / 64) < 0xFFFFFFFFull;  // task ids fit 32 bits
 }
 
 // ---- host batch pipeline -------------------------------------------------------
 // Chunks of stripes flow H2D -> kernel -> D2H on kStreams streams; each stream has
-// its own device slab, so chunk j+1's copy overlaps chunk j's kernel and D2H.
+// its own device slab (split layout), so chunk j+1's copies overlap chunk j's
+// kernel and D2H.
 constexpr int kStreams = 3;
 
 struct HostPipe {
@@ -403,60 +432,61 @@ struct HostPipe {
   }
 };
 
-// Copies `rows` rows of `width` bytes with independent pitches.
 hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
                   hipMemcpyKind kind, hipStream_t s) {
   if (rows == 0 || width == 0) return hipSuccess;
+  if (dpitch == width && spitch == width) return hipMemcpyAsync(dst, src, width * rows, kind, s);
   return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
 }
 
-// Host-resident batch: for each chunk, copy the in-slots of every stripe (H2D),
-// run the kernel, copy the out-slots back (D2H).
-int host_batch(rs_ctx* c, const uint8_t* in_host, size_t in_sp, const std::vector<int>& in_slots, uint8_t* out_host,
-               size_t out_sp, const std::vector<int>& out_slots, size_t shard_pitch, size_t S, size_t N,
-               const uint8_t* plan_dev, const uint32_t* masks_host /* per-stripe or null */) {
-  const int t = c->k + c->m;
+// Copies the listed slots of n stripes between two layouts.  Runs of consecutive
+// slots that are back to back in one region of both layouts travel as one 2D copy.
+int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<int>& slots, size_t s_dst0,
+               size_t s_src0, size_t n, size_t S, hipMemcpyKind kind, hipStream_t st) {
+  size_t i = 0;
+  while (i < slots.size()) {
+    size_t j = i + 1;
+    while (j < slots.size() && slots[j] == slots[j - 1] + 1 && (slots[j] < k) == (slots[i] < k) && dst.pitch == S &&
+           src.pitch == S)
+      ++j;
+    const int s0 = slots[i];
+    RS_HIP(copy2d(dst.slot(k, s_dst0, s0), dst.stripe_pitch(k, s0), src.slot(k, s_src0, s0), src.stripe_pitch(k, s0),
+                  S * (j - i), n, kind, st));
+    i = j;
+  }
+  return RS_OK;
+}
+
+int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
+               size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e) {
+  const int k = c->k, m = c->m;
   const size_t P = round_up(S, 64);
-  const size_t dev_stripe = P * static_cast<size_t>(t);
-  const size_t target = size_t(64) << 20;
-  size_t chunk = std::max<size_t>(1, target / dev_stripe);
-  chunk = std::min(chunk, N);
+  const size_t per_stripe = P * static_cast<size_t>(k + m) + (masks_host ? 4 : 0);
+  const size_t chunk = std::min(N, std::max<size_t>(1, (size_t(64) << 20) / per_stripe));
   HostPipe pipe;
   for (int i = 0; i < kStreams; ++i) {
     RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
-    if (pipe.buf[i].ensure(chunk * dev_stripe + (masks_host ? chunk * 4 + 256 : 0))) return RS_ERR_DEVICE;
-  }
-  rs::KernelArgs a = base_args(c, S, 0);
-  a.in_stripe_pitch = a.out_stripe_pitch = dev_stripe;
-  a.shard_pitch = P;
-  a.plans = plan_dev;
-  if (masks_host) {
-    a.lut = static_cast<const uint16_t*>(c->d_lut.p);
-    a.status = static_cast<uint32_t*>(c->d_status.p);
+    if (pipe.buf[i].ensure(chunk * per_stripe + 256)) return RS_ERR_DEVICE;
   }
   int j = 0;
   for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
     const size_t n = std::min(chunk, N - s0);
     hipStream_t st = pipe.st[j % kStreams];
     uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kStreams].p);
-    // H2D: slot s of stripes [s0, s0+n): rows of S bytes, pitch in_sp -> dev_stripe
-    for (int slot : in_slots)
-      RS_HIP(copy2d(d + static_cast<size_t>(slot) * P, dev_stripe, in_host + s0 * in_sp + slot * shard_pitch, in_sp, S,
-                    n, hipMemcpyHostToDevice, st));
-    rs::KernelArgs aa = a;
-    aa.in = d;
-    aa.out = d;
-    aa.n_stripes = static_cast<uint32_t>(n);
-    if (masks_host) {
-      uint32_t* dm = reinterpret_cast<uint32_t*>(d + round_up(chunk * dev_stripe, 256));
-      RS_HIP(hipMemcpyAsync(dm, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
-      aa.present_masks = dm;
-    }
-    int rc = launch(c, aa, masks_host != nullptr, st);
+    const Layout dl{d, P * k, d + chunk * P * k, P * m, P};
+    int rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
     if (rc) return rc;
-    for (int slot : out_slots)
-      RS_HIP(copy2d(out_host + s0 * out_sp + slot * shard_pitch, out_sp, d + static_cast<size_t>(slot) * P, dev_stripe, S,
-                    n, hipMemcpyDeviceToHost, st));
+    rs::KernelArgs a = make_args(c, dl, S, n);
+    a.plans = plan_dev;
+    if (masks_host) {
+      uint32_t* dm = reinterpret_cast<uint32_t*>(d + round_up(chunk * P * (k + m), 256));
+      RS_HIP(hipMemcpyAsync(dm, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
+      a.present_masks = dm;
+    }
+    rc = launch(c, a, e, masks_host != nullptr, st);
+    if (rc) return rc;
+    rc = copy_slots(hl, dl, k, out_slots, s0, 0, n, S, hipMemcpyDeviceToHost, st);
+    if (rc) return rc;
   }
   for (int i = 0; i < kStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
   return RS_OK;
@@ -523,14 +553,13 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
   c->device = device;
   c->cu_count = prop.multiProcessorCount;
   c->enc = rs::build_encode_matrix(k, m);
-  if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu_override = std::atoi(e);
+  if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("RSGPU_FORCE_GENERIC")) c->force_generic = std::atoi(e) != 0;
   char name[160];
   std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
   c->backend = name;
 
-  // encode plan: in = data 0..k-1, out = parity slots k..k+m-1 (unified layout);
-  // rs_encode_batch remaps outputs for a separate parity buffer via out_idx - k.
+  // Encode plan: in = data slots 0..k-1, out = parity slots k..k+m-1.
   {
     std::vector<int> in_idx(k), out_idx(m);
     for (int i = 0; i < k; ++i) in_idx[i] = i;
@@ -538,52 +567,46 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
     std::vector<uint8_t> rows(static_cast<size_t>(m) * k);
     for (int p = 0; p < m; ++p)
       for (int i = 0; i < k; ++i) rows[p * k + i] = c->enc.at(k + p, i);
-    // two encode plans back to back: [0] unified (out slots k..), [1] separate parity buffer (out slots 0..)
     std::vector<uint8_t> p0 = make_plan(k, m, in_idx, out_idx, rows);
-    for (int p = 0; p < m; ++p) out_idx[p] = p;
-    std::vector<uint8_t> p1 = make_plan(k, m, in_idx, out_idx, rows);
-    p0.insert(p0.end(), p1.begin(), p1.end());
     if (c->d_enc_plan.ensure(p0.size())) return RS_ERR_DEVICE;
     if (hipMemcpy(c->d_enc_plan.p, p0.data(), p0.size(), hipMemcpyHostToDevice) != hipSuccess) return RS_ERR_DEVICE;
   }
-  // eager all-pattern plans + LUT for k+m <= 16
+  // Eager all-pattern plans + LUT for k+m <= 16.  Plan 0 = nothing missing.
   const int t = k + m;
   if (t <= 16 && m > 0) {
     const uint32_t full = (1u << t) - 1u;
-    c->h_lut.assign(size_t(1) << t, static_cast<uint16_t>(rs::kPlanInvalid));
+    c->h_lut.assign(size_t(1) << t, rs::kPlanInvalid);
     std::vector<uint8_t> all;
-    uint32_t count = 0;
-    // plan 0: no missing shard (n_out = 0)
     {
       std::vector<int> in_idx(k), none;
       for (int i = 0; i < k; ++i) in_idx[i] = i;
       std::vector<uint8_t> p = make_plan(k, m, in_idx, none, {});
       all.insert(all.end(), p.begin(), p.end());
       c->h_lut[0] = 0;
-      count = 1;
     }
+    uint32_t count = 1;
     bool ok = true;
     for (uint32_t missing = 1; missing <= full && ok; ++missing) {
       if (__builtin_popcount(missing) > m) continue;
       std::vector<uint8_t> p;
       if (make_decode_plan(k, m, c->enc, full & ~missing, false, &p) != RS_OK) continue;
-      if (count >= 0xFFFE || all.size() > (size_t(64) << 20)) {
+      if (all.size() + p.size() > (size_t(64) << 20)) {
         ok = false;
         break;
       }
       all.insert(all.end(), p.begin(), p.end());
-      c->h_lut[missing] = static_cast<uint16_t>(count++);
+      c->h_lut[missing] = count++;
     }
     if (ok) {
-      if (c->d_plans.ensure(all.size()) || c->d_lut.ensure(c->h_lut.size() * 2)) return RS_ERR_DEVICE;
+      if (c->d_plans.ensure(all.size()) || c->d_lut.ensure(c->h_lut.size() * 4)) return RS_ERR_DEVICE;
       if (hipMemcpy(c->d_plans.p, all.data(), all.size(), hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(c->d_lut.p, c->h_lut.data(), c->h_lut.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+          hipMemcpy(c->d_lut.p, c->h_lut.data(), c->h_lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return RS_ERR_DEVICE;
       c->n_plans = count;
       c->have_lut = true;
     }
   }
-  if (c->d_status.ensure(256) || c->h_status.ensure(256)) return RS_ERR_DEVICE;
+  if (c->d_status.ensure(256) || c->h_status.ensure(256) || c->d_scratch.ensure(256 * 1024)) return RS_ERR_DEVICE;
   if (hipMemset(c->d_status.p, 0, 256) != hipSuccess) return RS_ERR_DEVICE;
   *out = c.release();
   return RS_OK;
@@ -659,94 +682,55 @@ int rs_encode_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, uint8_t* par
   if (!c || !data || !parity) return RS_ERR_INVALID_ARG;
   if (N == 0) return RS_OK;
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
-  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || shard_pitch < S) return RS_ERR_INVALID_ARG;
+  if (!batch_sizes_ok(S, N, shard_pitch)) return RS_ERR_INVALID_ARG;
   if (c->m == 0) return RS_OK;
   (void)hipSetDevice(c->device);
-  const uint8_t* plan_sep = static_cast<const uint8_t*>(c->d_enc_plan.p) + rs::plan_stride(c->k, c->m);
+  const Layout L{const_cast<uint8_t*>(data), data_sp, parity, parity_sp, shard_pitch};
+  const uint8_t* plan = static_cast<const uint8_t*>(c->d_enc_plan.p);
   if (mem == RS_MEM_DEVICE) {
-    if (!device_layout_ok(data, data_sp, shard_pitch, S) || !device_layout_ok(parity, parity_sp, shard_pitch, S))
-      return RS_ERR_INVALID_ARG;
-    rs::KernelArgs a = base_args(c, S, N);
-    a.in = data;
-    a.out = parity;
-    a.in_stripe_pitch = data_sp;
-    a.out_stripe_pitch = parity_sp;
-    a.shard_pitch = shard_pitch;
-    a.plans = plan_sep;
-    return launch(c, a, false, pick_stream(c, stream));
+    if (!device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
+    rs::KernelArgs a = make_args(c, L, S, N);
+    a.plans = plan;
+    return launch(c, a, c->m, false, as_stream(stream));
   }
   if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
-  // host: stage data slots 0..k-1 in, parity slots k..k+m-1 out (unified device slab)
-  std::vector<int> in_slots(c->k), out_slots;
+  std::vector<int> in_slots(c->k), out_slots(c->m);
   for (int i = 0; i < c->k; ++i) in_slots[i] = i;
-  const uint8_t* plan_uni = static_cast<const uint8_t*>(c->d_enc_plan.p);
-  // out rows: parity p of stripe i -> parity + i*parity_sp + p*shard_pitch.  host_batch
-  // addresses out slots as out_host + slot*shard_pitch, so shift the base by -k slots.
-  const int t = c->k + c->m;
-  const size_t P = round_up(S, 64);
-  const size_t dev_stripe = P * static_cast<size_t>(t);
-  // run per chunk with explicit copies (parity buffer is separate from data buffer)
-  const size_t target = size_t(64) << 20;
-  const size_t chunk = std::min(N, std::max<size_t>(1, target / dev_stripe));
-  HostPipe pipe;
-  for (int i = 0; i < kStreams; ++i) {
-    RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
-    if (pipe.buf[i].ensure(chunk * dev_stripe)) return RS_ERR_DEVICE;
-  }
-  rs::KernelArgs a = base_args(c, S, 0);
-  a.in_stripe_pitch = a.out_stripe_pitch = dev_stripe;
-  a.shard_pitch = P;
-  a.plans = plan_uni;
-  int j = 0;
-  for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
-    const size_t n = std::min(chunk, N - s0);
-    hipStream_t st = pipe.st[j % kStreams];
-    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kStreams].p);
-    for (int slot = 0; slot < c->k; ++slot)
-      RS_HIP(copy2d(d + slot * P, dev_stripe, data + s0 * data_sp + slot * shard_pitch, data_sp, S, n,
-                    hipMemcpyHostToDevice, st));
-    rs::KernelArgs aa = a;
-    aa.in = aa.out = d;
-    aa.n_stripes = static_cast<uint32_t>(n);
-    int rc = launch(c, aa, false, st);
-    if (rc) return rc;
-    for (int p = 0; p < c->m; ++p)
-      RS_HIP(copy2d(parity + s0 * parity_sp + p * shard_pitch, parity_sp, d + (c->k + p) * P, dev_stripe, S, n,
-                    hipMemcpyDeviceToHost, st));
-  }
-  for (int i = 0; i < kStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
-  (void)out_slots;
-  return RS_OK;
+  for (int p = 0; p < c->m; ++p) out_slots[p] = c->k + p;
+  return host_batch(c, L, in_slots, out_slots, S, N, plan, nullptr, c->m);
 }
 
-int rs_reconstruct_batch(rs_ctx* c, uint8_t* shards, size_t sp, size_t shard_pitch, size_t S, size_t N,
-                         const uint32_t* masks, size_t n_masks, int mem, void* stream) {
-  if (!c || !shards || !masks) return RS_ERR_INVALID_ARG;
+int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
+                         size_t shard_pitch, size_t S, size_t N, const uint32_t* masks, size_t n_masks, int mem,
+                         void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !masks) return RS_ERR_INVALID_ARG;
   if (N == 0) return RS_OK;
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
-  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || shard_pitch < S) return RS_ERR_INVALID_ARG;
+  if (!batch_sizes_ok(S, N, shard_pitch)) return RS_ERR_INVALID_ARG;
   if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
   const int t = c->k + c->m;
-  const uint32_t full = (t >= 32) ? 0xFFFFFFFFu : ((1u << t) - 1u);
-  for (size_t i = 0; i < n_masks; ++i)
-    if (__builtin_popcount(masks[i] & full) < c->k) return RS_ERR_TOO_FEW_SHARDS;
+  const uint32_t full = static_cast<uint32_t>(full_mask64(t));
+  int max_missing = 0;
+  for (size_t i = 0; i < n_masks; ++i) {
+    const int np = __builtin_popcount(masks[i] & full);
+    if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
+    max_missing = std::max(max_missing, t - np);
+  }
+  if (max_missing == 0) return RS_OK;
+  if (mem != RS_MEM_DEVICE && mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
+  const Layout L{data, data_sp, parity, parity_sp, shard_pitch};
+  if (mem == RS_MEM_DEVICE && !device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
   if (n_masks == 1) {
     const uint32_t present = masks[0] & full;
-    if (present == full) return RS_OK;
     const uint8_t* plan = nullptr;
     int rc = uniform_plan(c, present, false, &plan);
     if (rc) return rc;
     if (mem == RS_MEM_DEVICE) {
-      if (!device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
-      rs::KernelArgs a = base_args(c, S, N);
-      a.in = a.out = shards;
-      a.in_stripe_pitch = a.out_stripe_pitch = sp;
-      a.shard_pitch = shard_pitch;
+      rs::KernelArgs a = make_args(c, L, S, N);
       a.plans = plan;
-      return launch(c, a, false, pick_stream(c, stream));
+      return launch(c, a, max_missing, false, as_stream(stream));
     }
-    if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
     std::vector<int> in_slots, out_slots;
     for (int i = 0; i < t; ++i) {
       if ((present >> i) & 1u) {
@@ -755,60 +739,48 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* shards, size_t sp, size_t shard_pit
         out_slots.push_back(i);
       }
     }
-    return host_batch(c, shards, sp, in_slots, shards, sp, out_slots, shard_pitch, S, N, plan, nullptr);
+    return host_batch(c, L, in_slots, out_slots, S, N, plan, nullptr, max_missing);
   }
   if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
   if (mem == RS_MEM_DEVICE) {
-    if (!device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
-    hipStream_t s = pick_stream(c, stream);
+    hipStream_t s = as_stream(stream);
     const uint32_t* dm = nullptr;
     int rc = upload_masks(c, masks, N, s, &dm);
     if (rc) return rc;
-    rs::KernelArgs a = base_args(c, S, N);
-    a.in = a.out = shards;
-    a.in_stripe_pitch = a.out_stripe_pitch = sp;
-    a.shard_pitch = shard_pitch;
+    rs::KernelArgs a = make_args(c, L, S, N);
     a.plans = static_cast<const uint8_t*>(c->d_plans.p);
     a.present_masks = dm;
-    a.lut = static_cast<const uint16_t*>(c->d_lut.p);
-    a.status = static_cast<uint32_t*>(c->d_status.p);
-    return launch(c, a, true, s);
+    return launch(c, a, max_missing, true, s);
   }
-  if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
   // host, per-stripe patterns: every slot travels both ways (present slots come back
   // unchanged); selective copies per pattern are a later optimisation.
   std::vector<int> all(t);
   for (int i = 0; i < t; ++i) all[i] = i;
-  return host_batch(c, shards, sp, all, shards, sp, all, shard_pitch, S, N, static_cast<const uint8_t*>(c->d_plans.p),
-                    masks);
+  return host_batch(c, L, all, all, S, N, static_cast<const uint8_t*>(c->d_plans.p), masks, max_missing);
 }
 
-int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* shards, size_t sp, size_t shard_pitch, size_t S, size_t N,
-                                 const uint32_t* masks_dev, void* stream) {
-  if (!c || !shards || !masks_dev) return RS_ERR_INVALID_ARG;
+int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
+                                 size_t shard_pitch, size_t S, size_t N, const uint32_t* masks_dev, void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !masks_dev) return RS_ERR_INVALID_ARG;
   if (N == 0) return RS_OK;
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
   if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
-  if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || !device_layout_ok(shards, sp, shard_pitch, S)) return RS_ERR_INVALID_ARG;
+  const Layout L{data, data_sp, parity, parity_sp, shard_pitch};
+  if (!batch_sizes_ok(S, N, shard_pitch) || !device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
-  rs::KernelArgs a = base_args(c, S, N);
-  a.in = a.out = shards;
-  a.in_stripe_pitch = a.out_stripe_pitch = sp;
-  a.shard_pitch = shard_pitch;
+  rs::KernelArgs a = make_args(c, L, S, N);
   a.plans = static_cast<const uint8_t*>(c->d_plans.p);
   a.present_masks = masks_dev;
-  a.lut = static_cast<const uint16_t*>(c->d_lut.p);
-  a.status = static_cast<uint32_t*>(c->d_status.p);
-  return launch(c, a, true, pick_stream(c, stream));
+  return launch(c, a, c->m, true, as_stream(stream));
 }
 
 int rs_sync(rs_ctx* c, void* stream) {
   if (!c) return RS_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
-  hipStream_t s = pick_stream(c, stream);
+  hipStream_t s = as_stream(stream);
   RS_HIP(hipMemcpyAsync(c->h_status.p, c->d_status.p, 4, hipMemcpyDeviceToHost, s));
   RS_HIP(hipStreamSynchronize(s));
-  uint32_t st = *static_cast<uint32_t*>(c->h_status.p);
+  const uint32_t st = *static_cast<uint32_t*>(c->h_status.p);
   if (st) {
     RS_HIP(hipMemsetAsync(c->d_status.p, 0, 4, s));
     RS_HIP(hipStreamSynchronize(s));
@@ -837,8 +809,8 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
     return RS_ERR_INVALID_ARG;
   (void)hipSetDevice(c->device);
   const uint32_t grid = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(c->cu_count) * 8, (bytes / 16 + 255) / 256)));
-  rs::launch_copy(src, dst, bytes, grid, pick_stream(c, stream));
+      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(c->cu_count) * 2, (bytes / 16 + 1023) / 1024)));
+  rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
   c->last_kernel.store("copy_kernel");
   RS_HIP(hipGetLastError());
   return RS_OK;
@@ -846,7 +818,7 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
 
 int rs_set_blocks_per_cu(rs_ctx* c, int bpc) {
   if (!c || bpc < 0) return RS_ERR_INVALID_ARG;
-  c->blocks_per_cu_override = bpc;
+  c->blocks_per_cu = bpc;  // 0 = by shape
   return RS_OK;
 }
 

@@ -1,28 +1,33 @@
 // rs_kernels.hip -- CDNA4 (gfx950) kernels for Reed-Solomon encode/reconstruct.
 //
-// One kernel family computes  Y[e x S] = C[e x K] (x) X[K x S]  over GF(2^8) for
-// a batch of independent stripes.  Encode (C = parity rows of the encode matrix,
+// One kernel family computes  Y[e x S] = C[e x K] (x) X[K x S]  over GF(2^8) for a
+// batch of independent stripes.  Encode (C = parity rows of the encode matrix,
 // [upstream klauspost reedsolomon.go Encode -> codeSomeShards], called from
-// internal/ec/ec.go:54-56) and reconstruct (C = composed decode rows over the
-// first K present shards, [upstream reconstruct], internal/ec/ec.go:59-61) are
-// the same kernel with different coefficient plans.
+// internal/ec/ec.go:54-56) and reconstruct (C = composed decode rows over the first
+// K present shards, [upstream reconstruct], internal/ec/ec.go:59-61) are the same
+// kernel with different coefficient plans.
 //
 // GF(2^8) multiply by a wave-uniform coefficient f, 4 bytes per VALU op:
-//   x = x[2:0] | x[5:3]<<3 | x[7:6]<<6, and multiplication is GF(2)-linear, so
-//   f*x = A[x[2:0]] ^ B[x[5:3]] ^ C[x[7:6]]  with 8-, 8- and 4-entry product
-//   tables.  An 8-entry byte table is exactly one v_perm_b32 byte pool (two
-//   dwords), so each table lookup is ONE v_perm_b32 on 4 packed bytes, with no
-//   LDS traffic and no data-dependent bank conflicts.  Per (coefficient, data
-//   dword): 3 v_perm_b32 + ~1.5 v_xor3_b32; per data dword 5 ops of index prep
-//   shared by all M outputs.  The tables (5 dwords per coefficient) are
-//   wave-uniform and live in SGPRs.
+//   x = x[2:0] | x[5:3]<<3 | x[7:6]<<6 and multiplication is GF(2)-linear, so
+//   f*x = A[x[2:0]] ^ B[x[5:3]] ^ C[x[7:6]]  with 8-, 8- and 4-entry product tables.
+//   An 8-entry byte table is exactly the byte pool of one v_perm_b32 (two dwords),
+//   so each lookup is ONE v_perm_b32 on 4 packed bytes: no LDS traffic, no
+//   data-dependent bank conflicts.  Per (coefficient, data dword): 3 v_perm_b32 +
+//   1.5 v_xor3_b32; per data dword 5 ops of index prep shared by all outputs.  The
+//   tables (5 dwords per coefficient) are wave-uniform and live in SGPRs.
 //
-// Memory: HBM-bound streaming.  Each wave owns one (stripe, 1 KiB column block)
-// task: lane l reads 16 B at byte offset 16*(64*blk+l) of each of the K input
-// shards (K coalesced 1 KiB wave loads), and writes 16 B of each output shard.
-// Layout (device): shard s of stripe i at base + i*stripe_pitch + s*shard_pitch,
-// shard_pitch and stripe_pitch multiples of 16, shard_pitch >= round_up(S, 16):
-// reads of the tail column may touch the shard slot's padding; writes never do.
+// Memory (HBM-bound streaming; measured pattern study in tools/hbm_probe2.hip):
+//   * split layout: data shards of stripe i at data + i*data_sp + s*P (s < K),
+//     parity at parity + i*parity_sp + (s-K)*P -- two sequential streams;
+//   * grid-stride over tasks (task = one stripe's 1 KiB column block, lane l owns
+//     the 16 B at column 64*blk + l of every shard), 1-2 workgroups per CU;
+//   * 16-B non-temporal loads and stores (one 1 KiB wave instruction each).
+// Every loop trip issues the same vector-memory sequence -- [mask(t+1)] [K loads]
+// [E stores] -- with no branch around any of them (lanes past the last full column
+// and outputs beyond a plan's n_out store to a per-wave scratch line), so the
+// compiler's s_waitcnt vmcnt(N) counts stay exact and the per-stripe plan lookup of
+// the NEXT task overlaps the current task.  Partial tail columns (S % 16) are done
+// by tail_kernel.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,10 +49,17 @@ __device__ __forceinline__ Idx3 split3(uint32_t x) {
   return r;
 }
 
-__device__ __forceinline__ uint32_t lookup3(const Idx3& i, uint32_t t0, uint32_t t1, uint32_t t2,
-                                            uint32_t t3, uint32_t t4) {
-  return __builtin_amdgcn_perm(t1, t0, i.a) ^ __builtin_amdgcn_perm(t3, t2, i.b) ^
-         __builtin_amdgcn_perm(0u, t4, i.c);
+// 3-input XOR in one VALU op: gfx950 has no v_xor3_b32, but v_bitop3_b32 evaluates
+// any 3-input truth table (0x96 = a ^ b ^ c).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// perm(hi, lo, sel) picks byte sel (0..7) of the 8-byte pool {hi:lo}.
+__device__ __forceinline__ uint32_t lookup3(const Idx3& i, uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3,
+                                            uint32_t t4) {
+  return xor3(__builtin_amdgcn_perm(t1, t0, i.a), __builtin_amdgcn_perm(t3, t2, i.b),
+              __builtin_amdgcn_perm(0u, t4, i.c));
 }
 
 __device__ __forceinline__ u32x4 load16(const uint8_t* p) {
@@ -59,99 +71,136 @@ __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
 }
 
 __device__ __forceinline__ void store_tail(uint8_t* p, u32x4 v, uint32_t nbytes) {
-  // nbytes in [1, 15]: byte stores of the valid prefix of the last column.
   for (uint32_t q = 0; q < nbytes; ++q) p[q] = static_cast<uint8_t>(v[q >> 2] >> (8 * (q & 3)));
 }
 
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
-  return __builtin_amdgcn_readfirstlane(v);
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Pins a wave-uniform pointer into SGPRs so loads through it stay scalar.
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// Shard slot s of stripe i (s < k: data region, else parity region).
+__device__ __forceinline__ uint8_t* slot_ptr(const KernelArgs& a, int k, uint32_t stripe, uint32_t s) {
+  return s < static_cast<uint32_t>(k)
+             ? a.data + static_cast<uint64_t>(stripe) * a.data_sp + static_cast<uint64_t>(s) * a.shard_pitch
+             : a.parity + static_cast<uint64_t>(stripe) * a.parity_sp +
+                   static_cast<uint64_t>(s - static_cast<uint32_t>(k)) * a.shard_pitch;
 }
 
 // ---------------------------------------------------------------------------
-// Specialised kernel: compile-time K and M (max outputs), fully unrolled.
-// PER_STRIPE: plan chosen per stripe from present_masks via a missing-mask LUT.
-template <int K, int M, bool PER_STRIPE>
+// Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
+// #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
+template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint64_t ntasks = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
-  const PlanView pv0(a.plans, K, M);
+  const uint32_t bps = a.blocks_full;
+  const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
+  uint8_t* const dummy = a.scratch + (wave & 255u) * 1024u + lane * 16u;
+  uint32_t bad = 0u;
 
-  for (uint64_t t = wave; t < ntasks; t += nwaves) {
-    const uint32_t stripe = static_cast<uint32_t>(t / a.blocks_per_stripe);
-    const uint32_t blk = static_cast<uint32_t>(t - static_cast<uint64_t>(stripe) * a.blocks_per_stripe);
+  // mask of task t's stripe; every lane loads the same word (one request)
+  auto load_mask = [&](uint32_t t) -> uint32_t {
+    const uint32_t tt = t < ntasks ? t : ntasks - 1u;
+    return a.present_masks[tt / bps];
+  };
+
+  uint32_t mask = 0u;
+  if (PER_STRIPE && wave < ntasks) mask = load_mask(wave);
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
     const uint8_t* plan = a.plans;
     if (PER_STRIPE) {
-      const uint32_t present = as_const<uint32_t>(a.present_masks)[stripe];
+      const uint32_t present = __builtin_amdgcn_readfirstlane(mask);  // waits for this mask only
+      mask = load_mask(t + nwaves);                                  // next task's mask in flight
       const uint32_t missing = (~present) & a.full_mask;
-      const uint32_t pid = as_const<uint16_t>(a.lut)[missing];
-      if (pid == kPlanInvalid) {
-        if (lane == 0 && blk == 0) atomicOr(a.status, 1u);
-        continue;
-      }
-      plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
+      uint32_t pid = as_const<uint32_t>(a.lut)[missing];
+      bad |= (pid == kPlanInvalid) ? 1u : 0u;
+      pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> scratch stores
+      plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+    }
+    if constexpr (K * E * 5 > 48) {
+      // Too many table dwords to keep resident in SGPRs across trips: make the plan
+      // pointer opaque per trip so its loads are not hoisted out of the loop (LICM
+      // would otherwise spill them through VGPR lanes: v_writelane/v_readlane).
+      asm volatile("" : "+s"(plan));
     }
     const PlanView pv(plan, K, M);
-    const uint32_t n_out = pv.n_out();
-    if (n_out == 0) continue;
-
     const uint32_t col = blk * 64u + lane;
-    const uint32_t off = col * 16u;
-    if (off >= a.shard_len) continue;
-
-    const uint8_t* in_base = a.in + static_cast<uint64_t>(stripe) * a.in_stripe_pitch;
-    uint8_t* out_base = a.out + static_cast<uint64_t>(stripe) * a.out_stripe_pitch;
+    const bool valid = col < a.full_cols;
+    const uint32_t off = valid ? col * 16u : 0u;  // clamped, never branched
 
     u32x4 x[K];
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = load16(in_base + static_cast<uint64_t>(pv.in_idx(c)) * a.shard_pitch + off);
+    for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
 
-    Idx3 ix[K][4];
+    // input-outer order (as upstream codeSomeShards): one input's chunk indices
+    // and E x 5 table dwords live at a time.  Products of inputs c-1 and c are
+    // folded into the accumulator with one 3-input XOR.  The scheduling barrier
+    // per input stops the compiler from hoisting every input's tables into SGPRs
+    // at once (K*E*5 dwords: 200 for RS(10+4) -> SGPR spills through VGPR lanes).
+    u32x4 y[E], pend[E];
 #pragma unroll
-    for (int c = 0; c < K; ++c)
+    for (int r = 0; r < E; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
-
-    const uint32_t tail = a.shard_len - off;  // >= 1
+    for (int c = 0; c < K; ++c) {
+      Idx3 ix[4];
 #pragma unroll
-    for (int r = 0; r < M; ++r) {
-      if (r >= static_cast<int>(n_out)) break;
-      u32x4 y = {0u, 0u, 0u, 0u};
+      for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
 #pragma unroll
-      for (int c = 0; c < K; ++c) {
+      for (int r = 0; r < E; ++r) {
         const RS_CONST uint32_t* tb = pv.tab(r, c);
-        const uint32_t t0 = tb[0], t1 = tb[1], t2 = tb[2], t3 = tb[3], t4 = tb[4];
+        const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) y[d] ^= lookup3(ix[c][d], t0, t1, t2, t3, t4);
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
+          if (c & 1)
+            y[r][d] = xor3(y[r][d], pend[r][d], prod);
+          else if (c == K - 1)
+            y[r][d] ^= prod;
+          else
+            pend[r][d] = prod;
+        }
       }
-      uint8_t* dst = out_base + static_cast<uint64_t>(pv.out_idx(r)) * a.shard_pitch + off;
-      if (tail >= 16u)
-        store16(dst, y);
-      else
-        store_tail(dst, y, tail);
+      if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t n_out = pv.n_out();
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      uint8_t* real = slot_ptr(a, K, stripe, pv.out_idx(r)) + off;
+      store16((valid && static_cast<uint32_t>(r) < n_out) ? real : dummy, y[r]);
     }
   }
+  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
 }
 
 // ---------------------------------------------------------------------------
-// Generic kernel: runtime K (<= kMaxK), outputs in groups of 4.
+// Generic kernel: runtime K (<= kMaxK) and M, outputs in groups of 4, inline tail
+// handling.  Serves the (K, M) shapes without a specialisation.
 template <bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint64_t ntasks = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  const uint32_t bps = a.blocks_per_stripe;
+  const uint32_t ntasks = a.n_stripes * bps;
   const int K = a.k, M = a.m;
 
-  for (uint64_t t = wave; t < ntasks; t += nwaves) {
-    const uint32_t stripe = static_cast<uint32_t>(t / a.blocks_per_stripe);
-    const uint32_t blk = static_cast<uint32_t>(t - static_cast<uint64_t>(stripe) * a.blocks_per_stripe);
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
     const uint8_t* plan = a.plans;
     if (PER_STRIPE) {
       const uint32_t present = as_const<uint32_t>(a.present_masks)[stripe];
       const uint32_t missing = (~present) & a.full_mask;
-      const uint32_t pid = as_const<uint16_t>(a.lut)[missing];
+      const uint32_t pid = as_const<uint32_t>(a.lut)[missing];
       if (pid == kPlanInvalid) {
         if (lane == 0 && blk == 0) atomicOr(a.status, 1u);
         continue;
@@ -160,11 +209,8 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
     }
     const PlanView pv(plan, K, M);
     const int n_out = static_cast<int>(pv.n_out());
-    const uint32_t col = blk * 64u + lane;
-    const uint32_t off = col * 16u;
+    const uint32_t off = (blk * 64u + lane) * 16u;
     if (n_out == 0 || off >= a.shard_len) continue;
-    const uint8_t* in_base = a.in + static_cast<uint64_t>(stripe) * a.in_stripe_pitch;
-    uint8_t* out_base = a.out + static_cast<uint64_t>(stripe) * a.out_stripe_pitch;
     const uint32_t tail = a.shard_len - off;
 
     for (int r0 = 0; r0 < n_out; r0 += 4) {
@@ -172,7 +218,7 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 #pragma unroll
       for (int q = 0; q < 4; ++q) y[q] = u32x4{0u, 0u, 0u, 0u};
       for (int c = 0; c < K; ++c) {
-        const u32x4 x = load16(in_base + static_cast<uint64_t>(pv.in_idx(c)) * a.shard_pitch + off);
+        const u32x4 x = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
         Idx3 ix[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) ix[d] = split3(x[d]);
@@ -180,15 +226,15 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
         for (int q = 0; q < 4; ++q) {
           if (r0 + q >= n_out) break;
           const RS_CONST uint32_t* tb = pv.tab(r0 + q, c);
-          const uint32_t t0 = tb[0], t1 = tb[1], t2 = tb[2], t3 = tb[3], t4 = tb[4];
+          const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
-          for (int d = 0; d < 4; ++d) y[q][d] ^= lookup3(ix[d], t0, t1, t2, t3, t4);
+          for (int d = 0; d < 4; ++d) y[q][d] ^= lookup3(ix[d], q0, q1, q2, q3, q4);
         }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (r0 + q >= n_out) break;
-        uint8_t* dst = out_base + static_cast<uint64_t>(pv.out_idx(r0 + q)) * a.shard_pitch + off;
+        uint8_t* dst = slot_ptr(a, K, stripe, pv.out_idx(r0 + q)) + off;
         if (tail >= 16u)
           store16(dst, y[q]);
         else
@@ -199,61 +245,134 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 }
 
 // ---------------------------------------------------------------------------
+// Partial last column of every shard (S % 16 != 0) for the specialised kernels:
+// one thread per stripe.  The whole 16-B column lies inside the shard slot
+// (shard_pitch >= round_up(S, 16)), so inputs are read as one 16-B load each;
+// only the nb valid output bytes are stored.  Keeps the main loop branch-free.
+__global__ __launch_bounds__(256) void tail_kernel(const KernelArgs a, int per_stripe) {
+  const uint32_t off = a.full_cols * 16u;
+  const uint32_t nb = a.shard_len - off;  // 1..15
+  const int K = a.k, M = a.m;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_stripes; i += gridDim.x * blockDim.x) {
+    const uint8_t* plan = a.plans;
+    if (per_stripe) {
+      const uint32_t missing = (~a.present_masks[i]) & a.full_mask;
+      const uint32_t pid = a.lut[missing];
+      if (pid == kPlanInvalid) {
+        atomicOr(a.status, 1u);
+        continue;
+      }
+      plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
+    }
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
+    const uint32_t n_out = pw[0];
+    const uint32_t* idx = pw + 2;
+    const uint32_t* tab = reinterpret_cast<const uint32_t*>(plan + plan_tab_offset(K, M));
+    u32x4 y[kMaxM];
+    for (uint32_t r = 0; r < n_out; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
+    for (int c = 0; c < K; ++c) {
+      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, idx[c]) + off);
+      Idx3 ix[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) ix[d] = split3(x[d]);
+      for (uint32_t r = 0; r < n_out; ++r) {
+        const uint32_t* tb = tab + (r * K + c) * 5;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) y[r][d] ^= lookup3(ix[d], tb[0], tb[1], tb[2], tb[3], tb[4]);
+      }
+    }
+    for (uint32_t r = 0; r < n_out; ++r) store_tail(slot_ptr(a, K, i, idx[K + r]) + off, y[r], nb);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Streaming copy (bench only): the measured HBM ceiling next to the RS kernels.
+// Shape from tools/hbm_probe.hip's best: 4 independent 16-B nt loads per lane in
+// flight, 2 workgroups per CU.
 __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                    uint64_t n16) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += stride)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u * 4u;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 1024u + threadIdx.x; base < n16; base += stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256u < n16) v[u] = __builtin_nontemporal_load(src + base + u * 256u);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * 256u < n16) __builtin_nontemporal_store(v[u], dst + base + u * 256u);
+  }
 }
 
 // ---------------------------------------------------------------------------
 // Host-side launch dispatch.
-template <int K, int M>
-static bool try_launch(const KernelArgs& a, int k, int m, bool per_stripe, dim3 grid, hipStream_t s) {
-  if (k != K || m != M) return false;
-  if (per_stripe)
-    hipLaunchKernelGGL((apply_kernel<K, M, true>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((apply_kernel<K, M, false>), grid, dim3(256), 0, s, a);
-  return true;
+template <int K, int M, int E>
+static const void* spec_fn(bool per_stripe) {
+  return per_stripe ? reinterpret_cast<const void*>(&apply_kernel<K, M, E, true>)
+                    : reinterpret_cast<const void*>(&apply_kernel<K, M, E, false>);
 }
 
-const char* launch_apply(const KernelArgs& a, bool per_stripe, uint32_t grid_blocks, hipStream_t s,
-                         bool force_generic) {
-  const dim3 grid(grid_blocks);
-  if (!force_generic) {
-    if (try_launch<4, 2>(a, a.k, a.m, per_stripe, grid, s)) return "apply_kernel<4,2>";
-    if (try_launch<8, 4>(a, a.k, a.m, per_stripe, grid, s)) return "apply_kernel<8,4>";
-    if (try_launch<10, 4>(a, a.k, a.m, per_stripe, grid, s)) return "apply_kernel<10,4>";
-    if (try_launch<6, 3>(a, a.k, a.m, per_stripe, grid, s)) return "apply_kernel<6,3>";
+// Specialised kernels: (K, M, E) with E <= M.
+static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name) {
+#define RS_SPEC(KK, MM, EE)                                  \
+  if (k == KK && m == MM && e == EE) {                       \
+    *name = "apply_kernel<" #KK "," #MM "," #EE ">";         \
+    return spec_fn<KK, MM, EE>(per_stripe);                  \
   }
-  if (per_stripe)
-    hipLaunchKernelGGL((apply_kernel_generic<true>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((apply_kernel_generic<false>), grid, dim3(256), 0, s, a);
-  return "apply_kernel_generic";
+  RS_SPEC(4, 2, 1) RS_SPEC(4, 2, 2)
+  RS_SPEC(8, 4, 1) RS_SPEC(8, 4, 2) RS_SPEC(8, 4, 3) RS_SPEC(8, 4, 4)
+  RS_SPEC(10, 4, 1) RS_SPEC(10, 4, 2) RS_SPEC(10, 4, 3) RS_SPEC(10, 4, 4)
+  RS_SPEC(6, 3, 1) RS_SPEC(6, 3, 2) RS_SPEC(6, 3, 3)
+#undef RS_SPEC
+  return nullptr;
+}
+
+static const void* pick(const KernelArgs& a, int e, bool per_stripe, bool force_generic, bool* spec,
+                        const char** name) {
+  *spec = false;
+  if (!force_generic) {
+    if (const void* f = pick_spec(a.k, a.m, e, per_stripe, name)) {
+      *spec = true;
+      return f;
+    }
+  }
+  *name = "apply_kernel_generic";
+  return per_stripe ? reinterpret_cast<const void*>(&apply_kernel_generic<true>)
+                    : reinterpret_cast<const void*>(&apply_kernel_generic<false>);
+}
+
+int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic) {
+  bool spec;
+  const char* name;
+  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name);
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess || nb < 1) nb = 1;
+  return nb;
+}
+
+const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
+                         hipStream_t s, bool force_generic) {
+  bool spec;
+  const char* name;
+  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name);
+  const uint32_t bps = spec ? a.blocks_full : a.blocks_per_stripe;
+  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
+  if (waves > 0) {
+    const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
+    const uint64_t need = (waves + 3) / 4;
+    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+    void* args[] = {const_cast<KernelArgs*>(&a)};
+    if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
+  }
+  if (spec && a.full_cols * 16u != a.shard_len) {
+    const uint32_t g = (a.n_stripes + 255u) / 256u;
+    hipLaunchKernelGGL(tail_kernel, dim3(g < 4096u ? g : 4096u), dim3(256), 0, s, a, per_stripe ? 1 : 0);
+  }
+  return name;
 }
 
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s) {
   hipLaunchKernelGGL(copy_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
                      static_cast<u32x4*>(dst), bytes / 16);
-}
-
-int apply_kernel_max_blocks_per_cu(int k, int m, bool per_stripe) {
-  int nb = 0;
-  const void* fn = nullptr;
-#define RS_PICK(KK, MM)                                                                          \
-  if (k == KK && m == MM)                                                                        \
-    fn = per_stripe ? reinterpret_cast<const void*>(&apply_kernel<KK, MM, true>)                 \
-                    : reinterpret_cast<const void*>(&apply_kernel<KK, MM, false>);
-  RS_PICK(4, 2) RS_PICK(8, 4) RS_PICK(10, 4) RS_PICK(6, 3)
-#undef RS_PICK
-  if (!fn)
-    fn = per_stripe ? reinterpret_cast<const void*>(&apply_kernel_generic<true>)
-                    : reinterpret_cast<const void*>(&apply_kernel_generic<false>);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess || nb < 1) nb = 1;
-  return nb;
 }
 
 }  // namespace rs

@@ -55,28 +55,37 @@ struct PlanView {
   }
 };
 
+// Shard slot s of stripe i lives at
+//   s <  k : data   + i*data_sp   + s*shard_pitch
+//   s >= k : parity + i*parity_sp + (s-k)*shard_pitch
+// (a unified K+M-slot layout is parity = data + k*shard_pitch, parity_sp = data_sp).
 struct KernelArgs {
-  const uint8_t* in;
-  uint8_t* out;
-  uint64_t in_stripe_pitch;
-  uint64_t out_stripe_pitch;
+  uint8_t* data;
+  uint8_t* parity;
+  uint64_t data_sp;
+  uint64_t parity_sp;
   uint64_t shard_pitch;
   uint32_t shard_len;
   uint32_t n_stripes;
-  uint32_t blocks_per_stripe;  // ceil(ceil(S/16) / 64)
+  uint32_t blocks_per_stripe;  // ceil(ceil(S/16) / 64): all columns (generic kernel)
+  uint32_t full_cols;          // S / 16: full 16-B columns
+  uint32_t blocks_full;        // ceil(full_cols / 64) (specialised kernels)
   int32_t k, m;
   uint32_t full_mask;          // (1 << (k+m)) - 1
   uint32_t plan_bytes;
   const uint8_t* plans;            // uniform plan, or plan array (PER_STRIPE)
   const uint32_t* present_masks;   // PER_STRIPE: bit s = shard s present
-  const uint16_t* lut;             // PER_STRIPE: missing mask -> plan index
+  const uint32_t* lut;             // PER_STRIPE: missing mask -> plan index
   uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards
+  uint8_t* scratch;                // 256 KiB sink for stores that must not land
 };
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
-const char* launch_apply(const KernelArgs& a, bool per_stripe, uint32_t grid_blocks,
-                         hipStream_t s, bool force_generic);
+// e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or
+// nullptr if the launch failed.
+const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
+                         uint32_t cu_count, hipStream_t s, bool force_generic);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
-int apply_kernel_max_blocks_per_cu(int k, int m, bool per_stripe);
+int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic);
 
 }  // namespace rs

@@ -1,0 +1,157 @@
+// ec_service.hpp -- C++ mirror of the reference's internal/ec package over the
+// C-ABI in include/rsgpu.h (header-only; link librsgpu.so).
+//
+// Reference surface, name for name (Go has no toolchain in this image, so the host
+// layer above the C-ABI is C++; INTEGRATION.md has the cgo shim for Go):
+//   internal/ec/ec.go:15-17   type Service struct { driver reedsolomon.Encoder }
+//   internal/ec/ec.go:21-44   func NewService() interfaces.IEcDriver
+//   internal/ec/ec.go:48-50   Split(data []byte) ([][]byte, error)
+//   internal/ec/ec.go:54-56   Encode(shards [][]byte) error
+//   internal/ec/ec.go:59-61   Reconstruct(shards [][]byte) error
+//   internal/interfaces/interfaces.go:41-52  IEcDriver
+// Go's [][]byte is Shards (a vector of byte vectors, empty == nil); Go's error is
+// Error (0 == nil) whose message is klauspost's sentinel text (rs_strerror).
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+
+namespace ec {
+
+constexpr int K = 4;  // internal/config/config.go:21
+constexpr int M = 2;  // internal/config/config.go:22
+
+using Shard = std::vector<uint8_t>;
+using Shards = std::vector<Shard>;
+
+// Go-style error value: code 0 is nil.
+struct Error {
+  int code = RS_OK;
+  explicit operator bool() const { return code != RS_OK; }
+  std::string Message() const { return rs_strerror(code); }
+  const char* c_str() const { return rs_strerror(code); }
+};
+
+// interfaces.IEcDriver (interfaces.go:41-52)
+class IEcDriver {
+ public:
+  virtual ~IEcDriver() = default;
+  virtual Error Split(const uint8_t* data, size_t len, Shards* out) = 0;
+  virtual Error Encode(Shards& shards) = 0;
+  virtual Error Reconstruct(Shards& shards) = 0;
+};
+
+class Service final : public IEcDriver {
+ public:
+  // ec.go:21 NewService(): RS(K, M) on the MI355X engine.  Unlike the reference
+  // (which can only fail on bad K/M and then log.Fatalf, ec.go:27-29), this can also
+  // report a missing GPU; the caller decides.
+  static std::unique_ptr<Service> NewService(int k = K, int m = M, int device = 0, Error* err = nullptr) {
+    rs_ctx* ctx = nullptr;
+    const int rc = rs_create(k, m, device, 0, &ctx);
+    if (err) err->code = rc;
+    if (rc != RS_OK) return nullptr;
+    std::fprintf(stderr, "[EC Driver] Reed-Solomon k=%d m=%d on %s\n", k, m, rs_backend(ctx));
+    return std::unique_ptr<Service>(new Service(ctx, k, m));
+  }
+  ~Service() override { rs_destroy(ctx_); }
+  Service(const Service&) = delete;
+  Service& operator=(const Service&) = delete;
+
+  int DataShards() const { return k_; }
+  int ParityShards() const { return m_; }
+  rs_ctx* ctx() const { return ctx_; }
+
+  // [upstream reedsolomon.go Split]: perShard = ceil(len/K); data shards carry the
+  // payload zero-padded to K*perShard, parity shards are zeroed.  (Go aliases the
+  // caller's buffer; the bytes are identical.)
+  Error Split(const uint8_t* data, size_t len, Shards* out) override {
+    if (len == 0) return Error{RS_ERR_SHORT_DATA};
+    const size_t S = rs_shard_size(ctx_, len);
+    out->assign(static_cast<size_t>(k_ + m_), Shard(S, 0));
+    for (int i = 0; i < k_; ++i) {
+      const size_t off = static_cast<size_t>(i) * S;
+      if (off < len) {
+        const size_t n = len - off < S ? len - off : S;
+        std::copy(data + off, data + off + n, (*out)[i].begin());
+      }
+    }
+    return Error{};
+  }
+
+  Error Encode(Shards& shards) override {
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      p[i] = shards[i].empty() ? nullptr : shards[i].data();
+      n[i] = shards[i].size();
+    }
+    return Error{rs_encode(ctx_, p.data(), n.data())};
+  }
+
+  // Fills every empty (nil) entry, data and parity (readservice.go:285 and
+  // poller.go:282 rely on it).
+  Error Reconstruct(Shards& shards) override { return reconstruct(shards, false); }
+  Error ReconstructData(Shards& shards) { return reconstruct(shards, true); }
+
+  // [upstream Verify]
+  Error Verify(const Shards& shards, bool* ok) {
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      p[i] = const_cast<uint8_t*>(shards[i].data());
+      n[i] = shards[i].size();
+    }
+    int v = 0;
+    Error e{rs_verify(ctx_, p.data(), n.data(), &v)};
+    *ok = v != 0;
+    return e;
+  }
+
+ private:
+  Service(rs_ctx* c, int k, int m) : ctx_(c), k_(k), m_(m) {}
+
+  Error reconstruct(Shards& shards, bool data_only) {
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    size_t S = 0;
+    for (const Shard& s : shards)
+      if (!s.empty()) {
+        S = s.size();
+        break;
+      }
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    std::vector<Shard> fresh(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      if (shards[i].empty()) {
+        fresh[i].assign(S ? S : 1, 0);  // Go: make([]byte, shardSize)
+        p[i] = fresh[i].data();
+        n[i] = 0;
+      } else {
+        p[i] = shards[i].data();
+        n[i] = shards[i].size();
+      }
+    }
+    Error e{data_only ? rs_reconstruct_data(ctx_, p.data(), n.data()) : rs_reconstruct(ctx_, p.data(), n.data())};
+    if (e) return e;
+    for (size_t i = 0; i < shards.size(); ++i)
+      if (shards[i].empty() && n[i] == S && S > 0) {
+        fresh[i].resize(S);
+        shards[i] = std::move(fresh[i]);
+      }
+    return e;
+  }
+
+  rs_ctx* ctx_;
+  int k_, m_;
+};
+
+}  // namespace ec

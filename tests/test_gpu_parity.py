@@ -199,7 +199,7 @@ def test_batch_encode_separate_parity_buffer(engines):
     P = shard_pitch_for(S)
     data = _rand_batch(torch, N, k, P, seed=5)
     parity = torch.full((N, m, P), 0xAB, dtype=torch.uint8, device="cuda")
-    eng.encode_batch(data, parity, S, P, N, k * P, m * P)
+    eng.encode(data, parity, S, N, P, k * P, m * P)
     torch.cuda.synchronize()
     uni = np.zeros((N, k + m, P), np.uint8)
     uni[:, :k] = data.cpu().numpy()
@@ -299,12 +299,12 @@ def test_batch_host_paths_match_device(engines):
     torch.cuda.synchronize()
     eng.host_register(host)
     try:
-        eng.encode_host(host, S, P, N)
+        eng.encode_host_unified(host, S, P, N)
         assert np.array_equal(host[:, :, :S], buf.cpu().numpy()[:, :, :S])
         orig = host.copy()
         host[:, 0, :S] = 0
         host[:, 3, :S] = 0
-        eng.reconstruct_host(host, S, P, N, 0b110110)
+        eng.reconstruct_host_unified(host, S, P, N, 0b110110)
         assert np.array_equal(host[:, :, :S], orig[:, :, :S])
         rng = np.random.default_rng(5)
         masks = np.array([0b111111 & ~(1 << rng.integers(0, 6)) for _ in range(N)], np.uint32)
@@ -312,7 +312,7 @@ def test_batch_host_paths_match_device(engines):
             for j in range(6):
                 if not (masks[i] >> j) & 1:
                     host[i, j, :S] = 0
-        eng.reconstruct_host(host, S, P, N, masks)
+        eng.reconstruct_host_unified(host, S, P, N, masks)
         assert np.array_equal(host[:, :, :S], orig[:, :, :S])
     finally:
         eng.host_unregister(host)
@@ -346,3 +346,91 @@ def test_config2_full_size_roundtrip(engines):
     eng.reconstruct_unified(buf, S, P, N, masks)
     torch.cuda.synchronize()
     assert torch.equal(buf[:, :, :S], orig[:, :, :S])
+
+
+# ---- split layout (data region + parity region): the bench layout -------------------
+def _masks_upto(rng, N, t, m):
+    masks = np.full(N, (1 << t) - 1, np.uint32)
+    for i in range(N):
+        for j in rng.choice(t, size=rng.integers(0, m + 1), replace=False):
+            masks[i] &= ~np.uint32(1 << int(j))
+    return masks
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (10, 4), (6, 3), (12, 4)])
+@pytest.mark.parametrize("S", [7, 1000, 1024, 6554])
+def test_split_layout_device(engines, k, m, S):
+    import torch
+
+    eng = eng_for(engines, k, m)
+    N = 777
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S + 17 * k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((N, m, P), 0xEE, dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    torch.cuda.synchronize()
+    uni = np.zeros((N, k + m, P), np.uint8)
+    uni[:, :k] = data.cpu().numpy()
+    rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
+    par = parity.cpu().numpy()
+    assert np.array_equal(par[:, :, :S], uni[:, k:, :S])
+    assert (par[:, :, S:] == 0xEE).all(), "slot padding must never be written"
+    # per-stripe erasures (0..m per stripe), host masks then device masks
+    rng = np.random.default_rng(S * 3 + k)
+    t = k + m
+    for use_dev in (False, True):
+        masks = _masks_upto(rng, N, t, m)
+        lost = ((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0
+        d2, p2 = data.clone(), parity.clone()
+        dl = torch.from_numpy(lost[:, :k]).cuda()
+        pl = torch.from_numpy(lost[:, k:]).cuda()
+        d2[:, :, :S][dl] = 0x33
+        p2[:, :, :S][pl] = 0x33
+        if use_dev and t <= 16:
+            eng.reconstruct_devmask(d2, p2, S, N, torch.from_numpy(masks.view(np.int32)).cuda())
+            eng.sync()
+        elif not use_dev:
+            if t > 16:
+                # per-stripe patterns need the k+m <= 16 LUT: one uniform pattern instead
+                one = np.uint32(((1 << t) - 1) & ~0b101)
+                d2[:, 0, :S] = 0x33
+                d2[:, 2, :S] = 0x33
+                eng.reconstruct(d2, p2, S, N, one)
+            else:
+                eng.reconstruct(d2, p2, S, N, masks)
+        torch.cuda.synchronize()
+        assert torch.equal(d2[:, :, :S], data[:, :, :S])
+        assert torch.equal(p2[:, :, :S], parity[:, :, :S])
+
+
+@pytest.mark.parametrize("S", [1024, 1000])
+def test_split_layout_host(engines, S):
+    k, m = 4, 2
+    eng = eng_for(engines, k, m)
+    N = 3000
+    P = S  # host layout: shards back to back (the Split view), no padding
+    rng = np.random.default_rng(S)
+    data = rng.integers(0, 256, (N, k, P), dtype=np.uint8)
+    parity = np.zeros((N, m, P), np.uint8)
+    eng.host_register(data)
+    eng.host_register(parity)
+    try:
+        eng.encode_host(data, parity, S, N)
+        uni = np.concatenate([data, np.zeros_like(parity)], axis=1).copy()
+        rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
+        assert np.array_equal(parity, uni[:, k:])
+        d0, p0 = data.copy(), parity.copy()
+        data[:, 1] = 0
+        parity[:, 0] = 0
+        eng.reconstruct_host(data, parity, S, N, 0b101101)
+        assert np.array_equal(data, d0) and np.array_equal(parity, p0)
+        masks = _masks_upto(rng, N, 6, 2)
+        lost = ((masks[:, None] >> np.arange(6)[None, :]) & 1) == 0
+        data[lost[:, :4]] = 0
+        parity[lost[:, 4:]] = 0
+        eng.reconstruct_host(data, parity, S, N, masks)
+        assert np.array_equal(data, d0) and np.array_equal(parity, p0)
+    finally:
+        eng.host_unregister(data)
+        eng.host_unregister(parity)

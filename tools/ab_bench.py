@@ -1,0 +1,112 @@
+"""A/B kernel variants and occupancy in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24).  Prints HBM GB/s (algorithmic bytes /
+event-timed kernel time) per (workload, variant, blocks/CU).
+
+Usage: python tools/ab_bench.py [--rounds 3] [--quick]
+"""
+import argparse
+import itertools
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--bpc", default="1,2,3,4,8")
+    ap.add_argument("--variants", default="0")
+    ap.add_argument("--workloads", default="all")
+    args = ap.parse_args()
+    import torch
+
+    from replication_erasurecoding_object_store_amd.batch import BatchEngine, shard_pitch_for
+
+    GiB = 1 << 30
+    workloads = {
+        # name: (k, m, S, N, mode)  mode: enc | rec2u (uniform {0,1}) | rec2p (per-stripe 2-erasure)
+        "rs42_4K_enc": (4, 2, 1024, 65536, "enc"),
+        "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
+        "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
+        "rs42_64K_enc": (4, 2, 16384, 16384, "enc"),
+        "rs42_64K_rec2p": (4, 2, 16384, 16384, "rec2p"),
+        "rs104_64K_enc": (10, 4, 6554, 16384, "enc"),
+        "rs104_64K_rec2p": (10, 4, 6554, 16384, "rec2p"),
+        "rs84_64K_enc": (8, 4, 8192, 16384, "enc"),
+    }
+    if args.workloads != "all":
+        workloads = {k: v for k, v in workloads.items() if k in args.workloads.split(",")}
+    variants = [int(v) for v in args.variants.split(",")]
+    bpcs = [int(b) for b in args.bpc.split(",")]
+    results = {}
+    engines = {}
+    for name, (k, m, S, N, mode) in workloads.items():
+        if (k, m) not in engines:
+            engines[(k, m)] = BatchEngine(k, m, 0)
+        eng = engines[(k, m)]
+        t = k + m
+        P = shard_pitch_for(S)
+        nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))
+        g = torch.Generator(device="cuda").manual_seed(1)
+        bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
+                 torch.empty((N, m, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
+        for d, p in bufs:
+            eng.encode(d, p, S, N)
+        rng = np.random.default_rng(3)
+        pairs = np.array(list(itertools.combinations(range(t), 2)))
+        masks_np = []
+        for _ in range(nb):
+            ch = pairs[rng.integers(0, len(pairs), N)]
+            masks_np.append(((1 << t) - 1 & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32))
+        masks = [torch.from_numpy(mm.view(np.int32)).cuda() for mm in masks_np]
+        alg = N * S * (k + (m if mode == "enc" else 2))
+
+        def run(i):
+            d, p = bufs[i % nb]
+            if mode == "enc":
+                eng.encode(d, p, S, N)
+            elif mode == "rec2u":
+                eng.reconstruct(d, p, S, N, ((1 << t) - 1) & ~3)
+            else:
+                eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
+
+        for rnd in range(args.rounds):
+            for v in variants:
+                for bpc in bpcs:
+                    eng.set_blocks_per_cu(bpc)
+                    for i in range(2):
+                        run(i)
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for i in range(args.iters):
+                        run(i)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / args.iters
+                    results.setdefault((name, v, bpc), []).append(alg / (ms * 1e-3) / 1e9)
+                    kname = eng.last_kernel()
+        eng.sync()
+        # correctness spot check after all variants: stripes reconstruct to the encoded bytes
+        d, p = bufs[0]
+        chk = torch.empty_like(p[:256])
+        eng.set_blocks_per_cu(0)
+        eng.encode(d[:256], chk, S, 256)
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(chk[:, :, :S], p[:256, :, :S]))
+        for v in variants:
+            for bpc in bpcs:
+                r = results[(name, v, bpc)]
+                print(f"{name:18s} v{v} bpc={bpc:2d}: median {np.median(r):7.1f} GB/s  max {np.max(r):7.1f}  "
+                      f"({np.median(r) / 8000 * 100:4.1f}% of 8 TB/s)  {kname if v == variants[-1] else ''}", flush=True)
+        print(f"{name:18s} parity-consistent after all runs: {ok}", flush=True)
+        del bufs, masks
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
