@@ -73,7 +73,7 @@ def make_batches(torch, n_batches, N, k, m, P, seed):
     return out
 
 
-def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofline_reps=20):
+def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofline_reps=20, barrier=lambda: None):
     """Step = encode the batch + reconstruct 2 erased shards per stripe (seeded
     per-stripe pattern, device-resident masks).  Returns the step time, and each
     kernel's average launch duration from `roofline_reps` back-to-back launches
@@ -103,11 +103,14 @@ def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofli
         enc(i)
         rec(i)
     torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
         enc(i)
         rec(i)
     torch.cuda.synchronize()
+    barrier()
     dt = time.perf_counter() - t0
     eng.sync()
     kernel_ms = {}
@@ -232,18 +235,14 @@ def main():
     args = parse()
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
+    from replication_erasurecoding_object_store_amd import dist as rdist
+    from replication_erasurecoding_object_store_amd.batch import BatchEngine
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    rank, local, world = rdist.world()
+    if world > 1:
+        rdist.init("nccl")  # RCCL; control collectives only (barrier, max time)
     else:
         torch.cuda.set_device(0)
-
-    from replication_erasurecoding_object_store_amd.batch import BatchEngine
 
     k, m = args.k, args.m
     S = args.stripe_kib * 1024 // k
@@ -251,17 +250,11 @@ def main():
     eng = BatchEngine(k, m, torch.cuda.current_device())
     rotate = int(args.rotate_gib * GiB)
 
-    if world > 1:
-        dist.barrier()
-    res = measure_rs(torch, eng, k, m, S, N, args.steps, args.warmup, rotate, seed=0x5EED0002 + rank)
-    dt = res["dt"]
-    if world > 1:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-        okt = torch.tensor([1 if res["ok"] else 0], dtype=torch.int32, device="cuda")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        res["ok"] = bool(okt.item())
+    # weak scaling: every rank owns its own N-stripe batches (independent objects)
+    res = measure_rs(torch, eng, k, m, S, N, args.steps, args.warmup, rotate, seed=0x5EED0002 + rank,
+                     barrier=rdist.barrier)
+    dt = rdist.max_over_ranks(res["dt"])
+    res["ok"] = rdist.all_true(res["ok"])
     user_bytes_per_step = 2 * N * k * S
     value = world * args.steps * user_bytes_per_step / dt / GiB
     ms_step = dt / args.steps * 1e3
@@ -272,7 +265,7 @@ def main():
     achieved = alg[dom] / (km.get(dom, float("nan")) * 1e-3) / 1e9 if km else None
     traffic = None
     pmc = pmc_traffic()
-    if pmc and pmc.get("workload") == f"rs{k}{m}_{args.stripe_kib}KiB_N{N}":
+    if pmc and pmc.get("workload") == f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split":
         traffic = pmc.get("hbm_bytes_per_launch", {}).get(dom)
 
     out = {
@@ -342,9 +335,7 @@ def main():
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
     eng.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    rdist.shutdown()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,157 @@
+//go:build rsgpu
+
+// Package ec, GPU build: a drop-in for internal/ec/ec.go that keeps the package
+// surface (NewService, Split, Encode, Reconstruct; interfaces.IEcDriver) and runs
+// the GF(2^8) arithmetic in librsgpu.so (MI355X / gfx950 HIP kernels) through the
+// C-ABI in include/rsgpu.h.  Build with:  CGO_ENABLED=1 go build -tags rsgpu ./...
+// (NOT compiled in this repo's image: there is no Go toolchain; see INTEGRATION.md.)
+package ec
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../third_party/rsgpu/include
+#cgo LDFLAGS: -L${SRCDIR}/../../third_party/rsgpu/lib -lrsgpu -Wl,-rpath,/opt/rsgpu/lib
+#include <stdlib.h>
+#include "rsgpu.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"log"
+	"runtime"
+	"unsafe"
+
+	"github.com/klauspost/reedsolomon"
+
+	"hybrid_distributed_store/internal/config"
+	"hybrid_distributed_store/internal/interfaces"
+)
+
+// Service implements interfaces.IEcDriver on the GPU engine (ec.go:15-17).
+type Service struct {
+	ctx *C.rs_ctx
+}
+
+// Keep klauspost's exported sentinels so errors.Is and %v output match ec.go.
+func toErr(rc C.int) error {
+	switch rc {
+	case C.RS_OK:
+		return nil
+	case C.RS_ERR_TOO_FEW_SHARDS:
+		return reedsolomon.ErrTooFewShards
+	case C.RS_ERR_SHARD_NO_DATA:
+		return reedsolomon.ErrShardNoData
+	case C.RS_ERR_SHARD_SIZE:
+		return reedsolomon.ErrShardSize
+	case C.RS_ERR_SHORT_DATA:
+		return reedsolomon.ErrShortData
+	case C.RS_ERR_INV_SHARD_NUM:
+		return reedsolomon.ErrInvShardNum
+	case C.RS_ERR_MAX_SHARD_NUM:
+		return reedsolomon.ErrMaxShardNum
+	case C.RS_ERR_NOT_SUPPORTED:
+		return reedsolomon.ErrNotSupported
+	default:
+		return errors.New(C.GoString(C.rs_strerror(rc)))
+	}
+}
+
+// NewService replaces reedsolomon.New(config.K, config.M, ...) at ec.go:26.
+func NewService() interfaces.IEcDriver {
+	log.Println("--- Initializing EC Driver (Reed-Solomon, MI355X) ---")
+	var ctx *C.rs_ctx
+	if rc := C.rs_create(C.int(config.K), C.int(config.M), 0, 0, &ctx); rc != C.RS_OK {
+		log.Fatalf("Failed to create Reed-Solomon encoder: %v", toErr(rc))
+	}
+	log.Printf("EC Driver loaded (k=%d, m=%d) on %s\n", config.K, config.M, C.GoString(C.rs_backend(ctx)))
+	return &Service{ctx: ctx}
+}
+
+// Split keeps klauspost's semantics in Go (no arithmetic): data shards alias
+// `data`, the short last shard and all parity shards are fresh zeroed slices.
+func (s *Service) Split(data []byte) ([][]byte, error) {
+	if len(data) == 0 {
+		return nil, reedsolomon.ErrShortData
+	}
+	k, total := config.K, config.K+config.M
+	perShard := (len(data) + k - 1) / k
+	dst := make([][]byte, total)
+	i := 0
+	for ; i < total && len(data) >= perShard; i++ {
+		dst[i] = data[:perShard:perShard]
+		data = data[perShard:]
+	}
+	for ; i < total; i++ {
+		b := make([]byte, perShard)
+		copy(b, data)
+		data = data[min(len(data), perShard):]
+		dst[i] = b
+	}
+	return dst, nil
+}
+
+// shardArgs builds C arrays of shard pointers and lengths.  Every Go pointer
+// handed to C is pinned for the duration of the call and never retained.
+func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, func()) {
+	n := len(shards)
+	ptrs := (*[1 << 16]*C.uint8_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:n:n]
+	lens := (*[1 << 16]C.size_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.size_t(0)))))[:n:n]
+	for i, sh := range shards {
+		ptrs[i], lens[i] = nil, C.size_t(len(sh))
+		if cap(sh) > 0 {
+			p := &sh[:cap(sh)][0]
+			pin.Pin(p)
+			ptrs[i] = (*C.uint8_t)(unsafe.Pointer(p))
+		}
+	}
+	return &ptrs[0], &lens[0], func() { C.free(unsafe.Pointer(&ptrs[0])); C.free(unsafe.Pointer(&lens[0])) }
+}
+
+// Encode fills shards[K:] in place (ec.go:54-56).
+func (s *Service) Encode(shards [][]byte) error {
+	if len(shards) != config.K+config.M {
+		return reedsolomon.ErrTooFewShards
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	p, l, free := shardArgs(shards, &pin)
+	defer free()
+	return toErr(C.rs_encode(s.ctx, p, l))
+}
+
+// Reconstruct fills every empty entry, data and parity (ec.go:59-61;
+// readservice.go:285 and poller.go:282 rely on all nil entries being filled).
+func (s *Service) Reconstruct(shards [][]byte) error {
+	if len(shards) != config.K+config.M {
+		return reedsolomon.ErrTooFewShards
+	}
+	size := 0
+	for _, sh := range shards {
+		if len(sh) > 0 {
+			size = len(sh)
+			break
+		}
+	}
+	if size == 0 {
+		return reedsolomon.ErrShardNoData
+	}
+	for i := range shards {
+		if len(shards[i]) == 0 && cap(shards[i]) < size {
+			shards[i] = make([]byte, 0, size) // storage for the engine; len 0 = missing
+		}
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	p, l, free := shardArgs(shards, &pin)
+	defer free()
+	lens := unsafe.Slice(l, len(shards))
+	if err := toErr(C.rs_reconstruct(s.ctx, p, l)); err != nil {
+		return err
+	}
+	for i := range shards {
+		if len(shards[i]) == 0 && int(lens[i]) == size {
+			shards[i] = shards[i][:size]
+		}
+	}
+	return nil
+}

@@ -1,0 +1,83 @@
+"""One process per GPU over torch.distributed (RCCL on ROCm; gloo for CPU tests).
+
+Stripes are independent objects: a batch is split into contiguous
+near-equal stripe ranges, one per rank, with NO data-path collective.  The only
+collectives are control: a barrier around timed regions, the max of per-rank
+elapsed times, and the AND of per-rank parity checks.
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+
+def world() -> Tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torchrun environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init(backend: str = "nccl") -> None:
+    import torch
+    import torch.distributed as dist
+
+    rank, local, ws = world()
+    if ws <= 1 or dist.is_initialized():
+        return
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        dist.init_process_group(backend)
+
+
+def stripe_range(n_stripes: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous [begin, end) share of a batch for `rank` (sizes differ by <= 1)."""
+    base, extra = divmod(n_stripes, world_size)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def _device():
+    import torch
+    import torch.distributed as dist
+
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def barrier() -> None:
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def max_over_ranks(x: float) -> float:
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_true(flag: bool) -> bool:
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return flag
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def shutdown() -> None:
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
