@@ -72,6 +72,24 @@ class LibraryMissing(RuntimeError):
     pass
 
 
+def _preload_torch_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm bundles its own libamdhip64 /
+    libhsa-runtime64 (soname libamdhip64.so.7).  If librsgpu.so is loaded first its
+    dependency resolves to /opt/rocm's copy, torch later maps its own, and the two
+    HSA runtimes fight over the device: whichever initialises second sees no GPU
+    (measured: tools/runtime_probe.py).  Loading torch's runtime first makes
+    librsgpu.so's libamdhip64.so.7 dependency bind to it.  No-op without torch
+    (C++/Go callers use /opt/rocm's runtime)."""
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib() -> ctypes.CDLL:
     """Load librsgpu.so (raises LibraryMissing if it was not built)."""
     global _lib
@@ -80,6 +98,7 @@ def lib() -> ctypes.CDLL:
             if not os.path.exists(LIB_PATH):
                 raise LibraryMissing(
                     f"{LIB_PATH} not found: run __graft_entry__.build() (no CPU fallback exists)")
+            _preload_torch_hip_runtime()
             handle = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(handle, name)

@@ -108,3 +108,13 @@ def test_product_never_imports_the_oracle():
     assert "rso_" not in out
     ldd = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "rs_oracle" not in ldd
+
+
+def test_single_hip_runtime_per_process():
+    """librsgpu.so must share torch's bundled HIP runtime, never map a second one
+    (two HSA runtimes in one process: the later one sees no GPU)."""
+    code = ("from replication_erasurecoding_object_store_amd import _lib; _lib.lib(); import torch; "
+            "print(sorted({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}))")
+    out = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT, check=True).stdout
+    libs = eval(out.strip().splitlines()[-1])
+    assert len(libs) == 1, libs

@@ -32,6 +32,9 @@ def main():
         "rs42_4K_enc": (4, 2, 1024, 65536, "enc"),
         "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
         "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
+        "rs42_4K_rec45p": (4, 2, 1024, 65536, "rec45p"),
+        "rs42_4K_rec45u": (4, 2, 1024, 65536, "rec45u"),
+        "rs42_4K_rec14u": (4, 2, 1024, 65536, "rec14u"),
         "rs42_64K_enc": (4, 2, 16384, 16384, "enc"),
         "rs42_64K_rec2p": (4, 2, 16384, 16384, "rec2p"),
         "rs104_64K_enc": (10, 4, 6554, 16384, "enc"),
@@ -63,6 +66,7 @@ def main():
             ch = pairs[rng.integers(0, len(pairs), N)]
             masks_np.append(((1 << t) - 1 & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32))
         masks = [torch.from_numpy(mm.view(np.int32)).cuda() for mm in masks_np]
+        m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         alg = N * S * (k + (m if mode == "enc" else 2))
 
         def run(i):
@@ -71,6 +75,12 @@ def main():
                 eng.encode(d, p, S, N)
             elif mode == "rec2u":
                 eng.reconstruct(d, p, S, N, ((1 << t) - 1) & ~3)
+            elif mode == "rec45u":
+                eng.reconstruct(d, p, S, N, 0b001111)
+            elif mode == "rec14u":
+                eng.reconstruct(d, p, S, N, 0b101101)
+            elif mode == "rec45p":
+                eng.reconstruct_devmask(d, p, S, N, m45)
             else:
                 eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
 
