@@ -86,6 +86,13 @@ def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofli
     batch_bytes = N * t * P
     nb = max(2, int(np.ceil(rotate_bytes / batch_bytes)))
     bufs = make_batches(torch, nb, N, k, m, P, seed)
+    # reconstruct writes the 2 missing shards of every stripe to a separate output
+    # buffer: the reference's semantics (Reconstruct gives missing entries NEW
+    # slices; the healer writes back only those) and include/rsgpu.h's
+    # rs_reconstruct_batch_out
+    # (device masks: the engine cannot bound #missing on the host, so it requires
+    # room for m outputs per stripe; only the first 2 are written here)
+    outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)]
     rng = np.random.default_rng(0x5EED0003)
     masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(nb)]
     for d, p in bufs:  # make every batch a codeword before timing
@@ -97,7 +104,7 @@ def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofli
 
     def rec(i):
         d, p = bufs[i % nb]
-        eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
+        eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
 
     for i in range(warmup):
         enc(i)
@@ -126,16 +133,17 @@ def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofli
         kernel_ms[name] = e0.elapsed_time(e1) / roofline_reps
         kernel_names[name] = eng.last_kernel()
     eng.sync()
-    # full-size property check: after encode + reconstruct the batch is still a
-    # codeword, i.e. re-encoding a sample reproduces the stored parity
+    # full-size property check on every stripe of two batches: the reconstructed
+    # shards equal the erased originals (encode -> erase 2 -> reconstruct round trip)
     ok = True
     for i in range(min(nb, 2)):
         d, p = bufs[i]
-        chk = torch.empty_like(p[:256])
-        eng.encode(d[:256], chk, S, 256)
-        torch.cuda.synchronize()
-        ok &= bool(torch.equal(chk[:, :, :S], p[:256, :, :S]))
-    del bufs, masks
+        full = torch.cat([d[:, :, :S], p[:, :, :S]], dim=1)
+        mk = masks[i].cpu().numpy().view(np.uint32)
+        lost = torch.from_numpy((((mk[:, None] >> np.arange(t)[None, :]) & 1) == 0)).cuda()
+        want = full[lost].view(N, 2, S)  # missing shards in index order
+        ok &= bool(torch.equal(outs[i][:, :2, :S], want))
+    del bufs, masks, outs
     torch.cuda.empty_cache()
     return {"dt": dt, "steps": steps, "kernel_ms": kernel_ms, "batch_bytes": batch_bytes, "n_batches": nb, "ok": ok,
             "kernels": kernel_names}

@@ -120,6 +120,21 @@ int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *data, size_t data_stripe_
                                  uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
                                  size_t shard_len, size_t n_stripes,
                                  const uint32_t *present_masks_dev, void *stream);
+/* Out-of-place reconstruct (RS_MEM_DEVICE only): the shard buffers are read-only;
+ * the r-th missing shard of stripe i (missing shards in index order, data before
+ * parity) is written to  out + i*out_stripe_pitch + r*shard_pitch.  This is the
+ * reference's own semantics (Reconstruct gives missing entries NEW slices) and the
+ * healer's (it writes back only the missing shards), and it streams faster: writes
+ * that land in the region being read cost ~20 % of HBM throughput on MI355X
+ * (profiles/r01_hbm_probe3.log).  present_masks is a host array of n_masks (1 or
+ * n_stripes) uint32, or with masks_on_device != 0 a device array of n_stripes
+ * (k+m <= 16; errors deferred to rs_sync).  out_stripe_pitch >= (#missing,
+ * at most m) * shard_pitch, multiple of 16. */
+int rs_reconstruct_batch_out(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch,
+                             const uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
+                             size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
+                             size_t n_masks, int masks_on_device, uint8_t *out,
+                             size_t out_stripe_pitch, void *stream);
 /* Wait for `stream` and return any deferred device-side error. */
 int rs_sync(rs_ctx *ctx, void *stream);
 

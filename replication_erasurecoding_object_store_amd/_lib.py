@@ -56,6 +56,7 @@ SIGNATURES = {
     "rs_encode_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _i, _vp]),
     "rs_reconstruct_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _u32p, _sz, _i, _vp]),
     "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
+    "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
     "rs_sync": (_i, [_vp, _vp]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),

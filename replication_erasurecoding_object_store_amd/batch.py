@@ -8,7 +8,7 @@ Layouts (include/rsgpu.h):
   split   data [N, K, P] + parity [N, M, P]  -- the fast device layout (two
           sequential streams; object i's K data shards contiguous = its Split view)
   unified one buffer [N, K+M, P]             -- parity = data + K*P
-P (shard pitch) >= S rounded up to 16; :func:`shard_pitch_for` picks 64-B multiples.
+P (shard pitch) >= S rounded up to 16; :func:`shard_pitch_for` picks 256-B multiples.
 """
 from __future__ import annotations
 
@@ -27,9 +27,11 @@ def _check(rc: int) -> None:
 
 
 def shard_pitch_for(shard_len: int) -> int:
-    """Device shard slot: 64-B multiple (16 B is the contract; 64 keeps every
-    wave's 1 KiB column block on whole 64-B lines)."""
-    return (shard_len + 63) // 64 * 64
+    """Device shard slot: 256-B multiple (16 B is the contract).  Slots that start
+    mid-128-B-line make every 1 KiB wave access touch 9 lines instead of 8: a
+    compute-free RS(10+4) stream at S = 6 554 ran 5.65 TB/s with a 6 592-B pitch
+    and 6.30 TB/s with 6 656 (profiles/r01_hbm_probe4.log)."""
+    return (shard_len + 255) // 256 * 256
 
 
 def _stream_handle(stream=None) -> ctypes.c_void_p:
@@ -75,6 +77,23 @@ class BatchEngine(Service):
         _check(_lib.lib().rs_reconstruct_batch_devmask(self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(),
                                                        self.m * P, P, shard_len, n_stripes, masks_dev.data_ptr(),
                                                        _stream_handle(stream)))
+
+    def reconstruct_out(self, data, parity, out, shard_len: int, n_stripes: int, present_masks=None,
+                        masks_dev=None, shard_pitch: Optional[int] = None, stream=None) -> None:
+        """Out-of-place: the r-th missing shard of stripe i goes to out[i, r].
+        `present_masks` (host: int or uint32 array) or `masks_dev` (device tensor)."""
+        P = shard_pitch or data.shape[-1]
+        osp = out.shape[-2] * out.shape[-1] if out.dim() == 3 else self.m * P
+        if masks_dev is not None:
+            mptr, n, on_dev = ctypes.c_void_p(masks_dev.data_ptr()), n_stripes, 1
+            keep = None
+        else:
+            keep = _masks(present_masks)
+            mptr, n, on_dev = ctypes.c_void_p(keep.ctypes.data), keep.size, 0
+        _check(_lib.lib().rs_reconstruct_batch_out(self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(),
+                                                   self.m * P, P, shard_len, n_stripes, mptr, n, on_dev,
+                                                   out.data_ptr(), osp, _stream_handle(stream)))
+        del keep
 
     # ---- device-resident, unified layout ------------------------------------------
     def encode_unified(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, stream=None) -> None:

@@ -345,7 +345,7 @@ int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_id
   if (lg.rc) return lg.rc;
   Lane* L = lg.lane;
   const int t = c->k + c->m;
-  const size_t P = round_up(S, 64);
+  const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t bytes = P * static_cast<size_t>(t);
   if (L->dev.ensure(bytes) || L->host.ensure(bytes)) return RS_ERR_DEVICE;
   uint8_t* h = static_cast<uint8_t*>(L->host.p);
@@ -460,7 +460,7 @@ int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<in
 int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
                size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e) {
   const int k = c->k, m = c->m;
-  const size_t P = round_up(S, 64);
+  const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t per_stripe = P * static_cast<size_t>(k + m) + (masks_host ? 4 : 0);
   const size_t chunk = std::min(N, std::max<size_t>(1, (size_t(64) << 20) / per_stripe));
   HostPipe pipe;
@@ -757,6 +757,54 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
   std::vector<int> all(t);
   for (int i = 0; i < t; ++i) all[i] = i;
   return host_batch(c, L, all, all, S, N, static_cast<const uint8_t*>(c->d_plans.p), masks, max_missing);
+}
+
+int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
+                             size_t shard_pitch, size_t S, size_t N, const uint32_t* masks, size_t n_masks,
+                             int masks_on_device, uint8_t* out, size_t out_sp, void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !masks || !out) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!batch_sizes_ok(S, N, shard_pitch)) return RS_ERR_INVALID_ARG;
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, shard_pitch};
+  if (!device_layout_ok(L, c->m, S) || reinterpret_cast<uintptr_t>(out) % 16 || out_sp % 16) return RS_ERR_INVALID_ARG;
+  const int t = c->k + c->m;
+  const uint32_t full = static_cast<uint32_t>(full_mask64(t));
+  (void)hipSetDevice(c->device);
+  hipStream_t s = as_stream(stream);
+  rs::KernelArgs a = make_args(c, L, S, N);
+  a.out = out;
+  a.out_sp = out_sp;
+  if (masks_on_device) {
+    if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
+    if (out_sp < static_cast<size_t>(c->m) * shard_pitch) return RS_ERR_INVALID_ARG;
+    a.plans = static_cast<const uint8_t*>(c->d_plans.p);
+    a.present_masks = masks;
+    return launch(c, a, c->m, true, s);
+  }
+  if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
+  int max_missing = 0;
+  for (size_t i = 0; i < n_masks; ++i) {
+    const int np = __builtin_popcount(masks[i] & full);
+    if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
+    max_missing = std::max(max_missing, t - np);
+  }
+  if (max_missing == 0) return RS_OK;
+  if (out_sp < static_cast<size_t>(max_missing) * shard_pitch) return RS_ERR_INVALID_ARG;
+  if (n_masks == 1) {
+    const uint8_t* plan = nullptr;
+    int rc = uniform_plan(c, masks[0] & full, false, &plan);
+    if (rc) return rc;
+    a.plans = plan;
+    return launch(c, a, max_missing, false, s);
+  }
+  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
+  const uint32_t* dm = nullptr;
+  int rc = upload_masks(c, masks, N, s, &dm);
+  if (rc) return rc;
+  a.plans = static_cast<const uint8_t*>(c->d_plans.p);
+  a.present_masks = dm;
+  return launch(c, a, max_missing, true, s);
 }
 
 int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,

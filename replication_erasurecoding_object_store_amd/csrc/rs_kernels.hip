@@ -92,6 +92,12 @@ __device__ __forceinline__ uint8_t* slot_ptr(const KernelArgs& a, int k, uint32_
                    static_cast<uint64_t>(s - static_cast<uint32_t>(k)) * a.shard_pitch;
 }
 
+// r-th output of stripe i: in place (its shard slot) or out of place.
+__device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t stripe, uint32_t r, uint32_t slot) {
+  return a.out ? a.out + static_cast<uint64_t>(stripe) * a.out_sp + static_cast<uint64_t>(r) * a.shard_pitch
+               : slot_ptr(a, k, stripe, slot);
+}
+
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
 // #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
@@ -174,7 +180,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t n_out = pv.n_out();
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      uint8_t* real = slot_ptr(a, K, stripe, pv.out_idx(r)) + off;
+      uint8_t* real = out_ptr(a, K, stripe, r, pv.out_idx(r)) + off;
       store16((valid && static_cast<uint32_t>(r) < n_out) ? real : dummy, y[r]);
     }
   }
@@ -234,7 +240,7 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         if (r0 + q >= n_out) break;
-        uint8_t* dst = slot_ptr(a, K, stripe, pv.out_idx(r0 + q)) + off;
+        uint8_t* dst = out_ptr(a, K, stripe, r0 + q, pv.out_idx(r0 + q)) + off;
         if (tail >= 16u)
           store16(dst, y[q]);
         else
@@ -281,7 +287,7 @@ __global__ __launch_bounds__(256) void tail_kernel(const KernelArgs a, int per_s
         for (int d = 0; d < 4; ++d) y[r][d] ^= lookup3(ix[d], tb[0], tb[1], tb[2], tb[3], tb[4]);
       }
     }
-    for (uint32_t r = 0; r < n_out; ++r) store_tail(slot_ptr(a, K, i, idx[K + r]) + off, y[r], nb);
+    for (uint32_t r = 0; r < n_out; ++r) store_tail(out_ptr(a, K, i, r, idx[K + r]) + off, y[r], nb);
   }
 }
 

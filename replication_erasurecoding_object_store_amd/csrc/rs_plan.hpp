@@ -78,6 +78,8 @@ struct KernelArgs {
   const uint32_t* lut;             // PER_STRIPE: missing mask -> plan index
   uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards
   uint8_t* scratch;                // 256 KiB sink for stores that must not land
+  uint8_t* out;                    // null: outputs in place (slot addresses); else the
+  uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
 };
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).

@@ -434,3 +434,49 @@ def test_split_layout_host(engines, S):
     finally:
         eng.host_unregister(data)
         eng.host_unregister(parity)
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (10, 4), (12, 4)])
+@pytest.mark.parametrize("S", [1024, 6554, 100])
+def test_reconstruct_out_of_place(engines, k, m, S):
+    """rs_reconstruct_batch_out: r-th missing shard of stripe i lands in out[i, r];
+    the shard buffers are not written."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    N, t = 513, k + m
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(k * 1000 + S)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    full = torch.cat([data, parity], dim=1)  # [N, t, P]
+    rng = np.random.default_rng(S + k)
+    modes = ["uniform", "host"] + (["dev"] if t <= 16 else [])
+    for mode in modes:
+        if mode == "uniform":
+            miss = sorted(rng.choice(t, size=m, replace=False).tolist())
+            masks = np.full(N, ((1 << t) - 1) & ~sum(1 << j for j in miss), np.uint32)
+        else:
+            masks = _masks_upto(rng, N, t, m)
+            masks[0] = (1 << t) - 1  # a complete stripe: nothing written for it
+        d0, p0 = data.clone(), parity.clone()
+        out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+        if mode == "uniform":
+            eng.reconstruct_out(data, parity, out, S, N, present_masks=masks[0])
+        elif mode == "host":
+            eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
+        else:
+            eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
+            eng.sync()
+        torch.cuda.synchronize()
+        assert torch.equal(data, d0) and torch.equal(parity, p0), "inputs must be read-only"
+        got = out.cpu().numpy()
+        ref = full.cpu().numpy()
+        for i in range(N):
+            missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+            for r, j in enumerate(missing):
+                assert np.array_equal(got[i, r, :S], ref[i, j, :S]), (mode, i, r, j)
+            for r in range(len(missing), m):
+                assert (got[i, r] == 0xC3).all(), "unused output slots untouched"
+        assert (got[:, :, S:] == 0xC3).all()

@@ -33,6 +33,10 @@ def main():
         "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
         "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
         "rs42_4K_rec45p": (4, 2, 1024, 65536, "rec45p"),
+        "rs42_4K_rec2p_out": (4, 2, 1024, 65536, "rec2p_out"),
+        "rs42_4K_rec2u_out": (4, 2, 1024, 65536, "rec2u_out"),
+        "rs42_64K_rec2p_out": (4, 2, 16384, 16384, "rec2p_out"),
+        "rs104_64K_rec2p_out": (10, 4, 6554, 16384, "rec2p_out"),
         "rs42_4K_rec45u": (4, 2, 1024, 65536, "rec45u"),
         "rs42_4K_rec14u": (4, 2, 1024, 65536, "rec14u"),
         "rs42_64K_enc": (4, 2, 16384, 16384, "enc"),
@@ -67,6 +71,7 @@ def main():
             masks_np.append(((1 << t) - 1 & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32))
         masks = [torch.from_numpy(mm.view(np.int32)).cuda() for mm in masks_np]
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
+        outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
         alg = N * S * (k + (m if mode == "enc" else 2))
 
         def run(i):
@@ -81,6 +86,10 @@ def main():
                 eng.reconstruct(d, p, S, N, 0b101101)
             elif mode == "rec45p":
                 eng.reconstruct_devmask(d, p, S, N, m45)
+            elif mode == "rec2p_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
+            elif mode == "rec2u_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=((1 << t) - 1) & ~3)
             else:
                 eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
 
