@@ -204,15 +204,32 @@ def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def link_peak(torch, nbytes=256 << 20):
+    """Pinned host <-> HBM copy rates (the PCIe ceiling the host path works under)."""
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, fn in (("h2d", lambda: d.copy_(h, non_blocking=True)), ("d2h", lambda: h.copy_(d, non_blocking=True))):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+        out[name + "_GBps"] = round(4 * nbytes / (time.perf_counter() - t0) / 1e9, 1)
+    return out
+
+
 def host_e2e(torch, eng, k, m, S, N):
     """Pinned host -> H2D -> kernel -> D2H (split layout, shards back to back as
-    Split produces them): encode, then 1-erasure reconstruct."""
+    Split produces them): encode, then 1-erasure reconstruct.  Rates are user data
+    bytes (N*K*S) per second; the link moves K+M (encode: K in, M out) shards."""
     data = np.random.default_rng(2).integers(0, 256, (N, k, S), dtype=np.uint8)
     parity = np.zeros((N, m, S), np.uint8)
     eng.host_register(data)
     eng.host_register(parity)
     try:
-        eng.encode_host(data, parity, S, N)
+        eng.encode_host(data, parity, S, N)  # pipeline state + first touch of the pinned pages
         t0 = time.perf_counter()
         eng.encode_host(data, parity, S, N)
         t_enc = time.perf_counter() - t0
@@ -224,7 +241,74 @@ def host_e2e(torch, eng, k, m, S, N):
         eng.host_unregister(data)
         eng.host_unregister(parity)
     return {"encode_GiBps": round(N * k * S / t_enc / GiB, 2), "reconstruct1_GiBps": round(N * k * S / t_rec / GiB, 2),
-            "bytes_user": N * k * S}
+            "bytes_user": N * k * S, **link_peak(torch)}
+
+
+def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
+    """N objects, each either encoded (parity missing) or
+    repaired from one erasure (index uniform in [0, k+m)), 50/50 by a seeded draw,
+    in ONE batched call with a present-mask per stripe.  e2e: shards in pinned host
+    memory, H2D + kernel + D2H inside the timed region (rs_reconstruct_batch,
+    RS_MEM_HOST).  device: the same masks on HBM-resident shards."""
+    t = k + m
+    full = (1 << t) - 1
+    rng = np.random.default_rng(seed)
+    is_rec = rng.random(N) < 0.5
+    lost = rng.integers(0, t, N)
+    masks = np.where(is_rec, full & ~(1 << lost), (1 << k) - 1).astype(np.uint32)
+    data = torch.empty((N, k, S), dtype=torch.uint8, pin_memory=True)
+    parity = torch.empty((N, m, S), dtype=torch.uint8, pin_memory=True)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    step = 1 << 16
+    for s0 in range(0, N, step):  # random data + its true parity, made on the GPU
+        n = min(step, N - s0)
+        dd = torch.randint(0, 256, (n, k, S), dtype=torch.uint8, device="cuda", generator=g)
+        pp = torch.empty((n, m, S), dtype=torch.uint8, device="cuda")
+        eng.encode(dd, pp, S, n)
+        data[s0:s0 + n].copy_(dd)
+        parity[s0:s0 + n].copy_(pp)
+    torch.cuda.synchronize()
+    dn, pn = data.numpy(), parity.numpy()
+    sample = rng.choice(N, size=min(N, 4096), replace=False)
+    ref_d, ref_p = dn[sample].copy(), pn[sample].copy()
+    lost_d = (~masks[:, None] >> np.arange(k)[None, :]) & 1
+    lost_p = (~masks[:, None] >> np.arange(k, t)[None, :]) & 1
+
+    def erase():
+        dn[lost_d.astype(bool)] = 0
+        pn[lost_p.astype(bool)] = 0
+
+    erase()
+    eng.reconstruct_host(dn, pn, S, N, masks)  # warm: pipeline slabs, LUT
+    times = []
+    for _ in range(2):
+        erase()
+        t0 = time.perf_counter()
+        eng.reconstruct_host(dn, pn, S, N, masks)
+        times.append(time.perf_counter() - t0)
+    ok = bool(np.array_equal(dn[sample], ref_d) and np.array_equal(pn[sample], ref_p))
+    t_e2e = min(times)
+    # device-resident, same masks, in place
+    dd = data.cuda()
+    pd = parity.cuda()
+    md = torch.from_numpy(masks.view(np.int32)).cuda()
+    eng.reconstruct_devmask(dd, pd, S, N, md)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        eng.reconstruct_devmask(dd, pd, S, N, md)
+    e1.record()
+    torch.cuda.synchronize()
+    t_dev = e0.elapsed_time(e1) / 5 * 1e-3
+    eng.sync()
+    del dd, pd, md, data, parity
+    torch.cuda.empty_cache()
+    user = N * k * S
+    return {"objects": N, "shard_len": S, "encode_frac": round(float((~is_rec).mean()), 4),
+            "e2e_GiBps": round(user / t_e2e / GiB, 2), "e2e_objects_per_s": round(N / t_e2e),
+            "device_GiBps": round(user / t_dev / GiB, 1), "ok_sample": ok,
+            "note": "e2e moves all k+m slots each way (in-place host batch API)"}
 
 
 def pmc_traffic():
@@ -334,7 +418,8 @@ def main():
             }
             e2.close()
         extras["kmsweep_64KiB_device"] = sweep
-        extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 16384)
+        extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 1 << 18)
+        extras["healer_mix_config5"] = healer_mix(torch, eng, k, m, S, 1 << 20)
         out["extras"] = extras
     if rank == 0:
         line = json.dumps(out)

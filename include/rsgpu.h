@@ -135,8 +135,51 @@ int rs_reconstruct_batch_out(rs_ctx *ctx, const uint8_t *data, size_t data_strip
                              size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
                              size_t n_masks, int masks_on_device, uint8_t *out,
                              size_t out_stripe_pitch, void *stream);
+/* Batched parity verify / bit-rot scrub ([upstream reedsolomon.go Verify], per
+ * object: rs_verify).  Recomputes every parity shard from the data shards and
+ * compares it with the stored one: bad[i] = bitmask of stripe i's parity shards
+ * that differ (bit r = parity shard r; 0 = stripe intact).  bad has n_stripes
+ * uint32 in the memory kind `mem` (device: written asynchronously on `stream`;
+ * host: synchronous).  Nothing else is written.  Reads K+M shards per stripe. */
+int rs_verify_batch(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch,
+                    const uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
+                    size_t shard_len, size_t n_stripes, uint32_t *bad, int mem, void *stream);
 /* Wait for `stream` and return any deferred device-side error. */
 int rs_sync(rs_ctx *ctx, void *stream);
+
+/* ---- batch coalescer (per-object calls -> device batches) ------------------
+ * Drop-in for the per-object entry points when many threads call them at once
+ * (one goroutine per request: writeservice.go:218-222, readservice.go:144,285,
+ * poller.go:282).  rs_co_* take exactly the arguments, perform the same checks
+ * and return the same codes as rs_encode / rs_reconstruct / rs_reconstruct_data /
+ * rs_verify, and are synchronous: on return the outputs are in the caller's
+ * buffers and nothing of the caller's is retained.  Concurrent calls with the
+ * same shard length are staged into one batch and run as one device launch (a
+ * batch closes when max_batch slots are taken or max_wait_us after its first
+ * call).  With k+m > 16 only encode and verify coalesce (reconstruct runs the
+ * per-object path).  Thread-safe; the context must outlive the coalescer.
+ * Batching is group commit: a batch starts as soon as fewer than max_exec batches
+ * are on the device (after an optional max_wait_us linger); calls arriving
+ * meanwhile join the open batch, so batch size follows the load and a lone caller
+ * waits for no timer. */
+typedef struct rs_coalescer rs_coalescer;
+typedef struct {
+  size_t max_batch;       /* stripes per batch (0 = 4096) */
+  uint32_t max_wait_us;   /* linger before a batch may start (0 = none) */
+  int inflight;           /* staging batches (0 = 8); each: stream + pinned + device slab */
+  size_t max_batch_bytes; /* staging bytes per batch (0 = 32 MiB) */
+  int max_exec;           /* batches executing at once (0 = 2; <= inflight) */
+} rs_coalescer_opts;
+int rs_coalescer_create(rs_ctx *ctx, const rs_coalescer_opts *opts /* NULL = defaults */,
+                        rs_coalescer **out);
+void rs_coalescer_destroy(rs_coalescer *co);
+int rs_co_encode(rs_coalescer *co, uint8_t *const *shards, const size_t *lens);
+int rs_co_reconstruct(rs_coalescer *co, uint8_t *const *shards, size_t *lens);
+int rs_co_reconstruct_data(rs_coalescer *co, uint8_t *const *shards, size_t *lens);
+int rs_co_verify(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, int *ok);
+/* Counters since creation: calls, device batches, stripes batched, largest batch. */
+int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
+                uint64_t *max_batch);
 
 /* ---- host memory helpers ------------------------------------------------ */
 int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin for async DMA */

@@ -12,6 +12,8 @@ import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librsgpu.so")
+# A/B tooling only (tools/ab_libs.py): load an alternative build of the same ABI.
+LIB_PATH = os.environ.get("RSGPU_LIB", LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "rsgpu.h")
 
 RS_OK = 0
@@ -57,7 +59,15 @@ SIGNATURES = {
     "rs_reconstruct_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _u32p, _sz, _i, _vp]),
     "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
     "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
+    "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
     "rs_sync": (_i, [_vp, _vp]),
+    "rs_coalescer_create": (_i, [_vp, _vp, _vp]),
+    "rs_coalescer_destroy": (None, [_vp]),
+    "rs_co_encode": (_i, [_vp, _u8pp, _szp]),
+    "rs_co_reconstruct": (_i, [_vp, _u8pp, _szp]),
+    "rs_co_reconstruct_data": (_i, [_vp, _u8pp, _szp]),
+    "rs_co_verify": (_i, [_vp, _u8pp, _szp, ctypes.POINTER(_i)]),
+    "rs_co_stats": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),

@@ -95,6 +95,15 @@ class BatchEngine(Service):
                                                    out.data_ptr(), osp, _stream_handle(stream)))
         del keep
 
+    def verify(self, data, parity, bad, shard_len: int, n_stripes: int, shard_pitch: Optional[int] = None,
+               stream=None) -> None:
+        """Scrub: bad [N] int32/uint32 device tensor <- bitmask of mismatching parity
+        shards per stripe (0 = intact).  Asynchronous; nothing else is written."""
+        P = shard_pitch or data.shape[-1]
+        _check(_lib.lib().rs_verify_batch(self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(), self.m * P, P,
+                                          shard_len, n_stripes, bad.data_ptr(), _lib.RS_MEM_DEVICE,
+                                          _stream_handle(stream)))
+
     # ---- device-resident, unified layout ------------------------------------------
     def encode_unified(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, stream=None) -> None:
         """buf: [n_stripes, k+m, shard_pitch] uint8 device tensor; fills parity slots."""
@@ -152,6 +161,15 @@ class BatchEngine(Service):
         base = buf.ctypes.data
         _check(_lib.lib().rs_reconstruct_batch(self.ctx, base, sp, base + self.k * shard_pitch, sp, shard_pitch,
                                                shard_len, n_stripes, _u32p(m), m.size, _lib.RS_MEM_HOST, None))
+
+    def verify_host(self, data: np.ndarray, parity: np.ndarray, shard_len: int, n_stripes: int,
+                    shard_pitch: Optional[int] = None) -> np.ndarray:
+        """Host-resident scrub: returns uint32 [N] mismatch bitmasks."""
+        P = shard_pitch or data.shape[-1]
+        bad = np.empty(n_stripes, np.uint32)
+        _check(_lib.lib().rs_verify_batch(self.ctx, data.ctypes.data, self.k * P, parity.ctypes.data, self.m * P, P,
+                                          shard_len, n_stripes, bad.ctypes.data, _lib.RS_MEM_HOST, None))
+        return bad
 
     def host_register(self, arr: np.ndarray) -> None:
         _check(_lib.lib().rs_host_register(self.ctx, arr.ctypes.data, arr.nbytes))

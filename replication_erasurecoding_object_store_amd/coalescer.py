@@ -1,0 +1,44 @@
+"""IEcDriver over the batch coalescer (include/rsgpu.h rs_coalescer_*, rs_co_*).
+
+Same surface and error behaviour as :class:`ec.Service` -- Split / Encode /
+Reconstruct / ReconstructData / Verify, internal/ec/ec.go:48-61 -- but concurrent
+callers with the same shard length share one device launch (SURVEY.md §8f rank
+1: callers stay unchanged while the GPU sees batches).  ctypes releases the GIL
+for the duration of a foreign call, so Python threads really do call in
+concurrently, as the reference's request goroutines do.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from .ec import M, K, Service, _check
+
+
+class CoalescerOpts(ctypes.Structure):
+    _fields_ = [("max_batch", ctypes.c_size_t), ("max_wait_us", ctypes.c_uint32), ("inflight", ctypes.c_int),
+                ("max_batch_bytes", ctypes.c_size_t), ("max_exec", ctypes.c_int)]
+
+
+class CoalescingService(Service):
+    def __init__(self, k: int = K, m: int = M, device: int = 0, max_batch: int = 0, max_wait_us: int = 0,
+                 inflight: int = 0, max_batch_bytes: int = 0, max_exec: int = 0):
+        super().__init__(k, m, device)
+        opts = CoalescerOpts(max_batch, max_wait_us, inflight, max_batch_bytes, max_exec)
+        co = ctypes.c_void_p()
+        _check(_lib.lib().rs_coalescer_create(self._ctx, ctypes.byref(opts), ctypes.byref(co)))
+        self._co = co
+
+    def _call(self, op: str, *args) -> int:
+        return getattr(_lib.lib(), "rs_co_" + op)(self._co, *args)
+
+    def stats(self) -> dict:
+        v = [ctypes.c_uint64() for _ in range(4)]
+        _check(_lib.lib().rs_co_stats(self._co, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("calls", "batches", "stripes", "max_batch"), (x.value for x in v)))
+
+    def close(self) -> None:
+        if getattr(self, "_co", None):
+            _lib.lib().rs_coalescer_destroy(self._co)
+            self._co = None
+        super().close()

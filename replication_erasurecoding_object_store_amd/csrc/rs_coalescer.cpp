@@ -1,0 +1,397 @@
+// rs_coalescer.cpp -- batch coalescer behind the per-object IEcDriver calls
+// (SURVEY.md §8f rank 1).
+//
+// The reference calls Encode / Reconstruct once per object from a goroutine per
+// HTTP request (writeservice.go:218-222,382-386; readservice.go:144,285; healer
+// workers poller.go:282).  One object is a few KiB to a few MiB -- far too little
+// to fill an MI355X, and each call alone pays a full H2D -> kernel -> D2H round
+// trip.  The coalescer keeps the per-object contract (same arguments, same checks
+// and error codes as rs_encode / rs_reconstruct / rs_reconstruct_data / rs_verify)
+// but parks concurrent calls with the same shard length in one staging batch and
+// runs the batch as ONE device launch:
+//
+//   caller i:  validate -> reserve slot i of the open batch for its S -> copy its
+//              shards into the batch's pinned staging (callers copy in parallel)
+//   leader  :  the batch's first caller waits until the batch is full or
+//              max_wait_us has passed, closes it, then moves it:
+//              H2D (data [n,K,P] (+ parity [n,M,P] if a reconstruct needs it) +
+//              masks) -> rs_reconstruct_batch_out with per-stripe masks (an encode
+//              is the pattern "all parity missing") or rs_verify_batch -> D2H
+//   caller i:  copies its outputs out of the staging batch and returns.
+//
+// Up to `inflight` batches exist at once (each with its own stream, pinned and
+// device slab), so one batch's transfers overlap the next batch's filling.  All
+// arithmetic is the device kernels'; the host only moves bytes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "../../include/rsgpu.h"
+#include "rs_host_util.hpp"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+enum class Kind : int { kApply = 0, kVerify = 1 };
+
+struct Batch {
+  enum class State { kFree, kOpen, kClosed, kDone };
+  State state = State::kFree;
+  Kind kind = Kind::kApply;
+  size_t S = 0, P = 0, cap = 0;
+  size_t reserved = 0, filled = 0, released = 0;
+  bool parity_in = false;  // some slot needs its parity shards uploaded
+  int rc = RS_OK;
+  Clock::time_point deadline;
+  std::condition_variable done_cv;  // followers: batch finished
+  hipStream_t stream = nullptr;
+  rs::PinnedBuf host;
+  rs::DevBuf dev;
+  // region offsets (same in host staging and device slab)
+  size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_bad = 0, bytes = 0;
+};
+
+}  // namespace
+
+struct rs_coalescer {
+  rs_ctx* ctx = nullptr;
+  int k = 0, m = 0, device = 0;
+  bool per_stripe = false;  // k+m <= 16: per-stripe masks (reconstruct coalesces)
+  size_t max_batch = 0, max_bytes = 0;
+  std::chrono::microseconds max_wait{0};
+
+  int max_exec = 2;   // batches on the device at once
+  int executing = 0;
+
+  std::mutex mu;
+  std::condition_variable free_cv;    // a batch became free (or opened)
+  std::condition_variable leader_cv;  // batch full / staged / an execution slot freed
+  std::vector<std::unique_ptr<Batch>> batches;
+  std::vector<Batch*> free_list;
+  std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots
+
+  std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
+
+  ~rs_coalescer() {
+    for (auto& b : batches)
+      if (b->stream) (void)hipStreamDestroy(b->stream);
+  }
+};
+
+namespace {
+
+using rs::round_up;
+
+uint8_t* host_at(Batch* b, size_t off) { return static_cast<uint8_t*>(b->host.p) + off; }
+uint8_t* dev_at(Batch* b, size_t off) { return static_cast<uint8_t*>(b->dev.p) + off; }
+
+// Lays out a batch for (kind, S) and makes sure its buffers are large enough.
+int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
+  const size_t k = co->k, m = co->m;
+  b->kind = kind;
+  b->S = S;
+  b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
+  (void)hipSetDevice(co->device);
+  const size_t per = b->P * (k + 2 * m) + 8;
+  b->cap = std::max<size_t>(1, std::min(co->max_batch, co->max_bytes / per));
+  b->o_data = 0;
+  b->o_parity = round_up(b->cap * k * b->P, 256);
+  b->o_out = b->o_parity + round_up(b->cap * m * b->P, 256);
+  b->o_masks = b->o_out + round_up(b->cap * m * b->P, 256);
+  b->o_bad = b->o_masks + round_up(b->cap * 4, 256);
+  b->bytes = b->o_bad + round_up(b->cap * 4, 256);
+  if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
+  b->reserved = b->filled = b->released = 0;
+  b->parity_in = false;
+  b->rc = RS_OK;
+  b->state = Batch::State::kOpen;
+  b->deadline = Clock::now() + co->max_wait;
+  return RS_OK;
+}
+
+// Runs a closed batch of n slots on its stream and waits for the outputs.
+int execute(rs_coalescer* co, Batch* b, size_t n) {
+  const size_t k = co->k, m = co->m, P = b->P;
+  (void)hipSetDevice(co->device);
+  hipStream_t st = b->stream;
+  RS_HIP(hipMemcpyAsync(dev_at(b, b->o_data), host_at(b, b->o_data), n * k * P, hipMemcpyHostToDevice, st));
+  if (b->parity_in || b->kind == Kind::kVerify)
+    RS_HIP(hipMemcpyAsync(dev_at(b, b->o_parity), host_at(b, b->o_parity), n * m * P, hipMemcpyHostToDevice, st));
+  int rc;
+  if (b->kind == Kind::kVerify) {
+    rc = rs_verify_batch(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_parity), m * P, P, b->S, n,
+                         reinterpret_cast<uint32_t*>(dev_at(b, b->o_bad)), RS_MEM_DEVICE, st);
+    if (rc) return rc;
+    RS_HIP(hipMemcpyAsync(host_at(b, b->o_bad), dev_at(b, b->o_bad), n * 4, hipMemcpyDeviceToHost, st));
+  } else {
+    if (co->per_stripe) {
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
+      rc = rs_reconstruct_batch_out(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_parity), m * P, P, b->S, n,
+                                    reinterpret_cast<const uint32_t*>(dev_at(b, b->o_masks)), n, 1,
+                                    dev_at(b, b->o_out), m * P, st);
+    } else {  // encode-only batches (k+m > 16): parity straight into the out region
+      rc = rs_encode_batch(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_out), m * P, P, b->S, n,
+                           RS_MEM_DEVICE, st);
+    }
+    if (rc) return rc;
+    RS_HIP(hipMemcpyAsync(host_at(b, b->o_out), dev_at(b, b->o_out), n * m * P, hipMemcpyDeviceToHost, st));
+  }
+  RS_HIP(hipStreamSynchronize(st));
+  return RS_OK;  // every mask was checked (>= k present) before it was staged
+}
+
+// One call through the coalescer.  fill(b, slot) stages the inputs, drain(b, slot)
+// copies the outputs back; both run outside the lock, in the caller's thread.
+//
+// Batching is group commit: a batch's leader starts it as soon as an execution slot
+// is free (at most max_exec batches on the device at once) and max_wait has passed
+// since the batch opened (default 0).  Callers that arrive while earlier batches
+// are on the device pile into the open batch, so batches grow with the load and a
+// lone caller pays no timer.
+template <class Fill, class Drain>
+int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, Drain&& drain) {
+  co->calls.fetch_add(1, std::memory_order_relaxed);
+  std::unique_lock<std::mutex> lk(co->mu);
+  const auto key = std::make_pair(static_cast<int>(kind), S);
+  Batch* b = nullptr;
+  for (;;) {
+    auto it = co->open.find(key);
+    if (it != co->open.end()) {
+      b = it->second;
+      break;
+    }
+    if (!co->free_list.empty()) {
+      b = co->free_list.back();
+      co->free_list.pop_back();
+      const int rc = prepare(co, b, kind, S);
+      if (rc) {
+        b->state = Batch::State::kFree;
+        co->free_list.push_back(b);
+        co->free_cv.notify_all();
+        return rc;
+      }
+      co->open[key] = b;
+      co->free_cv.notify_all();  // waiters for this S may join it
+      break;
+    }
+    co->free_cv.wait(lk);  // every batch is in flight: back-pressure
+  }
+  const size_t slot = b->reserved++;
+  const bool leader = slot == 0;
+  b->parity_in |= parity_in;
+  if (b->reserved == b->cap) {  // full: no more slots
+    co->open.erase(key);
+    b->state = Batch::State::kClosed;
+    co->leader_cv.notify_all();
+  }
+  lk.unlock();
+  fill(b, slot);
+  lk.lock();
+  if (++b->filled == b->reserved && b->state != Batch::State::kOpen) co->leader_cv.notify_all();
+  if (leader) {
+    // gather: until full, or (an execution slot is free and the linger is over)
+    for (;;) {
+      if (b->state != Batch::State::kOpen) break;
+      const bool slot_free = co->executing < co->max_exec;
+      if (slot_free && Clock::now() >= b->deadline) break;
+      if (slot_free)
+        co->leader_cv.wait_until(lk, b->deadline);
+      else
+        co->leader_cv.wait(lk);
+    }
+    if (b->state == Batch::State::kOpen) {
+      auto it = co->open.find(key);
+      if (it != co->open.end() && it->second == b) co->open.erase(it);
+      b->state = Batch::State::kClosed;
+    }
+    while (b->filled < b->reserved || co->executing >= co->max_exec) co->leader_cv.wait(lk);
+    ++co->executing;
+    const size_t n = b->reserved;
+    lk.unlock();
+    const int rc = execute(co, b, n);
+    co->n_batches.fetch_add(1, std::memory_order_relaxed);
+    co->stripes.fetch_add(n, std::memory_order_relaxed);
+    uint64_t seen = co->max_seen.load(std::memory_order_relaxed);
+    while (n > seen && !co->max_seen.compare_exchange_weak(seen, n)) {
+    }
+    lk.lock();
+    --co->executing;
+    co->leader_cv.notify_all();  // an execution slot is free
+    b->rc = rc;
+    b->state = Batch::State::kDone;
+    b->done_cv.notify_all();
+  } else {
+    while (b->state != Batch::State::kDone) b->done_cv.wait(lk);
+  }
+  const int rc = b->rc;
+  lk.unlock();
+  if (rc == RS_OK) drain(b, slot);
+  lk.lock();
+  if (++b->released == b->reserved) {
+    b->state = Batch::State::kFree;
+    co->free_list.push_back(b);
+    co->free_cv.notify_all();
+  }
+  return rc;
+}
+
+// Reconstruct / ReconstructData through the coalescer; semantics of
+// reconstruct_impl in rs_engine.cpp ([upstream reedsolomon.go reconstruct]).
+int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool data_only) {
+  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+  const int k = co->k, m = co->m, t = k + m;
+  if (!co->per_stripe)
+    return data_only ? rs_reconstruct_data(co->ctx, shards, lens) : rs_reconstruct(co->ctx, shards, lens);
+  size_t S = 0;
+  int rc = rs::check_shards(t, lens, true, &S);
+  if (rc) return rc;
+  uint32_t present = 0;
+  int np = 0, data_present = 0;
+  bool parity_used = false;
+  for (int i = 0; i < t; ++i)
+    if (lens[i]) {
+      present |= 1u << i;
+      ++np;
+      if (i < k) ++data_present;
+    }
+  if (np == t || (data_only && data_present == k)) return RS_OK;
+  if (np < k) return RS_ERR_TOO_FEW_SHARDS;
+  if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
+  int used = 0;  // survivors = first k present shards (the kernel reads those)
+  for (int i = 0; i < t && used < k; ++i)
+    if (lens[i]) {
+      ++used;
+      if (i >= k) parity_used = true;
+    }
+  for (int i = 0; i < t; ++i)
+    if (!lens[i] && (!data_only || i < k) && !shards[i]) return RS_ERR_INVALID_ARG;
+  auto fill = [&](Batch* b, size_t slot) {
+    const size_t P = b->P;
+    for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
+      if (!lens[i]) continue;
+      ++staged;
+      uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P)
+                           : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
+      std::memcpy(dst, shards[i], S);
+    }
+    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = present;
+  };
+  auto drain = [&](Batch* b, size_t slot) {
+    int r = 0;  // r-th missing shard (index order, data before parity) = out slot r
+    for (int i = 0; i < t; ++i) {
+      if (lens[i]) continue;
+      if (!data_only || i < k) {
+        std::memcpy(shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+        lens[i] = S;
+      }
+      ++r;
+    }
+  };
+  return submit(co, Kind::kApply, S, parity_used, fill, drain);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer** out) {
+  if (!ctx || !out) return RS_ERR_INVALID_ARG;
+  *out = nullptr;
+  rs_coalescer_opts o{4096, 0, 8, size_t(32) << 20, 2};
+  if (opts) {
+    if (opts->max_batch) o.max_batch = opts->max_batch;
+    o.max_wait_us = opts->max_wait_us;
+    if (opts->inflight > 0) o.inflight = opts->inflight;
+    if (opts->max_batch_bytes) o.max_batch_bytes = opts->max_batch_bytes;
+    if (opts->max_exec > 0) o.max_exec = opts->max_exec;
+  }
+  if (o.inflight > 64 || o.max_exec > o.inflight) return RS_ERR_INVALID_ARG;
+  auto co = std::make_unique<rs_coalescer>();
+  co->ctx = ctx;
+  co->k = rs_data_shards(ctx);
+  co->m = rs_parity_shards(ctx);
+  co->device = rs_device(ctx);
+  co->per_stripe = co->k + co->m <= 16;
+  co->max_batch = o.max_batch;
+  co->max_bytes = o.max_batch_bytes;
+  co->max_wait = std::chrono::microseconds(o.max_wait_us);
+  co->max_exec = o.max_exec;
+  for (int i = 0; i < o.inflight; ++i) {
+    co->batches.push_back(std::make_unique<Batch>());
+    co->free_list.push_back(co->batches.back().get());
+  }
+  *out = co.release();
+  return RS_OK;
+}
+
+void rs_coalescer_destroy(rs_coalescer* co) { delete co; }
+
+int rs_co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens) {
+  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+  const int k = co->k, m = co->m;
+  size_t S = 0;
+  int rc = rs::check_shards(k + m, lens, false, &S);
+  if (rc) return rc;
+  if (m == 0) return RS_OK;
+  for (int i = 0; i < k + m; ++i)
+    if (!shards[i]) return RS_ERR_INVALID_ARG;
+  if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
+  const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
+  auto fill = [&](Batch* b, size_t slot) {
+    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+  };
+  auto drain = [&](Batch* b, size_t slot) {
+    for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+  };
+  return submit(co, Kind::kApply, S, false, fill, drain);
+}
+
+int rs_co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens) {
+  return co_reconstruct(co, shards, lens, false);
+}
+
+int rs_co_reconstruct_data(rs_coalescer* co, uint8_t* const* shards, size_t* lens) {
+  return co_reconstruct(co, shards, lens, true);
+}
+
+int rs_co_verify(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, int* ok) {
+  if (!co || !shards || !lens || !ok) return RS_ERR_INVALID_ARG;
+  const int k = co->k, m = co->m;
+  size_t S = 0;
+  int rc = rs::check_shards(k + m, lens, false, &S);
+  if (rc) return rc;
+  *ok = 1;
+  if (m == 0) return RS_OK;
+  for (int i = 0; i < k + m; ++i)
+    if (!shards[i]) return RS_ERR_INVALID_ARG;
+  if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
+  auto fill = [&](Batch* b, size_t slot) {
+    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    for (int r = 0; r < m; ++r) std::memcpy(host_at(b, b->o_parity + (slot * m + r) * b->P), shards[k + r], S);
+  };
+  auto drain = [&](Batch* b, size_t slot) { *ok = reinterpret_cast<uint32_t*>(host_at(b, b->o_bad))[slot] == 0; };
+  return submit(co, Kind::kVerify, S, true, fill, drain);
+}
+
+int rs_co_stats(rs_coalescer* co, uint64_t* calls, uint64_t* batches, uint64_t* stripes, uint64_t* max_batch) {
+  if (!co) return RS_ERR_INVALID_ARG;
+  if (calls) *calls = co->calls.load();
+  if (batches) *batches = co->n_batches.load();
+  if (stripes) *stripes = co->stripes.load();
+  if (max_batch) *max_batch = co->max_seen.load();
+  return RS_OK;
+}
+
+}  // extern "C"

@@ -29,18 +29,17 @@
 
 #include "../../include/rsgpu.h"
 #include "gf256.hpp"
+#include "rs_host_util.hpp"
 #include "rs_plan.hpp"
 
 namespace {
 
 using rs::Matrix;
 
-#define RS_HIP(expr)                                \
-  do {                                              \
-    if ((expr) != hipSuccess) return RS_ERR_DEVICE; \
-  } while (0)
-
-size_t round_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+using rs::check_shards;
+using rs::DevBuf;
+using rs::PinnedBuf;
+using rs::round_up;
 
 // Default workgroups (256 threads) per CU for the batched kernels, measured with
 // tools/ab_bench.py on MI355X (profiles/r01_ab_occupancy.log): the streaming
@@ -122,40 +121,6 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
 }
 
 // ---- buffers -------------------------------------------------------------------
-struct DevBuf {
-  void* p = nullptr;
-  size_t n = 0;
-  int ensure(size_t bytes) {
-    if (bytes <= n) return RS_OK;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    if (hipMalloc(&p, bytes) != hipSuccess) return RS_ERR_DEVICE;
-    n = bytes;
-    return RS_OK;
-  }
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
-  }
-};
-
-struct PinnedBuf {
-  void* p = nullptr;
-  size_t n = 0;
-  int ensure(size_t bytes) {
-    if (bytes <= n) return RS_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    n = 0;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return RS_ERR_DEVICE;
-    n = bytes;
-    return RS_OK;
-  }
-  ~PinnedBuf() {
-    if (p) (void)hipHostFree(p);
-  }
-};
-
 // A lane serves one synchronous host call at a time.
 struct Lane {
   hipStream_t stream = nullptr;
@@ -187,6 +152,23 @@ struct Layout {
 
 }  // namespace
 
+// ---- host batch pipeline state ---------------------------------------------------
+// Chunks of stripes flow H2D -> kernel -> D2H on kHostStreams streams; each stream
+// has its own device slab (split layout), so chunk j+1's copies overlap chunk j's
+// kernel and D2H.  Kept in the context: creating streams and slabs per call cost
+// more than a small call's transfers.
+constexpr int kHostStreams = 4;
+constexpr size_t kHostChunkBytes = size_t(16) << 20;  // device bytes per chunk
+
+struct HostPipe {
+  hipStream_t st[kHostStreams] = {};
+  DevBuf buf[kHostStreams];
+  ~HostPipe() {
+    for (auto& s : st)
+      if (s) (void)hipStreamDestroy(s);
+  }
+};
+
 struct rs_ctx {
   int k = 0, m = 0, device = 0, cu_count = 0;
   int blocks_per_cu = kDefaultBlocksPerCu;
@@ -212,8 +194,12 @@ struct rs_ctx {
   int max_lanes = 8;
 
   std::mutex upload_mu;
-  std::vector<UploadSlot> uploads;
+  static constexpr size_t kUploadSlots = 4;
+  UploadSlot uploads[kUploadSlots];
   size_t upload_next = 0;
+
+  std::mutex host_mu;             // host-resident batches: one at a time per context
+  HostPipe host_pipe;
 
   std::atomic<const char*> last_kernel{"none"};
 
@@ -256,6 +242,17 @@ int launch(rs_ctx* c, const rs::KernelArgs& a, int e, bool per_stripe, hipStream
   const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, e);
   const char* name = rs::launch_apply(a, e, per_stripe, static_cast<uint32_t>(bpc),
                                       static_cast<uint32_t>(c->cu_count), s, c->force_generic);
+  if (!name) return RS_ERR_DEVICE;
+  c->last_kernel.store(name);
+  RS_HIP(hipGetLastError());
+  return RS_OK;
+}
+
+int launch_verify_args(rs_ctx* c, rs::KernelArgs& a, hipStream_t s) {
+  a.plans = static_cast<const uint8_t*>(c->d_enc_plan.p);
+  const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, c->m);
+  const char* name = rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(c->cu_count), s,
+                                       c->force_generic);
   if (!name) return RS_ERR_DEVICE;
   c->last_kernel.store(name);
   RS_HIP(hipGetLastError());
@@ -322,20 +319,6 @@ struct LaneGuard {
 };
 
 // [upstream reedsolomon.go checkShards(shards, nilok)] + shardSize.
-int check_shards(int n, const size_t* lens, bool nilok, size_t* S) {
-  size_t s = 0;
-  for (int i = 0; i < n; ++i)
-    if (lens[i]) {
-      s = lens[i];
-      break;
-    }
-  if (s == 0) return RS_ERR_SHARD_NO_DATA;
-  for (int i = 0; i < n; ++i)
-    if (lens[i] != s && (lens[i] != 0 || !nilok)) return RS_ERR_SHARD_SIZE;
-  *S = s;
-  return RS_OK;
-}
-
 // One object through a lane: pack inputs into pinned staging, H2D, one kernel,
 // D2H of the outputs, unpack.  in/out slots are shard indices into `shards`.
 int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
@@ -417,21 +400,6 @@ bool batch_sizes_ok(size_t S, size_t N, size_t pitch) {
   return N * ((cols + 63) / 64) < 0xFFFFFFFFull;  // task ids fit 32 bits
 }
 
-// ---- host batch pipeline -------------------------------------------------------
-// Chunks of stripes flow H2D -> kernel -> D2H on kStreams streams; each stream has
-// its own device slab (split layout), so chunk j+1's copies overlap chunk j's
-// kernel and D2H.
-constexpr int kStreams = 3;
-
-struct HostPipe {
-  hipStream_t st[kStreams] = {};
-  DevBuf buf[kStreams];
-  ~HostPipe() {
-    for (auto& s : st)
-      if (s) (void)hipStreamDestroy(s);
-  }
-};
-
 hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
                   hipMemcpyKind kind, hipStream_t s) {
   if (rows == 0 || width == 0) return hipSuccess;
@@ -458,21 +426,25 @@ int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<in
 }
 
 int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
-               size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e) {
+               size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e,
+               uint32_t* bad_host = nullptr) {
   const int k = c->k, m = c->m;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
-  const size_t per_stripe = P * static_cast<size_t>(k + m) + (masks_host ? 4 : 0);
-  const size_t chunk = std::min(N, std::max<size_t>(1, (size_t(64) << 20) / per_stripe));
-  HostPipe pipe;
-  for (int i = 0; i < kStreams; ++i) {
-    RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
-    if (pipe.buf[i].ensure(chunk * per_stripe + 256)) return RS_ERR_DEVICE;
+  const size_t per_stripe = P * static_cast<size_t>(k + m) + ((masks_host || bad_host) ? 4 : 0);
+  const size_t chunk = std::min(N, std::max<size_t>(1, kHostChunkBytes / per_stripe));
+  std::lock_guard<std::mutex> g(c->host_mu);
+  HostPipe& pipe = c->host_pipe;
+  for (int i = 0; i < kHostStreams; ++i) {
+    if (!pipe.st[i]) RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
+    // sized for a full chunk whatever N is, so a small call never leaves slabs that
+    // a later large call has to reallocate
+    if (pipe.buf[i].ensure(std::max(kHostChunkBytes, per_stripe) + per_stripe + 256)) return RS_ERR_DEVICE;
   }
   int j = 0;
   for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
     const size_t n = std::min(chunk, N - s0);
-    hipStream_t st = pipe.st[j % kStreams];
-    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kStreams].p);
+    hipStream_t st = pipe.st[j % kHostStreams];
+    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kHostStreams].p);
     const Layout dl{d, P * k, d + chunk * P * k, P * m, P};
     int rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
     if (rc) return rc;
@@ -483,19 +455,26 @@ int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, co
       RS_HIP(hipMemcpyAsync(dm, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
       a.present_masks = dm;
     }
+    if (bad_host) {
+      uint32_t* db = reinterpret_cast<uint32_t*>(d + round_up(chunk * P * (k + m), 256));
+      a.bad = db;
+      rc = launch_verify_args(c, a, st);
+      if (rc) return rc;
+      RS_HIP(hipMemcpyAsync(bad_host + s0, db, n * 4, hipMemcpyDeviceToHost, st));
+      continue;
+    }
     rc = launch(c, a, e, masks_host != nullptr, st);
     if (rc) return rc;
     rc = copy_slots(hl, dl, k, out_slots, s0, 0, n, S, hipMemcpyDeviceToHost, st);
     if (rc) return rc;
   }
-  for (int i = 0; i < kStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
+  for (int i = 0; i < kHostStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
   return RS_OK;
 }
 
 int upload_masks(rs_ctx* c, const uint32_t* masks, size_t n, hipStream_t s, const uint32_t** dev) {
   std::lock_guard<std::mutex> g(c->upload_mu);
-  if (c->uploads.empty()) c->uploads.resize(4);
-  UploadSlot& u = c->uploads[c->upload_next++ % c->uploads.size()];
+  UploadSlot& u = c->uploads[c->upload_next++ % rs_ctx::kUploadSlots];
   if (!u.done) RS_HIP(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
   if (u.used) RS_HIP(hipEventSynchronize(u.done));
   if (u.host.ensure(n * 4) || u.dev.ensure(n * 4)) return RS_ERR_DEVICE;
@@ -805,6 +784,34 @@ int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, con
   a.plans = static_cast<const uint8_t*>(c->d_plans.p);
   a.present_masks = dm;
   return launch(c, a, max_missing, true, s);
+}
+
+int rs_verify_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
+                    size_t shard_pitch, size_t S, size_t N, uint32_t* bad, int mem, void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !bad) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!batch_sizes_ok(S, N, shard_pitch) || reinterpret_cast<uintptr_t>(bad) % 4) return RS_ERR_INVALID_ARG;
+  if (mem != RS_MEM_DEVICE && mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  if (c->m == 0) {  // nothing to verify
+    if (mem == RS_MEM_HOST) {
+      std::memset(bad, 0, N * 4);
+      return RS_OK;
+    }
+    RS_HIP(hipMemsetAsync(bad, 0, N * 4, as_stream(stream)));
+    return RS_OK;
+  }
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, shard_pitch};
+  if (mem == RS_MEM_DEVICE) {
+    if (!device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
+    rs::KernelArgs a = make_args(c, L, S, N);
+    a.bad = bad;
+    return launch_verify_args(c, a, as_stream(stream));
+  }
+  std::vector<int> all(c->k + c->m), none;
+  for (int i = 0; i < c->k + c->m; ++i) all[i] = i;
+  return host_batch(c, L, all, none, S, N, nullptr, nullptr, c->m, bad);
 }
 
 int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,

@@ -35,6 +35,12 @@
 
 namespace rs {
 
+// A/B knob (tools/ab_libs.py): 0 restores one plan base for all of a trip's inputs.
+#ifndef RS_OPAQUE_INPUT_TABLES
+#define RS_OPAQUE_INPUT_TABLES 1
+#endif
+constexpr bool kOpaqueInputTables = RS_OPAQUE_INPUT_TABLES != 0;
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct Idx3 {
@@ -160,9 +166,14 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       Idx3 ix[4];
 #pragma unroll
       for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+      // one opaque base per input: the scalar load merger cannot fuse this
+      // input's table loads with later inputs' (which would pin them in SGPRs)
+      const uint8_t* tcol = plan;
+      if constexpr (kOpaqueInputTables && K * E * 5 > 48) asm volatile("" : "+s"(tcol));
+      const PlanView pc(tcol, K, M);
 #pragma unroll
       for (int r = 0; r < E; ++r) {
-        const RS_CONST uint32_t* tb = pv.tab(r, c);
+        const RS_CONST uint32_t* tb = pc.tab(r, c);
         const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
@@ -292,6 +303,128 @@ __global__ __launch_bounds__(256) void tail_kernel(const KernelArgs a, int per_s
 }
 
 // ---------------------------------------------------------------------------
+// Verify / scrub ([upstream reedsolomon.go Verify]: re-encode and compare; the
+// reference lists bit-rot detection as missing, docs/ARCHITECTURE.md:175-178).
+// Same lookup arithmetic as apply_kernel, but the M stored parity columns are
+// loaded next to the K data columns and nothing is stored: a task ends in one
+// compare per parity row, and only a mismatching lane issues an atomic.  All
+// columns, the partial last one included, run here: a byte mask limits the
+// compare to the shard's S bytes (16-B loads stay inside the shard slot).
+__device__ __forceinline__ uint32_t byte_mask(uint32_t nbytes, int d) {
+  const int v = static_cast<int>(nbytes) - 4 * d;  // valid bytes of dword d
+  return v >= 4 ? 0xFFFFFFFFu : (v <= 0 ? 0u : (1u << (8 * v)) - 1u);
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void verify_kernel(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t bps = a.blocks_per_stripe;
+  const uint32_t ntasks = a.n_stripes * bps;
+  const uint8_t* const plan0 = uniform_ptr(a.plans);
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
+    const uint8_t* plan = plan0;
+    uint64_t pitch = a.shard_pitch;
+    if constexpr (K * M * 5 > 48) {
+      // opaque per trip (see apply_kernel): neither the tables nor the K+M slot
+      // offsets c*pitch may be hoisted into SGPRs for the whole loop
+      asm volatile("" : "+s"(plan));
+      asm volatile("" : "+s"(pitch));
+    }
+    const PlanView pv(plan, K, M);
+    const uint32_t col = blk * 64u + lane;
+    const uint32_t start = col * 16u;
+    const uint32_t nbytes = start < a.shard_len ? min(16u, a.shard_len - start) : 0u;
+    const uint32_t off = nbytes ? start : 0u;
+    const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp + off;
+    const uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + off;
+    u32x4 x[K], st[M];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = load16(dbase + static_cast<uint64_t>(c) * pitch);
+#pragma unroll
+    for (int r = 0; r < M; ++r) st[r] = load16(pbase + static_cast<uint64_t>(r) * pitch);
+    u32x4 y[M], pend[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) y[r] = st[r];  // y = stored ^ recomputed: zero when intact
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      Idx3 ix[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+      // one opaque base per input: the scalar load merger cannot fuse this
+      // input's table loads with later inputs' (which would pin them in SGPRs)
+      const uint8_t* tcol = plan;
+      if constexpr (K * M * 5 > 48) asm volatile("" : "+s"(tcol));
+      const PlanView pc(tcol, K, M);
+#pragma unroll
+      for (int r = 0; r < M; ++r) {
+        const RS_CONST uint32_t* tb = pc.tab(r, c);
+        const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
+          if (c & 1)
+            y[r][d] = xor3(y[r][d], pend[r][d], prod);
+          else if (c == K - 1)
+            y[r][d] ^= prod;
+          else
+            pend[r][d] = prod;
+        }
+      }
+      if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t bits = 0u;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      uint32_t diff = 0u;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) diff |= y[r][d] & byte_mask(nbytes, d);
+      bits |= diff ? (1u << r) : 0u;
+    }
+    if (bits) atomicOr(a.bad + stripe, bits);
+  }
+}
+
+// Runtime K/M variant (shapes without a specialisation).
+__global__ __launch_bounds__(256) void verify_kernel_generic(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t bps = a.blocks_per_stripe;
+  const uint32_t ntasks = a.n_stripes * bps;
+  const int K = a.k, M = a.m;
+  const PlanView pv(a.plans, K, M);
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
+    const uint32_t start = (blk * 64u + lane) * 16u;
+    if (start >= a.shard_len) continue;
+    const uint32_t nbytes = min(16u, a.shard_len - start);
+    const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp + start;
+    const uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + start;
+    uint32_t bits = 0u;
+    for (int r = 0; r < M; ++r) {
+      u32x4 y = load16(pbase + static_cast<uint64_t>(r) * a.shard_pitch);
+      for (int c = 0; c < K; ++c) {
+        const u32x4 x = load16(dbase + static_cast<uint64_t>(c) * a.shard_pitch);
+        const RS_CONST uint32_t* tb = pv.tab(r, c);
+        const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), q0, q1, q2, q3, q4);
+      }
+      uint32_t diff = 0u;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) diff |= y[d] & byte_mask(nbytes, d);
+      bits |= diff ? (1u << r) : 0u;
+    }
+    if (bits) atomicOr(a.bad + stripe, bits);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Streaming copy (bench only): the measured HBM ceiling next to the RS kernels.
 // Shape from tools/hbm_probe.hip's best: 4 independent 16-B nt loads per lane in
 // flight, 2 workgroups per CU.
@@ -373,6 +506,31 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
     const uint32_t g = (a.n_stripes + 255u) / 256u;
     hipLaunchKernelGGL(tail_kernel, dim3(g < 4096u ? g : 4096u), dim3(256), 0, s, a, per_stripe ? 1 : 0);
   }
+  return name;
+}
+
+const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s,
+                          bool force_generic) {
+  const void* fn = nullptr;
+  const char* name = "verify_kernel_generic";
+#define RS_VSPEC(KK, MM)                                                  \
+  if (!fn && a.k == KK && a.m == MM) {                                    \
+    fn = reinterpret_cast<const void*>(&verify_kernel<KK, MM>);           \
+    name = "verify_kernel<" #KK "," #MM ">";                              \
+  }
+  if (!force_generic) {
+    RS_VSPEC(4, 2) RS_VSPEC(8, 4) RS_VSPEC(10, 4) RS_VSPEC(6, 3)
+  }
+#undef RS_VSPEC
+  if (!fn) fn = reinterpret_cast<const void*>(&verify_kernel_generic);
+  if (hipMemsetAsync(a.bad, 0, static_cast<size_t>(a.n_stripes) * 4u, s) != hipSuccess) return nullptr;
+  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  if (waves == 0) return name;
+  const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
+  const uint64_t need = (waves + 3) / 4;
+  const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+  void* args[] = {const_cast<KernelArgs*>(&a)};
+  if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
 }
 

@@ -80,6 +80,7 @@ struct KernelArgs {
   uint8_t* scratch;                // 256 KiB sink for stores that must not land
   uint8_t* out;                    // null: outputs in place (slot addresses); else the
   uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
+  uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
 };
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
@@ -88,6 +89,11 @@ struct KernelArgs {
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s, bool force_generic);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
+// Verify: recompute parity from the data shards (uniform encode plan) and compare
+// with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.
+// a.bad must be zeroed first (launch_verify does it on s).
+const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s,
+                          bool force_generic);
 int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic);
 
 }  // namespace rs

@@ -101,6 +101,10 @@ class Service:
         _check(_lib.lib().rs_encode_matrix(self._ctx, out))
         return [list(out[r * self.k:(r + 1) * self.k]) for r in range(t)]
 
+    def _call(self, op: str, *args) -> int:
+        """Per-object entry point rs_<op> (the coalescing service swaps in rs_co_<op>)."""
+        return getattr(_lib.lib(), "rs_" + op)(self._ctx, *args)
+
     # ---- IEcDriver -------------------------------------------------------------
     def Split(self, data: bytes) -> List[bytearray]:
         """[upstream reedsolomon.go Split]: perShard = ceil(len/K); data shards hold
@@ -119,7 +123,7 @@ class Service:
         if len(shards) != self.k + self.m:
             raise ECError(ErrTooFewShards)
         ptrs, lens, keep = _shard_array(shards, 0, fill_missing=False)
-        _check(_lib.lib().rs_encode(self._ctx, ptrs, lens))
+        _check(self._call("encode", ptrs, lens))
         del keep
 
     def _reconstruct(self, shards: List[Optional[bytearray]], data_only: bool) -> None:
@@ -127,8 +131,7 @@ class Service:
             raise ECError(ErrTooFewShards)
         S = next((len(s) for s in shards if s is not None and len(s) > 0), 0)
         ptrs, lens, keep = _shard_array(shards, S, fill_missing=True)
-        fn = _lib.lib().rs_reconstruct_data if data_only else _lib.lib().rs_reconstruct
-        _check(fn(self._ctx, ptrs, lens))
+        _check(self._call("reconstruct_data" if data_only else "reconstruct", ptrs, lens))
         for i, sh in enumerate(shards):
             if (sh is None or len(sh) == 0) and lens[i] == S and S > 0:
                 shards[i] = bytearray(ctypes.string_at(ptrs[i], S))
@@ -147,7 +150,7 @@ class Service:
             raise ECError(ErrTooFewShards)
         ptrs, lens, keep = _shard_array(shards, 0, fill_missing=False)
         ok = ctypes.c_int(0)
-        _check(_lib.lib().rs_verify(self._ctx, ptrs, lens, ctypes.byref(ok)))
+        _check(self._call("verify", ptrs, lens, ctypes.byref(ok)))
         del keep
         return bool(ok.value)
 

@@ -60,7 +60,23 @@ class Service final : public IEcDriver {
     std::fprintf(stderr, "[EC Driver] Reed-Solomon k=%d m=%d on %s\n", k, m, rs_backend(ctx));
     return std::unique_ptr<Service>(new Service(ctx, k, m));
   }
-  ~Service() override { rs_destroy(ctx_); }
+  // The same driver with concurrent per-object calls merged into device batches
+  // (rs_coalescer_*).  Callers see no difference.
+  static std::unique_ptr<Service> NewCoalescingService(int k = K, int m = M, int device = 0,
+                                                       const rs_coalescer_opts* opts = nullptr,
+                                                       Error* err = nullptr) {
+    std::unique_ptr<Service> s = NewService(k, m, device, err);
+    if (!s) return s;
+    const int rc = rs_coalescer_create(s->ctx_, opts, &s->co_);
+    if (err) err->code = rc;
+    if (rc != RS_OK) return nullptr;
+    return s;
+  }
+  ~Service() override {
+    if (co_) rs_coalescer_destroy(co_);
+    rs_destroy(ctx_);
+  }
+  rs_coalescer* coalescer() const { return co_; }
   Service(const Service&) = delete;
   Service& operator=(const Service&) = delete;
 
@@ -93,7 +109,7 @@ class Service final : public IEcDriver {
       p[i] = shards[i].empty() ? nullptr : shards[i].data();
       n[i] = shards[i].size();
     }
-    return Error{rs_encode(ctx_, p.data(), n.data())};
+    return Error{co_ ? rs_co_encode(co_, p.data(), n.data()) : rs_encode(ctx_, p.data(), n.data())};
   }
 
   // Fills every empty (nil) entry, data and parity (readservice.go:285 and
@@ -111,7 +127,7 @@ class Service final : public IEcDriver {
       n[i] = shards[i].size();
     }
     int v = 0;
-    Error e{rs_verify(ctx_, p.data(), n.data(), &v)};
+    Error e{co_ ? rs_co_verify(co_, p.data(), n.data(), &v) : rs_verify(ctx_, p.data(), n.data(), &v)};
     *ok = v != 0;
     return e;
   }
@@ -140,7 +156,12 @@ class Service final : public IEcDriver {
         n[i] = shards[i].size();
       }
     }
-    Error e{data_only ? rs_reconstruct_data(ctx_, p.data(), n.data()) : rs_reconstruct(ctx_, p.data(), n.data())};
+    int rc;
+    if (co_)
+      rc = data_only ? rs_co_reconstruct_data(co_, p.data(), n.data()) : rs_co_reconstruct(co_, p.data(), n.data());
+    else
+      rc = data_only ? rs_reconstruct_data(ctx_, p.data(), n.data()) : rs_reconstruct(ctx_, p.data(), n.data());
+    Error e{rc};
     if (e) return e;
     for (size_t i = 0; i < shards.size(); ++i)
       if (shards[i].empty() && n[i] == S && S > 0) {
@@ -151,6 +172,7 @@ class Service final : public IEcDriver {
   }
 
   rs_ctx* ctx_;
+  rs_coalescer* co_ = nullptr;
   int k_, m_;
 };
 

@@ -140,6 +140,30 @@ static void test_concurrent(ec::Service& svc) {
   for (int f : fails) CHECK(f == 0);
 }
 
+// 16 callers, batch of 16, generous wait: all 16 land in ONE device batch (the
+// batch closes because it is full, not because the timer fired).
+static void test_coalesces_exactly() {
+  rs_coalescer_opts opts{16, 2000000, 2, 0};
+  ec::Error err;
+  auto co = ec::Service::NewCoalescingService(ec::K, ec::M, 0, &opts, &err);
+  CHECK(co != nullptr);
+  if (!co) return;
+  std::vector<std::thread> ts;
+  std::vector<int> fails(16, 0);
+  for (int t = 0; t < 16; ++t)
+    ts.emplace_back([&, t] {
+      const std::vector<uint8_t> v = rand_bytes(5000 + t, 4096);
+      ec::Shards sh;
+      if (co->Split(v.data(), v.size(), &sh) || co->Encode(sh)) ++fails[t];
+      if (sh != oracle_encode(ec::K, ec::M, sh)) ++fails[t];
+    });
+  for (auto& th : ts) th.join();
+  for (int f : fails) CHECK(f == 0);
+  uint64_t calls = 0, batches = 0, stripes = 0, maxb = 0;
+  CHECK(rs_co_stats(co->coalescer(), &calls, &batches, &stripes, &maxb) == RS_OK);
+  CHECK(calls == 16 && batches == 1 && stripes == 16 && maxb == 16);
+}
+
 int main() {
   ec::Error err;
   auto svc = ec::Service::NewService(ec::K, ec::M, 0, &err);
@@ -152,6 +176,24 @@ int main() {
   test_healer_all_patterns(*svc);
   test_errors(*svc);
   test_concurrent(*svc);
+  // the same flows through the batch coalescer (small batches + short wait so the
+  // full-batch and timed-close paths both run)
+  rs_coalescer_opts opts{8, 300, 3, 0};
+  auto co = ec::Service::NewCoalescingService(ec::K, ec::M, 0, &opts, &err);
+  CHECK(co != nullptr);
+  if (co) {
+    test_write_then_degraded_read(*co);
+    test_healer_all_patterns(*co);
+    test_errors(*co);
+    test_concurrent(*co);
+    uint64_t calls = 0, batches = 0, stripes = 0, maxb = 0;
+    CHECK(rs_co_stats(co->coalescer(), &calls, &batches, &stripes, &maxb) == RS_OK);
+    std::printf("coalescer: %llu calls, %llu batches, %llu stripes, largest batch %llu\n",
+                (unsigned long long)calls, (unsigned long long)batches, (unsigned long long)stripes,
+                (unsigned long long)maxb);
+    CHECK(batches > 0 && batches <= calls && maxb >= 1 && maxb <= 8);
+  }
+  test_coalesces_exactly();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -480,3 +480,77 @@ def test_reconstruct_out_of_place(engines, k, m, S):
             for r in range(len(missing), m):
                 assert (got[i, r] == 0xC3).all(), "unused output slots untouched"
         assert (got[:, :, S:] == 0xC3).all()
+
+
+# ---- batched verify / scrub (rs_verify_batch) -------------------------------------
+def _oracle_bad(k, m, data_np, parity_np, S):
+    """Expected mismatch bitmask per stripe: oracle re-encode vs stored parity."""
+    N, _, P = data_np.shape
+    uni = np.zeros((N, k + m, P), np.uint8)
+    uni[:, :k] = data_np
+    rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
+    diff = (uni[:, k:, :S] != parity_np[:, :, :S]).any(axis=2)  # [N, m]
+    return (diff * (1 << np.arange(m))[None, :]).sum(axis=1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (10, 4), (6, 3), (5, 5), (12, 4)])
+@pytest.mark.parametrize("S", [1, 15, 16, 100, 1024, 6554])
+def test_verify_batch_device(engines, k, m, S):
+    """Clean stripes report 0; corrupting a data or parity byte flags exactly the
+    parity rows the oracle's re-encode disagrees with; slot padding is ignored."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    N = 300
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 31 + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    bad = torch.full((N,), -1, dtype=torch.int32, device="cuda")
+    eng.verify(data, parity, bad, S, N)
+    torch.cuda.synchronize()
+    assert int(bad.abs().sum()) == 0, "intact stripes must verify clean"
+    assert eng.last_kernel().startswith("verify_kernel")
+    # corrupt: one random byte in a data shard or a parity shard of ~1/3 of stripes;
+    # garbage in the slot padding of every stripe must not count
+    rng = np.random.default_rng(S + k * 7)
+    d_np, p_np = data.cpu().numpy(), parity.cpu().numpy()
+    if P > S:
+        d_np[:, :, S:] ^= 0x5A
+        p_np[:, :, S:] ^= 0xA5
+    hit = rng.random(N) < 0.33
+    for i in np.nonzero(hit)[0]:
+        b = int(rng.integers(0, S))
+        flip = np.uint8(rng.integers(1, 256))
+        if rng.random() < 0.5:
+            d_np[i, int(rng.integers(0, k)), b] ^= flip
+        else:
+            p_np[i, int(rng.integers(0, m)), b] ^= flip
+    exp = _oracle_bad(k, m, d_np, p_np, S)
+    assert (exp[hit] != 0).all() and (exp[~hit] == 0).all()
+    data.copy_(torch.from_numpy(d_np))
+    parity.copy_(torch.from_numpy(p_np))
+    eng.verify(data, parity, bad, S, N)
+    torch.cuda.synchronize()
+    assert np.array_equal(bad.cpu().numpy().view(np.uint32), exp)
+
+
+def test_verify_batch_host_and_per_object(engines):
+    k, m, S, N = 4, 2, 1000, 2500
+    eng = eng_for(engines, k, m)
+    rng = np.random.default_rng(99)
+    data = rng.integers(0, 256, (N, k, S), dtype=np.uint8)
+    parity = np.zeros((N, m, S), np.uint8)
+    eng.encode_host(data, parity, S, N)
+    assert not eng.verify_host(data, parity, S, N).any()
+    parity[7, 1, 999] ^= 1
+    data[1234, 0, 0] ^= 0x80
+    bad = eng.verify_host(data, parity, S, N)
+    exp = _oracle_bad(k, m, data, parity, S)
+    assert np.array_equal(bad, exp) and bad[7] == 0b10 and bad[1234] != 0
+    assert np.count_nonzero(bad) == 2
+    # per-object Verify agrees (klauspost Verify -> false on any parity mismatch)
+    for i in (6, 7, 1234):
+        shards = [bytearray(data[i, j]) for j in range(k)] + [bytearray(parity[i, j]) for j in range(m)]
+        assert eng.Verify(shards) == (bad[i] == 0)

@@ -44,6 +44,9 @@ def main():
         "rs104_64K_enc": (10, 4, 6554, 16384, "enc"),
         "rs104_64K_rec2p": (10, 4, 6554, 16384, "rec2p"),
         "rs84_64K_enc": (8, 4, 8192, 16384, "enc"),
+        "rs42_4K_ver": (4, 2, 1024, 65536, "ver"),
+        "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
+        "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
     }
     if args.workloads != "all":
         workloads = {k: v for k, v in workloads.items() if k in args.workloads.split(",")}
@@ -72,12 +75,15 @@ def main():
         masks = [torch.from_numpy(mm.view(np.int32)).cuda() for mm in masks_np]
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
-        alg = N * S * (k + (m if mode == "enc" else 2))
+        alg = N * S * (k + (m if mode in ("enc", "ver") else 2))
+        bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
         def run(i):
             d, p = bufs[i % nb]
             if mode == "enc":
                 eng.encode(d, p, S, N)
+            elif mode == "ver":
+                eng.verify(d, p, bad, S, N)
             elif mode == "rec2u":
                 eng.reconstruct(d, p, S, N, ((1 << t) - 1) & ~3)
             elif mode == "rec45u":
