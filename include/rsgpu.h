@@ -169,6 +169,8 @@ typedef struct {
   int inflight;           /* staging batches (0 = 8); each: stream + pinned + device slab */
   size_t max_batch_bytes; /* staging bytes per batch (0 = 32 MiB) */
   int max_exec;           /* batches executing at once (0 = 2; <= inflight) */
+  int staged_dma;         /* 0: kernels read/write the pinned staging in place (zero-copy);
+                             1: H2D / D2H copies around the kernel */
 } rs_coalescer_opts;
 int rs_coalescer_create(rs_ctx *ctx, const rs_coalescer_opts *opts /* NULL = defaults */,
                         rs_coalescer **out);
@@ -182,7 +184,7 @@ int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *
                 uint64_t *max_batch);
 
 /* ---- host memory helpers ------------------------------------------------ */
-int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin for async DMA */
+int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin: DMA + zero-copy */
 int rs_host_unregister(rs_ctx *ctx, void *ptr);
 
 /* ---- measurement helpers (bench.py) ------------------------------------- */
@@ -193,6 +195,13 @@ int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *
 /* Tuning knob: workgroups (256 threads) per CU for the batched kernels
  * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
+/* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or
+ * rs_host_register) and 16-B aligned run zero-copy by default: the kernel reads
+ * the survivors and writes the missing shards across PCIe in place.  0 forces
+ * the staged H2D -> kernel -> D2H pipeline (A/B and tests). */
+int rs_set_host_zero_copy(rs_ctx *ctx, int enable);
+/* "zero-copy" or "staged": how the last RS_MEM_HOST batch ran. */
+const char *rs_last_host_path(const rs_ctx *ctx);
 
 #ifdef __cplusplus
 }

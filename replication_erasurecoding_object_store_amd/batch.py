@@ -185,5 +185,11 @@ class BatchEngine(Service):
     def last_kernel(self) -> str:
         return _lib.lib().rs_last_kernel(self.ctx).decode()
 
+    def set_host_zero_copy(self, enable: bool) -> None:
+        _check(_lib.lib().rs_set_host_zero_copy(self.ctx, 1 if enable else 0))
+
+    def last_host_path(self) -> str:
+        return _lib.lib().rs_last_host_path(self.ctx).decode()
+
     def set_blocks_per_cu(self, n: int) -> None:
         _check(_lib.lib().rs_set_blocks_per_cu(self.ctx, n))

@@ -17,14 +17,15 @@ from .ec import M, K, Service, _check
 
 class CoalescerOpts(ctypes.Structure):
     _fields_ = [("max_batch", ctypes.c_size_t), ("max_wait_us", ctypes.c_uint32), ("inflight", ctypes.c_int),
-                ("max_batch_bytes", ctypes.c_size_t), ("max_exec", ctypes.c_int)]
+                ("max_batch_bytes", ctypes.c_size_t), ("max_exec", ctypes.c_int),
+                ("staged_dma", ctypes.c_int)]
 
 
 class CoalescingService(Service):
     def __init__(self, k: int = K, m: int = M, device: int = 0, max_batch: int = 0, max_wait_us: int = 0,
-                 inflight: int = 0, max_batch_bytes: int = 0, max_exec: int = 0):
+                 inflight: int = 0, max_batch_bytes: int = 0, max_exec: int = 0, staged_dma: bool = False):
         super().__init__(k, m, device)
-        opts = CoalescerOpts(max_batch, max_wait_us, inflight, max_batch_bytes, max_exec)
+        opts = CoalescerOpts(max_batch, max_wait_us, inflight, max_batch_bytes, max_exec, int(staged_dma))
         co = ctypes.c_void_p()
         _check(_lib.lib().rs_coalescer_create(self._ctx, ctypes.byref(opts), ctypes.byref(co)))
         self._co = co

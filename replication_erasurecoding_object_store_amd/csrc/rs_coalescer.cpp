@@ -23,8 +23,12 @@
 // device slab), so one batch's transfers overlap the next batch's filling.  All
 // arithmetic is the device kernels'; the host only moves bytes.
 #include <hip/hip_runtime.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -32,6 +36,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -45,21 +50,41 @@ using Clock = std::chrono::steady_clock;
 enum class Kind : int { kApply = 0, kVerify = 1 };
 
 struct Batch {
-  enum class State { kFree, kOpen, kClosed, kDone };
-  State state = State::kFree;
+  enum class State { kFree, kOpen, kClosed };
+  State state = State::kFree;  // guarded by rs_coalescer::mu
   Kind kind = Kind::kApply;
   size_t S = 0, P = 0, cap = 0;
-  size_t reserved = 0, filled = 0, released = 0;
-  bool parity_in = false;  // some slot needs its parity shards uploaded
-  int rc = RS_OK;
+  size_t reserved = 0;         // guarded by mu while open; fixed once closed
+  bool parity_in = false;      // some slot needs its parity shards uploaded
+  int rc = RS_OK;              // published by done_gen
   Clock::time_point deadline;
-  std::condition_variable done_cv;  // followers: batch finished
+  // Lock-free completion: callers stage, wait and drain without the mutex, so a
+  // finished batch of n callers does not turn into a convoy of n lock handoffs.
+  std::atomic<uint32_t> filled{0};    // slots staged
+  std::atomic<uint32_t> released{0};  // slots drained
+  std::atomic<uint32_t> done_gen{0};  // bumped (and futex-woken) when a run finishes
   hipStream_t stream = nullptr;
   rs::PinnedBuf host;
   rs::DevBuf dev;
   // region offsets (same in host staging and device slab)
   size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_bad = 0, bytes = 0;
 };
+static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
+
+void futex_wait(std::atomic<uint32_t>* w, uint32_t expected) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, expected, nullptr, nullptr, 0);
+}
+void futex_wake_all(std::atomic<uint32_t>* w) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+// Waits until *w != v: a short spin (a batch finishes within tens of µs), then sleeps.
+void wait_change(std::atomic<uint32_t>* w, uint32_t v) {
+  for (int i = 0; i < 512; ++i) {
+    if (w->load(std::memory_order_acquire) != v) return;
+    __builtin_ia32_pause();
+  }
+  while (w->load(std::memory_order_acquire) == v) futex_wait(w, v);
+}
 
 }  // namespace
 
@@ -71,11 +96,12 @@ struct rs_coalescer {
   std::chrono::microseconds max_wait{0};
 
   int max_exec = 2;   // batches on the device at once
+  bool zero_copy = true;
   int executing = 0;
 
   std::mutex mu;
   std::condition_variable free_cv;    // a batch became free (or opened)
-  std::condition_variable leader_cv;  // batch full / staged / an execution slot freed
+  std::condition_variable leader_cv;  // batch full / an execution slot freed
   std::vector<std::unique_ptr<Batch>> batches;
   std::vector<Batch*> free_list;
   std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots
@@ -112,7 +138,9 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->bytes = b->o_bad + round_up(b->cap * 4, 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
-  b->reserved = b->filled = b->released = 0;
+  b->reserved = 0;
+  b->filled.store(0, std::memory_order_relaxed);
+  b->released.store(0, std::memory_order_relaxed);
   b->parity_in = false;
   b->rc = RS_OK;
   b->state = Batch::State::kOpen;
@@ -125,27 +153,39 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
   const size_t k = co->k, m = co->m, P = b->P;
   (void)hipSetDevice(co->device);
   hipStream_t st = b->stream;
-  RS_HIP(hipMemcpyAsync(dev_at(b, b->o_data), host_at(b, b->o_data), n * k * P, hipMemcpyHostToDevice, st));
-  if (b->parity_in || b->kind == Kind::kVerify)
-    RS_HIP(hipMemcpyAsync(dev_at(b, b->o_parity), host_at(b, b->o_parity), n * m * P, hipMemcpyHostToDevice, st));
+  // Zero-copy (default): the staging is pinned host memory the GPU can address, so
+  // the kernel reads the staged shards and writes its outputs there directly --
+  // one launch + one sync per batch instead of 3-4 DMA round trips.
+  void* hd = nullptr;
+  const bool zc = co->zero_copy && hipHostGetDevicePointer(&hd, b->host.p, 0) == hipSuccess && hd;
+  if (!zc) (void)hipGetLastError();
+  uint8_t* base = zc ? static_cast<uint8_t*>(hd) : static_cast<uint8_t*>(b->dev.p);
+  auto at = [&](size_t off) { return base + off; };
+  if (!zc) {
+    RS_HIP(hipMemcpyAsync(dev_at(b, b->o_data), host_at(b, b->o_data), n * k * P, hipMemcpyHostToDevice, st));
+    if (b->parity_in || b->kind == Kind::kVerify)
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_parity), host_at(b, b->o_parity), n * m * P, hipMemcpyHostToDevice, st));
+    if (b->kind == Kind::kApply && co->per_stripe)
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
+  }
   int rc;
   if (b->kind == Kind::kVerify) {
-    rc = rs_verify_batch(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_parity), m * P, P, b->S, n,
+    // the mismatch words are OR-ed atomically: keep them in HBM, copy them back
+    rc = rs_verify_batch(co->ctx, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
                          reinterpret_cast<uint32_t*>(dev_at(b, b->o_bad)), RS_MEM_DEVICE, st);
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(host_at(b, b->o_bad), dev_at(b, b->o_bad), n * 4, hipMemcpyDeviceToHost, st));
   } else {
     if (co->per_stripe) {
-      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
-      rc = rs_reconstruct_batch_out(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_parity), m * P, P, b->S, n,
-                                    reinterpret_cast<const uint32_t*>(dev_at(b, b->o_masks)), n, 1,
-                                    dev_at(b, b->o_out), m * P, st);
+      rc = rs_reconstruct_batch_out(co->ctx, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
+                                    reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, at(b->o_out), m * P,
+                                    st);
     } else {  // encode-only batches (k+m > 16): parity straight into the out region
-      rc = rs_encode_batch(co->ctx, dev_at(b, b->o_data), k * P, dev_at(b, b->o_out), m * P, P, b->S, n,
-                           RS_MEM_DEVICE, st);
+      rc = rs_encode_batch(co->ctx, at(b->o_data), k * P, at(b->o_out), m * P, P, b->S, n, RS_MEM_DEVICE, st);
     }
     if (rc) return rc;
-    RS_HIP(hipMemcpyAsync(host_at(b, b->o_out), dev_at(b, b->o_out), n * m * P, hipMemcpyDeviceToHost, st));
+    if (!zc)
+      RS_HIP(hipMemcpyAsync(host_at(b, b->o_out), dev_at(b, b->o_out), n * m * P, hipMemcpyDeviceToHost, st));
   }
   RS_HIP(hipStreamSynchronize(st));
   return RS_OK;  // every mask was checked (>= k present) before it was staged
@@ -189,6 +229,7 @@ int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, D
   }
   const size_t slot = b->reserved++;
   const bool leader = slot == 0;
+  const uint32_t gen = b->done_gen.load(std::memory_order_relaxed);
   b->parity_in |= parity_in;
   if (b->reserved == b->cap) {  // full: no more slots
     co->open.erase(key);
@@ -197,9 +238,9 @@ int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, D
   }
   lk.unlock();
   fill(b, slot);
-  lk.lock();
-  if (++b->filled == b->reserved && b->state != Batch::State::kOpen) co->leader_cv.notify_all();
+  b->filled.fetch_add(1, std::memory_order_release);
   if (leader) {
+    lk.lock();
     // gather: until full, or (an execution slot is free and the linger is over)
     for (;;) {
       if (b->state != Batch::State::kOpen) break;
@@ -215,10 +256,11 @@ int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, D
       if (it != co->open.end() && it->second == b) co->open.erase(it);
       b->state = Batch::State::kClosed;
     }
-    while (b->filled < b->reserved || co->executing >= co->max_exec) co->leader_cv.wait(lk);
+    while (co->executing >= co->max_exec) co->leader_cv.wait(lk);
     ++co->executing;
     const size_t n = b->reserved;
     lk.unlock();
+    while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
     const int rc = execute(co, b, n);
     co->n_batches.fetch_add(1, std::memory_order_relaxed);
     co->stripes.fetch_add(n, std::memory_order_relaxed);
@@ -228,17 +270,18 @@ int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, D
     lk.lock();
     --co->executing;
     co->leader_cv.notify_all();  // an execution slot is free
+    lk.unlock();
     b->rc = rc;
-    b->state = Batch::State::kDone;
-    b->done_cv.notify_all();
+    b->done_gen.fetch_add(1, std::memory_order_release);
+    futex_wake_all(&b->done_gen);
   } else {
-    while (b->state != Batch::State::kDone) b->done_cv.wait(lk);
+    wait_change(&b->done_gen, gen);
   }
   const int rc = b->rc;
-  lk.unlock();
+  const size_t n = b->reserved;  // fixed since the batch closed (published by done_gen)
   if (rc == RS_OK) drain(b, slot);
-  lk.lock();
-  if (++b->released == b->reserved) {
+  if (b->released.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
+    lk.lock();
     b->state = Batch::State::kFree;
     co->free_list.push_back(b);
     co->free_cv.notify_all();
@@ -308,13 +351,14 @@ extern "C" {
 int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer** out) {
   if (!ctx || !out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
-  rs_coalescer_opts o{4096, 0, 8, size_t(32) << 20, 2};
+  rs_coalescer_opts o{4096, 0, 8, size_t(32) << 20, 2, 0};
   if (opts) {
     if (opts->max_batch) o.max_batch = opts->max_batch;
     o.max_wait_us = opts->max_wait_us;
     if (opts->inflight > 0) o.inflight = opts->inflight;
     if (opts->max_batch_bytes) o.max_batch_bytes = opts->max_batch_bytes;
     if (opts->max_exec > 0) o.max_exec = opts->max_exec;
+    o.staged_dma = opts->staged_dma;
   }
   if (o.inflight > 64 || o.max_exec > o.inflight) return RS_ERR_INVALID_ARG;
   auto co = std::make_unique<rs_coalescer>();
@@ -327,6 +371,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_bytes = o.max_batch_bytes;
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
+  co->zero_copy = o.staged_dma == 0;
   for (int i = 0; i < o.inflight; ++i) {
     co->batches.push_back(std::make_unique<Batch>());
     co->free_list.push_back(co->batches.back().get());

@@ -200,6 +200,9 @@ struct rs_ctx {
 
   std::mutex host_mu;             // host-resident batches: one at a time per context
   HostPipe host_pipe;
+  bool host_zero_copy = true;     // pinned host batches: kernel reads/writes them in place
+  DevBuf d_bad;                   // zero-copy verify: per-stripe result before D2H
+  std::atomic<const char*> last_host_path{"none"};
 
   std::atomic<const char*> last_kernel{"none"};
 
@@ -425,9 +428,78 @@ int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<in
   return RS_OK;
 }
 
+int upload_masks(rs_ctx* c, const uint32_t* masks, size_t n, hipStream_t s, const uint32_t** dev);
+
+// GPU address of a pinned host range [p, p+bytes) (hipHostMalloc'ed or
+// rs_host_register'ed), or nullptr if any part of it is pageable.
+uint8_t* mapped(const void* p, size_t bytes) {
+  if (!p || bytes == 0) return nullptr;
+  hipPointerAttribute_t a{}, b{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  const void* last = static_cast<const uint8_t*>(p) + bytes - 1;
+  if (hipPointerGetAttributes(&b, last) != hipSuccess || b.type != hipMemoryTypeHost || !b.devicePointer) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  uint8_t* d = static_cast<uint8_t*>(a.devicePointer);
+  if (static_cast<uint8_t*>(b.devicePointer) != d + (bytes - 1)) return nullptr;  // one linear mapping
+  return d;
+}
+
+// Zero-copy host batch: with the shards in pinned host memory the kernel itself
+// reads the K survivors and writes only the missing shards across PCIe, in place
+// -- per stripe exactly the bytes the codec needs, no staging slab, no DMA of
+// slots it does not touch (the staged pipeline must move every slot a stripe
+// might use).  Returns RS_ERR_NOT_SUPPORTED when the layout does not qualify.
+int host_zero_copy(rs_ctx* c, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
+                   const uint32_t* masks_host, int e, uint32_t* bad_host) {
+  const int k = c->k, m = c->m;
+  const size_t dbytes = (N - 1) * hl.data_sp + static_cast<size_t>(k - 1) * hl.pitch + S;
+  const size_t pbytes = m ? (N - 1) * hl.parity_sp + static_cast<size_t>(m - 1) * hl.pitch + S : 0;
+  uint8_t* dd = mapped(hl.data, dbytes);
+  uint8_t* pd = m ? mapped(hl.parity, pbytes) : nullptr;
+  if (!dd || (m && !pd)) return RS_ERR_NOT_SUPPORTED;
+  const Layout dl{dd, hl.data_sp, pd, hl.parity_sp, hl.pitch};
+  if (!device_layout_ok(dl, m, S)) return RS_ERR_NOT_SUPPORTED;
+  std::lock_guard<std::mutex> g(c->host_mu);
+  HostPipe& pipe = c->host_pipe;
+  if (!pipe.st[0]) RS_HIP(hipStreamCreateWithFlags(&pipe.st[0], hipStreamNonBlocking));
+  hipStream_t st = pipe.st[0];
+  rs::KernelArgs a = make_args(c, dl, S, N);
+  a.plans = plan_dev;
+  int rc;
+  if (bad_host) {
+    if (c->d_bad.ensure(N * 4)) return RS_ERR_DEVICE;
+    a.bad = static_cast<uint32_t*>(c->d_bad.p);
+    rc = launch_verify_args(c, a, st);
+    if (rc) return rc;
+    RS_HIP(hipMemcpyAsync(bad_host, a.bad, N * 4, hipMemcpyDeviceToHost, st));
+  } else {
+    if (masks_host) {
+      const uint32_t* dm = nullptr;
+      rc = upload_masks(c, masks_host, N, st, &dm);
+      if (rc) return rc;
+      a.present_masks = dm;
+    }
+    rc = launch(c, a, e, masks_host != nullptr, st);
+    if (rc) return rc;
+  }
+  RS_HIP(hipStreamSynchronize(st));
+  c->last_host_path.store("zero-copy");
+  return RS_OK;
+}
+
 int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
                size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e,
                uint32_t* bad_host = nullptr) {
+  if (c->host_zero_copy) {
+    const int rc = host_zero_copy(c, hl, S, N, plan_dev, masks_host, e, bad_host);
+    if (rc != RS_ERR_NOT_SUPPORTED) return rc;
+  }
+  c->last_host_path.store("staged");
   const int k = c->k, m = c->m;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t per_stripe = P * static_cast<size_t>(k + m) + ((masks_host || bad_host) ? 4 : 0);
@@ -534,6 +606,7 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
   c->enc = rs::build_encode_matrix(k, m);
   if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("RSGPU_FORCE_GENERIC")) c->force_generic = std::atoi(e) != 0;
+  if (const char* e = std::getenv("RSGPU_HOST_ZERO_COPY")) c->host_zero_copy = std::atoi(e) != 0;
   char name[160];
   std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
   c->backend = name;
@@ -870,6 +943,14 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
+
+int rs_set_host_zero_copy(rs_ctx* c, int enable) {
+  if (!c) return RS_ERR_INVALID_ARG;
+  c->host_zero_copy = enable != 0;
+  return RS_OK;
+}
+
+const char* rs_last_host_path(const rs_ctx* c) { return c ? c->last_host_path.load() : "none"; }
 
 int rs_set_blocks_per_cu(rs_ctx* c, int bpc) {
   if (!c || bpc < 0) return RS_ERR_INVALID_ARG;

@@ -36,9 +36,10 @@ def _run_threads(n, fn):
         raise errs[0]
 
 
+@pytest.mark.parametrize("staged_dma", [False, True])
 @pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3)])
-def test_concurrent_mixed_ops_match_oracle(gpu, k, m):
-    svc = CoalescingService(k, m, max_batch=64, max_wait_us=500, inflight=3)
+def test_concurrent_mixed_ops_match_oracle(gpu, k, m, staged_dma):
+    svc = CoalescingService(k, m, max_batch=64, max_wait_us=500, inflight=3, staged_dma=staged_dma)
     try:
         sizes = [4096, 1000, 65536 + 5]
 

@@ -286,7 +286,8 @@ def test_batch_reconstruct_too_few(engines):
         eng.sync()
 
 
-def test_batch_host_paths_match_device(engines):
+@pytest.mark.parametrize("zero_copy", [True, False])
+def test_batch_host_paths_match_device(engines, zero_copy):
     import torch
 
     k, m = 4, 2
@@ -298,8 +299,10 @@ def test_batch_host_paths_match_device(engines):
     eng.encode_unified(buf, S, P, N)
     torch.cuda.synchronize()
     eng.host_register(host)
+    eng.set_host_zero_copy(zero_copy)
     try:
         eng.encode_host_unified(host, S, P, N)
+        assert eng.last_host_path() == ("zero-copy" if zero_copy else "staged")
         assert np.array_equal(host[:, :, :S], buf.cpu().numpy()[:, :, :S])
         orig = host.copy()
         host[:, 0, :S] = 0
@@ -314,7 +317,9 @@ def test_batch_host_paths_match_device(engines):
                     host[i, j, :S] = 0
         eng.reconstruct_host_unified(host, S, P, N, masks)
         assert np.array_equal(host[:, :, :S], orig[:, :, :S])
+        assert eng.last_host_path() == ("zero-copy" if zero_copy else "staged")
     finally:
+        eng.set_host_zero_copy(True)
         eng.host_unregister(host)
 
 
@@ -404,8 +409,9 @@ def test_split_layout_device(engines, k, m, S):
         assert torch.equal(p2[:, :, :S], parity[:, :, :S])
 
 
+@pytest.mark.parametrize("zero_copy", [True, False])
 @pytest.mark.parametrize("S", [1024, 1000])
-def test_split_layout_host(engines, S):
+def test_split_layout_host(engines, S, zero_copy):
     k, m = 4, 2
     eng = eng_for(engines, k, m)
     N = 3000
@@ -415,8 +421,11 @@ def test_split_layout_host(engines, S):
     parity = np.zeros((N, m, P), np.uint8)
     eng.host_register(data)
     eng.host_register(parity)
+    eng.set_host_zero_copy(zero_copy)
+    path = "zero-copy" if zero_copy and S % 16 == 0 else "staged"  # zero-copy needs 16-B slots
     try:
         eng.encode_host(data, parity, S, N)
+        assert eng.last_host_path() == path
         uni = np.concatenate([data, np.zeros_like(parity)], axis=1).copy()
         rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
         assert np.array_equal(parity, uni[:, k:])
@@ -431,7 +440,13 @@ def test_split_layout_host(engines, S):
         parity[lost[:, 4:]] = 0
         eng.reconstruct_host(data, parity, S, N, masks)
         assert np.array_equal(data, d0) and np.array_equal(parity, p0)
+        # scrub, zero-copy or staged alike
+        assert not eng.verify_host(data, parity, S, N).any()
+        parity[17, 1, 3] ^= 4
+        assert np.array_equal(np.nonzero(eng.verify_host(data, parity, S, N))[0], [17])
+        assert eng.last_host_path() == path
     finally:
+        eng.set_host_zero_copy(True)
         eng.host_unregister(data)
         eng.host_unregister(parity)
 

@@ -9,7 +9,7 @@
 //          -Ireplication_erasurecoding_object_store_amd -Lreplication_erasurecoding_object_store_amd \
 //          -lrsgpu -Wl,-rpath,$PWD/replication_erasurecoding_object_store_amd \
 //          -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
-// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co> [max_batch] [max_wait_us] [obj_bytes] [max_exec]
+// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma]
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -31,11 +31,12 @@ int main(int argc, char** argv) {
   const double secs = std::atof(argv[2]);
   const bool mix = std::strcmp(argv[3], "mix") == 0;
   const bool co_mode = std::strcmp(argv[4], "co") == 0;
-  rs_coalescer_opts opts{0, 0, 0, 0, 0};
+  rs_coalescer_opts opts{0, 0, 0, 0, 0, 0};
   if (argc > 5) opts.max_batch = std::strtoull(argv[5], nullptr, 10);
   if (argc > 6) opts.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
   const size_t obj = argc > 7 ? std::strtoull(argv[7], nullptr, 10) : 4096;
   if (argc > 8) opts.max_exec = std::atoi(argv[8]);
+  if (argc > 9) opts.staged_dma = std::atoi(argv[9]);
   const int k = 4, m = 2;
   rs_ctx* ctx = nullptr;
   if (int rc = rs_create(k, m, 0, 0, &ctx)) {
@@ -96,11 +97,11 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
-      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u}\n",
+      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d}\n",
       co ? "coalesced" : "direct", mix ? "mix" : "enc", T, obj, dt, n_ops / dt,
       n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
-      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us);
+      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma);
   if (co) rs_coalescer_destroy(co);
   rs_destroy(ctx);
   return bad.load() ? 1 : 0;
