@@ -166,7 +166,7 @@ typedef struct rs_coalescer rs_coalescer;
 typedef struct {
   size_t max_batch;       /* stripes per batch (0 = 4096) */
   uint32_t max_wait_us;   /* linger before a batch may start (0 = none) */
-  int inflight;           /* staging batches (0 = 8); each: stream + pinned + device slab */
+  int inflight;           /* staging batches (0 = 16); each: stream + pinned + device slab */
   size_t max_batch_bytes; /* staging bytes per batch (0 = 32 MiB) */
   int max_exec;           /* batches executing at once (0 = 2; <= inflight) */
   int staged_dma;         /* 0: kernels read/write the pinned staging in place (zero-copy);
@@ -179,6 +179,16 @@ int rs_co_encode(rs_coalescer *co, uint8_t *const *shards, const size_t *lens);
 int rs_co_reconstruct(rs_coalescer *co, uint8_t *const *shards, size_t *lens);
 int rs_co_reconstruct_data(rs_coalescer *co, uint8_t *const *shards, size_t *lens);
 int rs_co_verify(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, int *ok);
+/* Many objects in one call (batched healer repair; bulk
+ * writes): object i's K+M shard pointers / lengths are shards[i*(k+m) ...] /
+ * lens[i*(k+m) ...]; each object gets exactly rs_reconstruct's (rs_encode's)
+ * contract and its return code in rcs[i].  Objects are grouped by shard length
+ * and staged into as few device batches as possible.  Returns RS_OK unless the
+ * call itself fails (bad arguments, device error). */
+int rs_co_reconstruct_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards, size_t *lens,
+                           int *rcs);
+int rs_co_encode_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards,
+                      const size_t *lens, int *rcs);
 /* Counters since creation: calls, device batches, stripes batched, largest batch. */
 int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
                 uint64_t *max_batch);

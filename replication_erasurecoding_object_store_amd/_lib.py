@@ -68,6 +68,8 @@ SIGNATURES = {
     "rs_co_reconstruct_data": (_i, [_vp, _u8pp, _szp]),
     "rs_co_verify": (_i, [_vp, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_stats": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "rs_co_reconstruct_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
+    "rs_co_encode_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),

@@ -11,8 +11,10 @@ from __future__ import annotations
 
 import ctypes
 
+from typing import List, Optional, Sequence
+
 from . import _lib
-from .ec import M, K, Service, _check
+from .ec import ECError, ErrTooFewShards, M, K, Service, _check, _shard_array
 
 
 class CoalescerOpts(ctypes.Structure):
@@ -32,6 +34,47 @@ class CoalescingService(Service):
 
     def _call(self, op: str, *args) -> int:
         return getattr(_lib.lib(), "rs_co_" + op)(self._co, *args)
+
+    def _many(self, op: str, objects: Sequence[List[Optional[bytearray]]], fill_missing: bool) -> List[Optional[ECError]]:
+        t = self.k + self.m
+        n = len(objects)
+        errs: List[Optional[ECError]] = [None] * n
+        ok_idx = [i for i, sh in enumerate(objects) if len(sh) == t]
+        for i in range(n):
+            if len(objects[i]) != t:
+                errs[i] = ECError(ErrTooFewShards)
+        ptrs = (_lib._u8p * (len(ok_idx) * t))()
+        lens = (ctypes.c_size_t * (len(ok_idx) * t))()
+        keep = []
+        for j, i in enumerate(ok_idx):
+            sh = objects[i]
+            S = next((len(s) for s in sh if s is not None and len(s) > 0), 0)
+            p, ln, kp = _shard_array(sh, S, fill_missing=fill_missing)
+            keep.append(kp)
+            for q in range(t):
+                ptrs[j * t + q] = p[q]
+                lens[j * t + q] = ln[q]
+        rcs = (ctypes.c_int * max(1, len(ok_idx)))()
+        _check(getattr(_lib.lib(), "rs_co_" + op + "_many")(self._co, len(ok_idx), ptrs, lens, rcs))
+        for j, i in enumerate(ok_idx):
+            if rcs[j] != _lib.RS_OK:
+                errs[i] = ECError(rcs[j])
+            elif fill_missing:
+                sh = objects[i]
+                for q in range(t):
+                    if (sh[q] is None or len(sh[q]) == 0) and lens[j * t + q] > 0:
+                        sh[q] = bytearray(ctypes.string_at(ptrs[j * t + q], lens[j * t + q]))
+        del keep
+        return errs
+
+    def ReconstructMany(self, objects: Sequence[List[Optional[bytearray]]]) -> List[Optional[ECError]]:
+        """Reconstruct for many objects in one call (rs_co_reconstruct_many): each
+        list is filled in place exactly as Reconstruct would; returns per-object
+        errors (None = ok)."""
+        return self._many("reconstruct", objects, True)
+
+    def EncodeMany(self, objects: Sequence[List[bytearray]]) -> List[Optional[ECError]]:
+        return self._many("encode", objects, False)
 
     def stats(self) -> dict:
         v = [ctypes.c_uint64() for _ in range(4)]

@@ -77,9 +77,10 @@ void futex_wait(std::atomic<uint32_t>* w, uint32_t expected) {
 void futex_wake_all(std::atomic<uint32_t>* w) {
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
 }
-// Waits until *w != v: a short spin (a batch finishes within tens of µs), then sleeps.
+// Waits until *w != v: a brief spin, then sleeps (callers may far outnumber cores,
+// so spinning long would steal the CPU the stragglers need to stage their shards).
 void wait_change(std::atomic<uint32_t>* w, uint32_t v) {
-  for (int i = 0; i < 512; ++i) {
+  for (int i = 0; i < 64; ++i) {
     if (w->load(std::memory_order_acquire) != v) return;
     __builtin_ia32_pause();
   }
@@ -200,108 +201,135 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
 // are on the device pile into the open batch, so batches grow with the load and a
 // lone caller pays no timer.
 template <class Fill, class Drain>
+int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity_in, Fill&& fill, Drain&& drain) {
+  const auto key = std::make_pair(static_cast<int>(kind), S);
+  int result = RS_OK;
+  size_t done_items = 0;
+  while (done_items < count) {
+    std::unique_lock<std::mutex> lk(co->mu);
+    Batch* b = nullptr;
+    for (;;) {
+      auto it = co->open.find(key);
+      if (it != co->open.end()) {
+        b = it->second;
+        break;
+      }
+      if (!co->free_list.empty()) {
+        b = co->free_list.back();
+        co->free_list.pop_back();
+        const int rc = prepare(co, b, kind, S);
+        if (rc) {
+          b->state = Batch::State::kFree;
+          co->free_list.push_back(b);
+          co->free_cv.notify_all();
+          return rc;
+        }
+        co->open[key] = b;
+        co->free_cv.notify_all();  // waiters for this S may join it
+        break;
+      }
+      co->free_cv.wait(lk);  // every batch is in flight: back-pressure
+    }
+    // reserve a run of slots for this caller's next objects
+    const size_t take = std::min(count - done_items, b->cap - b->reserved);
+    const size_t slot0 = b->reserved;
+    b->reserved += take;
+    const bool leader = slot0 == 0;
+    const uint32_t gen = b->done_gen.load(std::memory_order_relaxed);
+    b->parity_in |= parity_in;
+    if (b->reserved == b->cap) {  // full: no more slots
+      co->open.erase(key);
+      b->state = Batch::State::kClosed;
+      co->leader_cv.notify_all();
+    }
+    lk.unlock();
+    for (size_t j = 0; j < take; ++j) fill(b, slot0 + j, done_items + j);
+    b->filled.fetch_add(static_cast<uint32_t>(take), std::memory_order_release);
+    if (leader) {
+      lk.lock();
+      // gather: until full, or (an execution slot is free and the linger is over)
+      for (;;) {
+        if (b->state != Batch::State::kOpen) break;
+        const bool slot_free = co->executing < co->max_exec;
+        if (slot_free && Clock::now() >= b->deadline) break;
+        if (slot_free)
+          co->leader_cv.wait_until(lk, b->deadline);
+        else
+          co->leader_cv.wait(lk);
+      }
+      if (b->state == Batch::State::kOpen) {
+        auto it = co->open.find(key);
+        if (it != co->open.end() && it->second == b) co->open.erase(it);
+        b->state = Batch::State::kClosed;
+      }
+      while (co->executing >= co->max_exec) co->leader_cv.wait(lk);
+      ++co->executing;
+      const size_t n = b->reserved;
+      lk.unlock();
+      while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
+      const int rc = execute(co, b, n);
+      co->n_batches.fetch_add(1, std::memory_order_relaxed);
+      co->stripes.fetch_add(n, std::memory_order_relaxed);
+      uint64_t seen = co->max_seen.load(std::memory_order_relaxed);
+      while (n > seen && !co->max_seen.compare_exchange_weak(seen, n)) {
+      }
+      lk.lock();
+      --co->executing;
+      co->leader_cv.notify_all();  // an execution slot is free
+      lk.unlock();
+      b->rc = rc;
+      b->done_gen.fetch_add(1, std::memory_order_release);
+      futex_wake_all(&b->done_gen);
+    } else {
+      wait_change(&b->done_gen, gen);
+    }
+    const int rc = b->rc;
+    const size_t n = b->reserved;  // fixed since the batch closed (published by done_gen)
+    if (rc == RS_OK)
+      for (size_t j = 0; j < take; ++j) drain(b, slot0 + j, done_items + j);
+    else if (result == RS_OK)
+      result = rc;
+    if (b->released.fetch_add(static_cast<uint32_t>(take), std::memory_order_acq_rel) + take == n) {
+      lk.lock();
+      b->state = Batch::State::kFree;
+      co->free_list.push_back(b);
+      co->free_cv.notify_all();
+    }
+    done_items += take;
+  }
+  return result;
+}
+
+// One object (the per-call IEcDriver entry points).
+template <class Fill, class Drain>
 int submit(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, Drain&& drain) {
   co->calls.fetch_add(1, std::memory_order_relaxed);
-  std::unique_lock<std::mutex> lk(co->mu);
-  const auto key = std::make_pair(static_cast<int>(kind), S);
-  Batch* b = nullptr;
-  for (;;) {
-    auto it = co->open.find(key);
-    if (it != co->open.end()) {
-      b = it->second;
-      break;
-    }
-    if (!co->free_list.empty()) {
-      b = co->free_list.back();
-      co->free_list.pop_back();
-      const int rc = prepare(co, b, kind, S);
-      if (rc) {
-        b->state = Batch::State::kFree;
-        co->free_list.push_back(b);
-        co->free_cv.notify_all();
-        return rc;
-      }
-      co->open[key] = b;
-      co->free_cv.notify_all();  // waiters for this S may join it
-      break;
-    }
-    co->free_cv.wait(lk);  // every batch is in flight: back-pressure
-  }
-  const size_t slot = b->reserved++;
-  const bool leader = slot == 0;
-  const uint32_t gen = b->done_gen.load(std::memory_order_relaxed);
-  b->parity_in |= parity_in;
-  if (b->reserved == b->cap) {  // full: no more slots
-    co->open.erase(key);
-    b->state = Batch::State::kClosed;
-    co->leader_cv.notify_all();
-  }
-  lk.unlock();
-  fill(b, slot);
-  b->filled.fetch_add(1, std::memory_order_release);
-  if (leader) {
-    lk.lock();
-    // gather: until full, or (an execution slot is free and the linger is over)
-    for (;;) {
-      if (b->state != Batch::State::kOpen) break;
-      const bool slot_free = co->executing < co->max_exec;
-      if (slot_free && Clock::now() >= b->deadline) break;
-      if (slot_free)
-        co->leader_cv.wait_until(lk, b->deadline);
-      else
-        co->leader_cv.wait(lk);
-    }
-    if (b->state == Batch::State::kOpen) {
-      auto it = co->open.find(key);
-      if (it != co->open.end() && it->second == b) co->open.erase(it);
-      b->state = Batch::State::kClosed;
-    }
-    while (co->executing >= co->max_exec) co->leader_cv.wait(lk);
-    ++co->executing;
-    const size_t n = b->reserved;
-    lk.unlock();
-    while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
-    const int rc = execute(co, b, n);
-    co->n_batches.fetch_add(1, std::memory_order_relaxed);
-    co->stripes.fetch_add(n, std::memory_order_relaxed);
-    uint64_t seen = co->max_seen.load(std::memory_order_relaxed);
-    while (n > seen && !co->max_seen.compare_exchange_weak(seen, n)) {
-    }
-    lk.lock();
-    --co->executing;
-    co->leader_cv.notify_all();  // an execution slot is free
-    lk.unlock();
-    b->rc = rc;
-    b->done_gen.fetch_add(1, std::memory_order_release);
-    futex_wake_all(&b->done_gen);
-  } else {
-    wait_change(&b->done_gen, gen);
-  }
-  const int rc = b->rc;
-  const size_t n = b->reserved;  // fixed since the batch closed (published by done_gen)
-  if (rc == RS_OK) drain(b, slot);
-  if (b->released.fetch_add(1, std::memory_order_acq_rel) + 1 == n) {
-    lk.lock();
-    b->state = Batch::State::kFree;
-    co->free_list.push_back(b);
-    co->free_cv.notify_all();
-  }
-  return rc;
+  return submit_many(
+      co, kind, S, 1, parity_in, [&](Batch* b, size_t slot, size_t) { fill(b, slot); },
+      [&](Batch* b, size_t slot, size_t) { drain(b, slot); });
 }
 
 // Reconstruct / ReconstructData through the coalescer; semantics of
 // reconstruct_impl in rs_engine.cpp ([upstream reedsolomon.go reconstruct]).
-int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool data_only) {
-  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+struct RecItem {
+  uint8_t* const* shards = nullptr;
+  size_t* lens = nullptr;
+  size_t S = 0;
+  uint32_t present = 0;
+  bool parity_used = false;  // a parity shard is among the k survivors
+};
+
+// Checks one object; *need = false when there is nothing to do (rc RS_OK).
+int rec_check(const rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool data_only, RecItem* it,
+              bool* need) {
   const int k = co->k, m = co->m, t = k + m;
-  if (!co->per_stripe)
-    return data_only ? rs_reconstruct_data(co->ctx, shards, lens) : rs_reconstruct(co->ctx, shards, lens);
+  *need = false;
+  if (!shards || !lens) return RS_ERR_INVALID_ARG;
   size_t S = 0;
   int rc = rs::check_shards(t, lens, true, &S);
   if (rc) return rc;
   uint32_t present = 0;
   int np = 0, data_present = 0;
-  bool parity_used = false;
   for (int i = 0; i < t; ++i)
     if (lens[i]) {
       present |= 1u << i;
@@ -311,37 +339,59 @@ int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool 
   if (np == t || (data_only && data_present == k)) return RS_OK;
   if (np < k) return RS_ERR_TOO_FEW_SHARDS;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
-  int used = 0;  // survivors = first k present shards (the kernel reads those)
-  for (int i = 0; i < t && used < k; ++i)
-    if (lens[i]) {
-      ++used;
-      if (i >= k) parity_used = true;
-    }
   for (int i = 0; i < t; ++i)
     if (!lens[i] && (!data_only || i < k) && !shards[i]) return RS_ERR_INVALID_ARG;
-  auto fill = [&](Batch* b, size_t slot) {
-    const size_t P = b->P;
-    for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
-      if (!lens[i]) continue;
-      ++staged;
-      uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P)
-                           : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
-      std::memcpy(dst, shards[i], S);
+  it->shards = shards;
+  it->lens = lens;
+  it->S = S;
+  it->present = present;
+  it->parity_used = false;
+  for (int i = 0, used = 0; i < t && used < k; ++i)  // survivors = first k present
+    if (lens[i]) {
+      ++used;
+      if (i >= k) it->parity_used = true;
     }
-    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = present;
-  };
-  auto drain = [&](Batch* b, size_t slot) {
-    int r = 0;  // r-th missing shard (index order, data before parity) = out slot r
-    for (int i = 0; i < t; ++i) {
-      if (lens[i]) continue;
-      if (!data_only || i < k) {
-        std::memcpy(shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), S);
-        lens[i] = S;
-      }
-      ++r;
+  (void)m;
+  *need = true;
+  return RS_OK;
+}
+
+void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it) {
+  const int k = co->k, m = co->m, t = k + m;
+  const size_t P = b->P;
+  for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
+    if (!it.lens[i]) continue;
+    ++staged;
+    uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P) : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
+    std::memcpy(dst, it.shards[i], it.S);
+  }
+  reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
+}
+
+void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
+  const int k = co->k, m = co->m, t = k + m;
+  int r = 0;  // r-th missing shard (index order, data before parity) = out slot r
+  for (int i = 0; i < t; ++i) {
+    if (it.lens[i]) continue;
+    if (!data_only || i < k) {
+      std::memcpy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
+      it.lens[i] = it.S;
     }
-  };
-  return submit(co, Kind::kApply, S, parity_used, fill, drain);
+    ++r;
+  }
+}
+
+int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool data_only) {
+  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+  if (!co->per_stripe)
+    return data_only ? rs_reconstruct_data(co->ctx, shards, lens) : rs_reconstruct(co->ctx, shards, lens);
+  RecItem it;
+  bool need = false;
+  const int rc = rec_check(co, shards, lens, data_only, &it, &need);
+  if (rc || !need) return rc;
+  return submit(
+      co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it); },
+      [&](Batch* b, size_t slot) { rec_drain(co, b, slot, it, data_only); });
 }
 
 }  // namespace
@@ -351,7 +401,7 @@ extern "C" {
 int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer** out) {
   if (!ctx || !out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
-  rs_coalescer_opts o{4096, 0, 8, size_t(32) << 20, 2, 0};
+  rs_coalescer_opts o{4096, 0, 16, size_t(32) << 20, 2, 0};
   if (opts) {
     if (opts->max_batch) o.max_batch = opts->max_batch;
     o.max_wait_us = opts->max_wait_us;
@@ -428,6 +478,84 @@ int rs_co_verify(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, i
   };
   auto drain = [&](Batch* b, size_t slot) { *ok = reinterpret_cast<uint32_t*>(host_at(b, b->o_bad))[slot] == 0; };
   return submit(co, Kind::kVerify, S, true, fill, drain);
+}
+
+// Batched healer repair: the objects a scan found damaged
+// (poller.go:227-309 audits one object per goroutine, 10 at a time) go through in
+// as few device batches as their shard lengths allow.  Per object exactly
+// rs_reconstruct's contract; its code lands in rcs[i].
+int rs_co_reconstruct_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, size_t* lens, int* rcs) {
+  if (!co || (n_objects && (!shards || !lens || !rcs))) return RS_ERR_INVALID_ARG;
+  const size_t t = static_cast<size_t>(co->k + co->m);
+  co->calls.fetch_add(n_objects, std::memory_order_relaxed);
+  if (!co->per_stripe) {
+    for (size_t i = 0; i < n_objects; ++i) rcs[i] = rs_reconstruct(co->ctx, shards + i * t, lens + i * t);
+    return RS_OK;
+  }
+  std::vector<RecItem> items(n_objects);
+  std::map<size_t, std::vector<size_t>> by_len;
+  for (size_t i = 0; i < n_objects; ++i) {
+    bool need = false;
+    rcs[i] = rec_check(co, shards + i * t, lens + i * t, false, &items[i], &need);
+    if (need) by_len[items[i].S].push_back(i);
+  }
+  for (auto& g : by_len) {
+    const std::vector<size_t>& idx = g.second;
+    bool parity_in = false;
+    for (size_t i : idx) parity_in |= items[i].parity_used;
+    const int rc = submit_many(
+        co, Kind::kApply, g.first, idx.size(), parity_in,
+        [&](Batch* b, size_t slot, size_t j) { rec_fill(co, b, slot, items[idx[j]]); },
+        [&](Batch* b, size_t slot, size_t j) { rec_drain(co, b, slot, items[idx[j]], false); });
+    if (rc) {
+      for (size_t i : idx)
+        if (rcs[i] == RS_OK) rcs[i] = rc;  // device failure: the whole group
+      return rc;
+    }
+  }
+  return RS_OK;
+}
+
+// Bulk encode of many objects (e.g. a batch of writes): per object rs_encode's
+// contract, results in rcs[i].
+int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, const size_t* lens, int* rcs) {
+  if (!co || (n_objects && (!shards || !lens || !rcs))) return RS_ERR_INVALID_ARG;
+  const int k = co->k, m = co->m;
+  const size_t t = static_cast<size_t>(k + m);
+  co->calls.fetch_add(n_objects, std::memory_order_relaxed);
+  std::vector<size_t> Ss(n_objects, 0);
+  std::map<size_t, std::vector<size_t>> by_len;
+  for (size_t i = 0; i < n_objects; ++i) {
+    size_t S = 0;
+    int rc = rs::check_shards(k + m, lens + i * t, false, &S);
+    for (size_t j = 0; rc == RS_OK && j < t; ++j)
+      if (!shards[i * t + j]) rc = RS_ERR_INVALID_ARG;
+    if (rc == RS_OK && S > 0xFFFFFFF0u) rc = RS_ERR_INVALID_ARG;
+    rcs[i] = rc;
+    Ss[i] = S;
+    if (rc == RS_OK && m > 0) by_len[S].push_back(i);
+  }
+  const uint32_t data_mask = (1u << k) - 1u;
+  for (auto& g : by_len) {
+    const std::vector<size_t>& idx = g.second;
+    const size_t S = g.first;
+    const int rc = submit_many(
+        co, Kind::kApply, S, idx.size(), false,
+        [&](Batch* b, size_t slot, size_t j) {
+          uint8_t* const* sh = shards + idx[j] * t;
+          for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
+          reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+        },
+        [&](Batch* b, size_t slot, size_t j) {
+          uint8_t* const* sh = shards + idx[j] * t;
+          for (int r = 0; r < m; ++r) std::memcpy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+        });
+    if (rc) {
+      for (size_t i : idx) rcs[i] = rc;
+      return rc;
+    }
+  }
+  return RS_OK;
 }
 
 int rs_co_stats(rs_coalescer* co, uint64_t* calls, uint64_t* batches, uint64_t* stripes, uint64_t* max_batch) {
