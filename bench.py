@@ -324,6 +324,101 @@ def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
                     "staged: every k+m slot DMA'd each way"}
 
 
+def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
+    """Device-resident verify / bit-rot scrub (rs_verify_batch): re-encode and
+    compare every stripe, K+M shards read per stripe, nothing written but the
+    per-stripe mismatch words.  Checks clean batches verify clean and one flipped
+    byte is found."""
+    from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
+
+    P = shard_pitch_for(S)
+    nb = max(2, int(np.ceil(rotate_bytes / (N * (k + m) * P))))
+    bufs = make_batches(torch, nb, N, k, m, P, seed)
+    for d, p in bufs:
+        eng.encode(d, p, S, N)
+    bad = torch.empty(N, dtype=torch.int32, device="cuda")
+    for i in range(2):
+        eng.verify(*bufs[i % nb], bad, S, N)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(reps):
+        eng.verify(*bufs[i % nb], bad, S, N)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    d, p = bufs[0]
+    eng.verify(d, p, bad, S, N)
+    torch.cuda.synchronize()
+    clean = int(bad.count_nonzero()) == 0
+    p[N // 3, m - 1, S - 1] ^= 0x40
+    eng.verify(d, p, bad, S, N)
+    torch.cuda.synchronize()
+    hit = bad.nonzero().flatten().tolist() == [N // 3] and int(bad[N // 3]) == 1 << (m - 1)
+    kname = eng.last_kernel()
+    del bufs
+    torch.cuda.empty_cache()
+    return {"kernel": kname, "shard_len": S, "stripes": N, "ms": round(ms, 5),
+            "user_GiBps": round(N * k * S / (ms * 1e-3) / GiB, 1),
+            "hbm_frac": round(N * S * (k + m) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ok": clean and hit}
+
+
+def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
+    """Config 2's SoA layout variant and config 3's named erasure patterns, each as
+    kernel time per launch (HIP events, rotating >= 2 GiB).  Rates: user data
+    K*S*N per second and HBM fraction of the algorithmic bytes."""
+    from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
+
+    t = k + m
+    P = shard_pitch_for(S)
+    nb = max(2, int(np.ceil(rotate_bytes / (N * t * P))))
+    g = torch.Generator(device="cuda").manual_seed(0x5EED0003)
+    split = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
+              torch.empty((N, m, P), dtype=torch.uint8, device="cuda"), torch.empty((N, m, P), dtype=torch.uint8,
+                                                                                     device="cuda"))
+             for _ in range(nb)]
+    for d, p, _ in split:
+        eng.encode(d, p, S, N)
+    rng = np.random.default_rng(0x5EED0003)
+    one = ((1 << t) - 1) & ~(1 << rng.integers(0, t, N))
+    full = (1 << t) - 1
+    dev_one = torch.from_numpy(one.astype(np.uint32).view(np.int32)).cuda()
+
+    def timed(fn):
+        for i in range(2):
+            fn(i)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(reps):
+            fn(i)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    res = {}
+
+    def put(name, sec, e):
+        res[name] = {"user_GiBps": round(N * k * S / sec / GiB, 1),
+                     "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4)}
+
+    put("rec1_per_stripe_out", timed(lambda i: eng.reconstruct_out(split[i % nb][0], split[i % nb][1],
+                                                                      split[i % nb][2], S, N, masks_dev=dev_one)), 1)
+    for name, pat in (("rec_0_1_uniform_out", (0, 1)), ("rec_0_4_uniform_out", (0, 4)),
+                      ("rec_4_5_uniform_out", (4, 5))):
+        mask = full & ~sum(1 << j for j in pat)
+        put(name, timed(lambda i: eng.reconstruct_out(split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N,
+                                                      present_masks=mask)), 2)
+    del split
+    torch.cuda.empty_cache()
+    # SoA: shard s of every stripe in one plane
+    soa = [(torch.randint(0, 256, (k, N, P), dtype=torch.uint8, device="cuda", generator=g),
+            torch.empty((m, N, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
+    put("soa_encode", timed(lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N, shard_pitch=N * P,
+                                                 data_stripe_pitch=P, parity_stripe_pitch=P)), m)
+    del soa
+    torch.cuda.empty_cache()
+    return res
+
+
 def pmc_traffic():
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
@@ -431,6 +526,11 @@ def main():
             }
             e2.close()
         extras["kmsweep_64KiB_device"] = sweep
+        extras["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
+        extras["scrub_verify_device"] = {"rs42_4KiB": scrub_rate(torch, eng, k, m, S, N, rotate)}
+        e2 = BatchEngine(10, 4, 0)
+        extras["scrub_verify_device"]["rs104_64KiB"] = scrub_rate(torch, e2, 10, 4, 6554, 16384, rotate)
+        e2.close()
         extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 1 << 18)
         extras["healer_mix_config5"] = healer_mix(torch, eng, k, m, S, 1 << 20)
         out["extras"] = extras

@@ -397,6 +397,15 @@ bool device_layout_ok(const Layout& L, int m, size_t S) {
          L.pitch % 16 == 0 && L.pitch >= round_up(S, 16);
 }
 
+// Out-of-place outputs at out + i*out_sp + r*pitch (r < e) must not overlap:
+// stripe-major (the e outputs of a stripe inside its out_sp) or plane-major
+// (output r of every stripe in its own plane of N*out_sp bytes, the SoA layout).
+bool out_layout_ok(size_t out_sp, size_t pitch, size_t S, size_t N, int e) {
+  const size_t slot = round_up(S, 16);
+  if (e <= 1) return out_sp >= slot || N == 1;
+  return (out_sp >= static_cast<size_t>(e) * pitch && pitch >= slot) || (out_sp >= slot && pitch >= N * out_sp);
+}
+
 bool batch_sizes_ok(size_t S, size_t N, size_t pitch) {
   if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || pitch < S) return false;
   const uint64_t cols = round_up(S, 16) / 16;
@@ -829,7 +838,7 @@ int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, con
   a.out_sp = out_sp;
   if (masks_on_device) {
     if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
-    if (out_sp < static_cast<size_t>(c->m) * shard_pitch) return RS_ERR_INVALID_ARG;
+    if (!out_layout_ok(out_sp, shard_pitch, S, N, c->m)) return RS_ERR_INVALID_ARG;
     a.plans = static_cast<const uint8_t*>(c->d_plans.p);
     a.present_masks = masks;
     return launch(c, a, c->m, true, s);
@@ -842,7 +851,7 @@ int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, con
     max_missing = std::max(max_missing, t - np);
   }
   if (max_missing == 0) return RS_OK;
-  if (out_sp < static_cast<size_t>(max_missing) * shard_pitch) return RS_ERR_INVALID_ARG;
+  if (!out_layout_ok(out_sp, shard_pitch, S, N, max_missing)) return RS_ERR_INVALID_ARG;
   if (n_masks == 1) {
     const uint8_t* plan = nullptr;
     int rc = uniform_plan(c, masks[0] & full, false, &plan);

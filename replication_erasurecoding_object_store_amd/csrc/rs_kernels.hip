@@ -262,44 +262,57 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 }
 
 // ---------------------------------------------------------------------------
-// Partial last column of every shard (S % 16 != 0) for the specialised kernels:
-// one thread per stripe.  The whole 16-B column lies inside the shard slot
-// (shard_pitch >= round_up(S, 16)), so inputs are read as one 16-B load each;
-// only the nb valid output bytes are stored.  Keeps the main loop branch-free.
-__global__ __launch_bounds__(256) void tail_kernel(const KernelArgs a, int per_stripe) {
+// Partial last column of every shard (S % 16 != 0) for the specialised kernels.
+// Thread (stripe i, output r): r = blockIdx.y is wave-uniform, so a uniform plan's
+// tables for row r come through scalar loads; stripes spread over the lanes.  The
+// whole 16-B column lies inside the shard slot (shard_pitch >= round_up(S, 16)),
+// so inputs are read as one 16-B load each; only the nb valid output bytes are
+// stored.  Keeps the main loop branch-free.
+template <int K, int M, bool PER_STRIPE>
+__global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  const uint32_t r = blockIdx.y;
+  if (i >= a.n_stripes) return;
   const uint32_t off = a.full_cols * 16u;
   const uint32_t nb = a.shard_len - off;  // 1..15
-  const int K = a.k, M = a.m;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_stripes; i += gridDim.x * blockDim.x) {
-    const uint8_t* plan = a.plans;
-    if (per_stripe) {
-      const uint32_t missing = (~a.present_masks[i]) & a.full_mask;
-      const uint32_t pid = a.lut[missing];
-      if (pid == kPlanInvalid) {
-        atomicOr(a.status, 1u);
-        continue;
-      }
-      plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
+  const uint8_t* plan;
+  uint32_t n_out, out_slot;
+  u32x4 y = u32x4{0u, 0u, 0u, 0u};
+  if constexpr (PER_STRIPE) {
+    const uint32_t missing = (~a.present_masks[i]) & a.full_mask;
+    const uint32_t pid = a.lut[missing];
+    if (pid == kPlanInvalid) {
+      if (r == 0) atomicOr(a.status, 1u);
+      return;
     }
+    plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
-    const uint32_t n_out = pw[0];
-    const uint32_t* idx = pw + 2;
-    const uint32_t* tab = reinterpret_cast<const uint32_t*>(plan + plan_tab_offset(K, M));
-    u32x4 y[kMaxM];
-    for (uint32_t r = 0; r < n_out; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
+    n_out = pw[0];
+    if (r >= n_out) return;
+    const uint32_t* tab = reinterpret_cast<const uint32_t*>(plan + plan_tab_offset(K, M)) + r * K * 5;
+#pragma unroll
     for (int c = 0; c < K; ++c) {
-      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, idx[c]) + off);
-      Idx3 ix[4];
+      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, pw[2 + c]) + off);
+      const uint32_t* tb = tab + c * 5;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) ix[d] = split3(x[d]);
-      for (uint32_t r = 0; r < n_out; ++r) {
-        const uint32_t* tb = tab + (r * K + c) * 5;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) y[r][d] ^= lookup3(ix[d], tb[0], tb[1], tb[2], tb[3], tb[4]);
-      }
+      for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), tb[0], tb[1], tb[2], tb[3], tb[4]);
     }
-    for (uint32_t r = 0; r < n_out; ++r) store_tail(out_ptr(a, K, i, r, idx[K + r]) + off, y[r], nb);
+    out_slot = pw[2 + K + r];
+  } else {
+    const PlanView pv(uniform_ptr(a.plans), K, M);
+    n_out = pv.n_out();
+    if (r >= n_out) return;
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, pv.in_idx(c)) + off);
+      const RS_CONST uint32_t* tb = pv.tab(static_cast<int>(r), c);
+      const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), q0, q1, q2, q3, q4);
+    }
+    out_slot = pv.out_idx(static_cast<int>(r));
   }
+  store_tail(out_ptr(a, K, i, r, out_slot) + off, y, nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -445,17 +458,19 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src
 // ---------------------------------------------------------------------------
 // Host-side launch dispatch.
 template <int K, int M, int E>
-static const void* spec_fn(bool per_stripe) {
+static const void* spec_fn(bool per_stripe, const void** tail) {
+  *tail = per_stripe ? reinterpret_cast<const void*>(&tail_kernel<K, M, true>)
+                     : reinterpret_cast<const void*>(&tail_kernel<K, M, false>);
   return per_stripe ? reinterpret_cast<const void*>(&apply_kernel<K, M, E, true>)
                     : reinterpret_cast<const void*>(&apply_kernel<K, M, E, false>);
 }
 
 // Specialised kernels: (K, M, E) with E <= M.
-static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name) {
+static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name, const void** tail) {
 #define RS_SPEC(KK, MM, EE)                                  \
   if (k == KK && m == MM && e == EE) {                       \
     *name = "apply_kernel<" #KK "," #MM "," #EE ">";         \
-    return spec_fn<KK, MM, EE>(per_stripe);                  \
+    return spec_fn<KK, MM, EE>(per_stripe, tail);            \
   }
   RS_SPEC(4, 2, 1) RS_SPEC(4, 2, 2)
   RS_SPEC(8, 4, 1) RS_SPEC(8, 4, 2) RS_SPEC(8, 4, 3) RS_SPEC(8, 4, 4)
@@ -466,10 +481,11 @@ static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** 
 }
 
 static const void* pick(const KernelArgs& a, int e, bool per_stripe, bool force_generic, bool* spec,
-                        const char** name) {
+                        const char** name, const void** tail) {
   *spec = false;
+  *tail = nullptr;
   if (!force_generic) {
-    if (const void* f = pick_spec(a.k, a.m, e, per_stripe, name)) {
+    if (const void* f = pick_spec(a.k, a.m, e, per_stripe, name, tail)) {
       *spec = true;
       return f;
     }
@@ -482,7 +498,8 @@ static const void* pick(const KernelArgs& a, int e, bool per_stripe, bool force_
 int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic) {
   bool spec;
   const char* name;
-  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name);
+  const void* tail;
+  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name, &tail);
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess || nb < 1) nb = 1;
   return nb;
@@ -492,7 +509,8 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
                          hipStream_t s, bool force_generic) {
   bool spec;
   const char* name;
-  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name);
+  const void* tail;
+  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name, &tail);
   const uint32_t bps = spec ? a.blocks_full : a.blocks_per_stripe;
   const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
   if (waves > 0) {
@@ -503,8 +521,9 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
     if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   }
   if (spec && a.full_cols * 16u != a.shard_len) {
-    const uint32_t g = (a.n_stripes + 255u) / 256u;
-    hipLaunchKernelGGL(tail_kernel, dim3(g < 4096u ? g : 4096u), dim3(256), 0, s, a, per_stripe ? 1 : 0);
+    void* args[] = {const_cast<KernelArgs*>(&a)};
+    const dim3 g((a.n_stripes + 63u) / 64u, static_cast<uint32_t>(e));
+    if (hipLaunchKernel(tail, g, dim3(64), args, 0, s) != hipSuccess) return nullptr;
   }
   return name;
 }

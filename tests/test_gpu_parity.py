@@ -569,3 +569,42 @@ def test_verify_batch_host_and_per_object(engines):
     for i in (6, 7, 1234):
         shards = [bytearray(data[i, j]) for j in range(k)] + [bytearray(parity[i, j]) for j in range(m)]
         assert eng.Verify(shards) == (bad[i] == 0)
+
+
+@pytest.mark.parametrize("k,m,S", [(4, 2, 1024), (10, 4, 6554), (4, 2, 100)])
+def test_soa_layout_device(engines, k, m, S):
+    """SURVEY §8d config 2's strided SoA variant: shard s of every stripe in one
+    plane, data [K, N, P] / parity [M, N, P] (shard pitch = N*P, stripe pitch = P).
+    Same bytes as the split layout."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    N = 999
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S + k)
+    data = torch.randint(0, 256, (k, N, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((m, N, P), 0x77, dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N, shard_pitch=N * P, data_stripe_pitch=P, parity_stripe_pitch=P)
+    ref_d = data.permute(1, 0, 2).contiguous()
+    ref_p = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(ref_d, ref_p, S, N)
+    torch.cuda.synchronize()
+    assert torch.equal(parity.permute(1, 0, 2)[:, :, :S], ref_p[:, :, :S])
+    assert (parity[:, :, S:] == 0x77).all()
+    # per-stripe 2-erasure reconstruct, out of place, SoA out [M, N, P]
+    rng = np.random.default_rng(S)
+    t = k + m
+    masks = _masks_upto(rng, N, t, m)
+    out = torch.full((m, N, P), 0x55, dtype=torch.uint8, device="cuda")
+    _lib_out = __import__("replication_erasurecoding_object_store_amd._lib", fromlist=["lib"])
+    rc = _lib_out.lib().rs_reconstruct_batch_out(
+        eng.ctx, data.data_ptr(), P, parity.data_ptr(), P, N * P, S, N,
+        masks.ctypes.data, N, 0, out.data_ptr(), P, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    full = torch.cat([data, parity], dim=0).cpu().numpy()  # [t, N, P]
+    got = out.cpu().numpy()
+    for i in range(N):
+        missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+        for r, j in enumerate(missing):
+            assert np.array_equal(got[r, i, :S], full[j, i, :S]), (i, r, j)
