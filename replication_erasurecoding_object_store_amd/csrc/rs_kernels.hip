@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rs_plan.hpp"
 
 namespace rs {
@@ -40,6 +42,11 @@ namespace rs {
 #define RS_OPAQUE_INPUT_TABLES 1
 #endif
 constexpr bool kOpaqueInputTables = RS_OPAQUE_INPUT_TABLES != 0;
+// A/B knob: 0 = per-stripe kernels always compute all E outputs.
+#ifndef RS_SPLIT_OUTPUTS
+#define RS_SPLIT_OUTPUTS 1
+#endif
+constexpr bool kSplitOutputs = RS_SPLIT_OUTPUTS != 0;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -76,8 +83,24 @@ __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
 }
 
+// Stores the first nbytes (< 16) of v at a 16-B aligned p with at most 4 naturally
+// aligned stores (8, 4, 2, 1 B) instead of one store per byte.
 __device__ __forceinline__ void store_tail(uint8_t* p, u32x4 v, uint32_t nbytes) {
-  for (uint32_t q = 0; q < nbytes; ++q) p[q] = static_cast<uint8_t>(v[q >> 2] >> (8 * (q & 3)));
+  uint32_t q = 0;  // bytes stored so far (multiple of the next store's size)
+  if (nbytes & 8u) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(v[0], v[1]);
+    q = 8;
+  }
+  if (nbytes & 4u) {
+    *reinterpret_cast<uint32_t*>(p + q) = v[q >> 2];
+    q += 4;
+  }
+  const uint32_t w = q < 16u ? v[q >> 2] : 0u;  // dword holding the remaining 1-3 bytes
+  if (nbytes & 2u) {
+    *reinterpret_cast<uint16_t*>(p + q) = static_cast<uint16_t>(w);
+    q += 2;
+  }
+  if (nbytes & 1u) p[q] = static_cast<uint8_t>(w >> (8 * (q & 3u)));
 }
 
 __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -161,6 +184,12 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     u32x4 y[E], pend[E];
 #pragma unroll
     for (int r = 0; r < E; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
+    // Per-stripe batches carry mixed patterns: rows [kLo, E) are only computed
+    // when this task's plan fills more than kLo shards (a wave-uniform branch per
+    // input), so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs
+    // do half the lookups.  Skipped rows are stored to scratch, never to memory.
+    constexpr int kLo = (PER_STRIPE && kSplitOutputs && E >= 4) ? E / 2 : E;
+    const bool hi_rows = kLo == E || pv.n_out() > static_cast<uint32_t>(kLo);
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       Idx3 ix[4];
@@ -171,19 +200,30 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       const uint8_t* tcol = plan;
       if constexpr (kOpaqueInputTables && K * E * 5 > 48) asm volatile("" : "+s"(tcol));
       const PlanView pc(tcol, K, M);
+      auto rows = [&](auto lo_tag, auto hi_tag, const PlanView& pt) {
+        constexpr int R0 = decltype(lo_tag)::value, R1 = decltype(hi_tag)::value;
 #pragma unroll
-      for (int r = 0; r < E; ++r) {
-        const RS_CONST uint32_t* tb = pc.tab(r, c);
-        const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
+        for (int r = R0; r < R1; ++r) {
+          const RS_CONST uint32_t* tb = pt.tab(r, c);
+          const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
-          if (c & 1)
-            y[r][d] = xor3(y[r][d], pend[r][d], prod);
-          else if (c == K - 1)
-            y[r][d] ^= prod;
-          else
-            pend[r][d] = prod;
+          for (int d = 0; d < 4; ++d) {
+            const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
+            if (c & 1)
+              y[r][d] = xor3(y[r][d], pend[r][d], prod);
+            else if (c == K - 1)
+              y[r][d] ^= prod;
+            else
+              pend[r][d] = prod;
+          }
+        }
+      };
+      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo>{}, pc);
+      if constexpr (kLo < E) {
+        if (hi_rows) {
+          const uint8_t* thi = plan;  // the high rows' tables load inside the branch
+          asm volatile("" : "+s"(thi));
+          rows(std::integral_constant<int, kLo>{}, std::integral_constant<int, E>{}, PlanView(thi, K, M));
         }
       }
       if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);

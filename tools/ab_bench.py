@@ -45,6 +45,10 @@ def main():
         "rs104_64K_rec2p": (10, 4, 6554, 16384, "rec2p"),
         "rs84_64K_enc": (8, 4, 8192, 16384, "enc"),
         "rs42_4K_ver": (4, 2, 1024, 65536, "ver"),
+        "rs42_4K_rec1p_out": (4, 2, 1024, 65536, "rec1p_out"),
+        "rs104_64K_rec1p_out": (10, 4, 6554, 16384, "rec1p_out"),
+        "rs104_64K_rec4p_out": (10, 4, 6554, 16384, "rec4p_out"),
+        "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
         "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
         "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
     }
@@ -73,9 +77,15 @@ def main():
             ch = pairs[rng.integers(0, len(pairs), N)]
             masks_np.append(((1 << t) - 1 & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32))
         masks = [torch.from_numpy(mm.view(np.int32)).cuda() for mm in masks_np]
+        one = ((1 << t) - 1) & ~(1 << rng.integers(0, t, N))
+        masks1 = torch.from_numpy(one.astype(np.uint32).view(np.int32)).cuda()
+        four = np.array([((1 << t) - 1) & ~sum(1 << int(j) for j in rng.choice(t, size=min(4, m), replace=False))
+                         for _ in range(N)], np.uint32)
+        masks4 = torch.from_numpy(four.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
-        alg = N * S * (k + (m if mode in ("enc", "ver") else 2))
+        e_out = {"rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
+        alg = N * S * (k + (m if mode in ("enc", "ver") else e_out))
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
         def run(i):
@@ -92,6 +102,10 @@ def main():
                 eng.reconstruct(d, p, S, N, 0b101101)
             elif mode == "rec45p":
                 eng.reconstruct_devmask(d, p, S, N, m45)
+            elif mode == "rec1p_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks1)
+            elif mode == "rec4p_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks4)
             elif mode == "rec2p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
             elif mode == "rec2u_out":
