@@ -47,6 +47,11 @@ constexpr bool kOpaqueInputTables = RS_OPAQUE_INPUT_TABLES != 0;
 #define RS_SPLIT_OUTPUTS 1
 #endif
 constexpr bool kSplitOutputs = RS_SPLIT_OUTPUTS != 0;
+// A/B knob: 1 = the main kernel also does the partial last column (no tail launch).
+#ifndef RS_FUSED_TAIL
+#define RS_FUSED_TAIL 1
+#endif
+constexpr bool kFusedTail = RS_FUSED_TAIL != 0;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -126,6 +131,9 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
   return a.out ? a.out + static_cast<uint64_t>(stripe) * a.out_sp + static_cast<uint64_t>(r) * a.shard_pitch
                : slot_ptr(a, k, stripe, slot);
 }
+
+template <int K, int M, bool PER_STRIPE>
+__device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint32_t r);
 
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
@@ -236,6 +244,19 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     }
   }
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
+  if constexpr (kFusedTail) {
+    // the partial last column of every stripe (S % 16 != 0): tail tasks of 64
+    // stripes x one output row, picked up by waves as they leave the main loop
+    // (saves the tail launch and its gap; see tail_kernel)
+    if (a.full_cols * 16u != a.shard_len) {
+      const uint32_t ttasks = ((a.n_stripes + 63u) / 64u) * static_cast<uint32_t>(E);
+      for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
+        const uint32_t r = tt % static_cast<uint32_t>(E);
+        const uint32_t i = (tt / static_cast<uint32_t>(E)) * 64u + lane;
+        if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, r);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -309,14 +330,9 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 // so inputs are read as one 16-B load each; only the nb valid output bytes are
 // stored.  Keeps the main loop branch-free.
 template <int K, int M, bool PER_STRIPE>
-__global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
-  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
-  const uint32_t r = blockIdx.y;
-  if (i >= a.n_stripes) return;
+__device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint32_t r) {
   const uint32_t off = a.full_cols * 16u;
   const uint32_t nb = a.shard_len - off;  // 1..15
-  const uint8_t* plan;
-  uint32_t n_out, out_slot;
   u32x4 y = u32x4{0u, 0u, 0u, 0u};
   if constexpr (PER_STRIPE) {
     const uint32_t missing = (~a.present_masks[i]) & a.full_mask;
@@ -325,10 +341,9 @@ __global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
       if (r == 0) atomicOr(a.status, 1u);
       return;
     }
-    plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
+    const uint8_t* plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
-    n_out = pw[0];
-    if (r >= n_out) return;
+    if (r >= pw[0]) return;
     const uint32_t* tab = reinterpret_cast<const uint32_t*>(plan + plan_tab_offset(K, M)) + r * K * 5;
 #pragma unroll
     for (int c = 0; c < K; ++c) {
@@ -337,11 +352,10 @@ __global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
 #pragma unroll
       for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), tb[0], tb[1], tb[2], tb[3], tb[4]);
     }
-    out_slot = pw[2 + K + r];
+    store_tail(out_ptr(a, K, i, r, pw[2 + K + r]) + off, y, nb);
   } else {
     const PlanView pv(uniform_ptr(a.plans), K, M);
-    n_out = pv.n_out();
-    if (r >= n_out) return;
+    if (r >= pv.n_out()) return;
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, pv.in_idx(c)) + off);
@@ -350,9 +364,14 @@ __global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
 #pragma unroll
       for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), q0, q1, q2, q3, q4);
     }
-    out_slot = pv.out_idx(static_cast<int>(r));
+    store_tail(out_ptr(a, K, i, r, pv.out_idx(static_cast<int>(r))) + off, y, nb);
   }
-  store_tail(out_ptr(a, K, i, r, out_slot) + off, y, nb);
+}
+
+template <int K, int M, bool PER_STRIPE>
+__global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, blockIdx.y);
 }
 
 // ---------------------------------------------------------------------------
@@ -552,7 +571,12 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
   const void* tail;
   const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name, &tail);
   const uint32_t bps = spec ? a.blocks_full : a.blocks_per_stripe;
-  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
+  const bool has_tail = spec && a.full_cols * 16u != a.shard_len;
+  uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
+  if (has_tail && kFusedTail) {
+    const uint64_t tail_tasks = (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * static_cast<uint64_t>(e);
+    if (tail_tasks > waves) waves = tail_tasks;
+  }
   if (waves > 0) {
     const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
     const uint64_t need = (waves + 3) / 4;
@@ -560,7 +584,7 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
     void* args[] = {const_cast<KernelArgs*>(&a)};
     if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   }
-  if (spec && a.full_cols * 16u != a.shard_len) {
+  if (has_tail && !kFusedTail) {
     void* args[] = {const_cast<KernelArgs*>(&a)};
     const dim3 g((a.n_stripes + 63u) / 64u, static_cast<uint32_t>(e));
     if (hipLaunchKernel(tail, g, dim3(64), args, 0, s) != hipSuccess) return nullptr;
