@@ -419,6 +419,47 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
     return res
 
 
+def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
+    """Batched SHA-256 of N device-resident objects (the reference's cold_hash,
+    writeservice.go:51-54) vs hashlib (OpenSSL) on the host cores."""
+    import hashlib
+
+    g = torch.Generator(device="cuda").manual_seed(0x5EED0007)
+    bufs = [torch.randint(0, 256, (N, length), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
+    out = torch.empty((N, 32), dtype=torch.uint8, device="cuda")
+    eng.sha256(bufs[0], length, N, digests=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(reps):
+        eng.sha256(bufs[i % 2], length, N, digests=out)
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / reps * 1e-3
+    host = bufs[(reps - 1) % 2][:256].cpu().numpy()
+    ok = all(out[i].cpu().numpy().tobytes() == hashlib.sha256(host[i].tobytes()).digest() for i in range(0, 256, 17))
+    # host baseline: SHA-NI (the class of Go crypto/sha256's amd64 code) on all
+    # host threads, over a sample of the same objects, timed to ~cpu_seconds
+    sys.path.insert(0, ROOT)
+    from oracle import rs_oracle
+
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    sample = bufs[0][:8192].cpu().numpy()
+    ns, t_cpu, ni = 0, 0.0, False
+    while t_cpu < cpu_seconds:
+        t0 = time.perf_counter()
+        _, ni = rs_oracle.baseline_sha256_batch(sample, length, length, sample.shape[0], threads)
+        t_cpu += time.perf_counter() - t0
+        ns += sample.shape[0]
+    cpu_rate = ns * length / t_cpu / GiB
+    del bufs
+    torch.cuda.empty_cache()
+    return {"objects": N, "object_bytes": length, "ms": round(sec * 1e3, 4), "GiBps": round(N * length / sec / GiB, 1),
+            "objects_per_s": round(N / sec), "ok": ok,
+            "cpu_baseline_GiBps": round(cpu_rate, 2), "cpu_threads": threads,
+            "cpu_kind": "port (oracle/sha256_cpu_baseline.c, " + ("SHA-NI" if ni else "scalar") + ")"}
+
+
 def pmc_traffic():
     """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
@@ -533,6 +574,7 @@ def main():
         e2.close()
         extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 1 << 18)
         extras["healer_mix_config5"] = healer_mix(torch, eng, k, m, S, 1 << 20)
+        extras["sha256_cold_hash_4KiB"] = sha256_rate(torch, eng)
         out["extras"] = extras
     if rank == 0:
         line = json.dumps(out)

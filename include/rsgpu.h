@@ -193,6 +193,20 @@ int rs_co_encode_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards
 int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
                 uint64_t *max_batch);
 
+/* ---- batched SHA-256 (cold_hash next to encode) -----
+ * The reference hashes every EC-written value (writeservice.go:51-54
+ * computeSHA256Hex, stored as "cold_hash" :267, compared :326-327).  Digest i
+ * (32 bytes, FIPS 180-4 byte order) of message i goes to digests + 32*i.  Device
+ * memory (or pinned host memory the GPU can address), asynchronous on `stream`;
+ * digests 4-B aligned.
+ *   rs_sha256_batch:     message i = base + i*stride, `len` bytes each
+ *   rs_sha256_batch_var: message i = base + offsets[i], lens[i] bytes (device
+ *                        arrays of n uint64) */
+int rs_sha256_batch(rs_ctx *ctx, const uint8_t *base, size_t stride, size_t len, size_t n,
+                    uint8_t *digests, void *stream);
+int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offsets,
+                        const uint64_t *lens, size_t n, uint8_t *digests, void *stream);
+
 /* ---- host memory helpers ------------------------------------------------ */
 int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin: DMA + zero-copy */
 int rs_host_unregister(rs_ctx *ctx, void *ptr);

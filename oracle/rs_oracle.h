@@ -85,6 +85,15 @@ int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_id
                              const int *out_idx, uint8_t *base, size_t stripe_pitch,
                              size_t shard_pitch, size_t S, size_t N, int threads);
 
+
+/* ---- SHA-256 (FIPS 180-4), the reference's cold_hash (writeservice.go:51-54,267) ---- */
+void rso_sha256(const uint8_t *msg, size_t len, uint8_t out[32]);
+void rso_sha256_batch(const uint8_t *base, size_t stride, const uint64_t *lens, size_t len, size_t n,
+                      uint8_t *out);
+/* CPU baseline (SHA-NI, threads); returns 1 if SHA-NI ran */
+int rso_baseline_sha256_batch(const uint8_t *base, size_t stride, size_t len, size_t n, uint8_t *out,
+                              int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,11 @@ def lib() -> ctypes.CDLL:
         L.rso_shard_size.argtypes = [ctypes.c_int, ctypes.c_size_t]
         L.rso_encode_batch_scalar.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
                                               ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
+        L.rso_sha256.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.rso_sha256_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_size_t, ctypes.c_void_p]
+        L.rso_baseline_sha256_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                                ctypes.c_void_p, ctypes.c_int]
         L.rso_baseline_apply_batch.argtypes = [
             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]
@@ -147,3 +152,30 @@ def baseline_apply_batch(k: int, rows: np.ndarray, in_idx: Sequence[int], out_id
     return lib().rso_baseline_apply_batch(k, e, rows.ctypes.data, ctypes.cast(ii, ctypes.c_void_p),
                                           ctypes.cast(oo, ctypes.c_void_p), buf.ctypes.data, stripe_pitch,
                                           shard_pitch, S, N, threads)
+
+
+def sha256(msg: bytes) -> bytes:
+    """FIPS 180-4 SHA-256 (writeservice.go:51-54 computeSHA256Hex's Sum256)."""
+    buf = (ctypes.c_uint8 * max(1, len(msg))).from_buffer_copy(msg or b"\0")
+    out = (ctypes.c_uint8 * 32)()
+    lib().rso_sha256(ctypes.cast(buf, ctypes.c_void_p), len(msg), ctypes.cast(out, ctypes.c_void_p))
+    return bytes(out)
+
+
+def sha256_batch(base: np.ndarray, stride: int, n: int, length: int = 0, lens=None) -> np.ndarray:
+    """Digests [n, 32] of n messages at base + i*stride (lens[i] or `length` bytes)."""
+    out = np.zeros((n, 32), np.uint8)
+    lp = None
+    if lens is not None:
+        lens = np.ascontiguousarray(lens, np.uint64)
+        lp = lens.ctypes.data
+    lib().rso_sha256_batch(base.ctypes.data, stride, lp, length, n, out.ctypes.data)
+    return out
+
+
+def baseline_sha256_batch(base: np.ndarray, stride: int, length: int, n: int, threads: int):
+    """CPU baseline (SHA-NI on `threads` host threads): (digests [n, 32], used_sha_ni)."""
+    assert base.nbytes >= (n - 1) * stride + length
+    out = np.zeros((n, 32), np.uint8)
+    ni = lib().rso_baseline_sha256_batch(base.ctypes.data, stride, length, n, out.ctypes.data, threads)
+    return out, bool(ni)

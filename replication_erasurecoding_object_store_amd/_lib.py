@@ -61,6 +61,8 @@ SIGNATURES = {
     "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
     "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
     "rs_sync": (_i, [_vp, _vp]),
+    "rs_sha256_batch": (_i, [_vp, _vp, _sz, _sz, _sz, _vp, _vp]),
+    "rs_sha256_batch_var": (_i, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     "rs_coalescer_create": (_i, [_vp, _vp, _vp]),
     "rs_coalescer_destroy": (None, [_vp]),
     "rs_co_encode": (_i, [_vp, _u8pp, _szp]),

@@ -104,6 +104,30 @@ class BatchEngine(Service):
                                           shard_len, n_stripes, bad.data_ptr(), _lib.RS_MEM_DEVICE,
                                           _stream_handle(stream)))
 
+    def sha256(self, data, length: int, n: int, stride: Optional[int] = None, digests=None, stream=None):
+        """SHA-256 of n device messages at data + i*stride (`length` bytes each) ->
+        uint8 [n, 32] device tensor (the reference's cold_hash).  Asynchronous."""
+        import torch
+
+        if digests is None:
+            digests = torch.empty((n, 32), dtype=torch.uint8, device=data.device)
+        st = stride if stride is not None else length
+        _check(_lib.lib().rs_sha256_batch(self.ctx, data.data_ptr(), st, length, n, digests.data_ptr(),
+                                          _stream_handle(stream)))
+        return digests
+
+    def sha256_var(self, base, offsets, lens, digests=None, stream=None):
+        """Variable-length messages: base (uint8 device tensor), offsets / lens
+        (int64 device tensors of n) -> uint8 [n, 32]."""
+        import torch
+
+        n = offsets.numel()
+        if digests is None:
+            digests = torch.empty((n, 32), dtype=torch.uint8, device=base.device)
+        _check(_lib.lib().rs_sha256_batch_var(self.ctx, base.data_ptr(), offsets.data_ptr(), lens.data_ptr(), n,
+                                              digests.data_ptr(), _stream_handle(stream)))
+        return digests
+
     # ---- device-resident, unified layout ------------------------------------------
     def encode_unified(self, buf, shard_len: int, shard_pitch: int, n_stripes: int, stream=None) -> None:
         """buf: [n_stripes, k+m, shard_pitch] uint8 device tensor; fills parity slots."""

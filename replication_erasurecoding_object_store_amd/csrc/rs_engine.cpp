@@ -31,6 +31,7 @@
 #include "gf256.hpp"
 #include "rs_host_util.hpp"
 #include "rs_plan.hpp"
+#include "rs_sha256.hpp"
 
 namespace {
 
@@ -950,6 +951,34 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
   c->last_kernel.store("copy_kernel");
   RS_HIP(hipGetLastError());
+  return RS_OK;
+}
+
+// Batched SHA-256 (the reference's cold_hash, writeservice.go:51-54): device-resident
+// messages, asynchronous on `stream`.
+int rs_sha256_batch(rs_ctx* c, const uint8_t* base, size_t stride, size_t len, size_t n, uint8_t* digests,
+                    void* stream) {
+  if (!c || (n && (!base || !digests)) || n > 0xFFFFFFFFu || (n > 1 && stride < len) ||
+      reinterpret_cast<uintptr_t>(digests) % 4)
+    return RS_ERR_INVALID_ARG;
+  if (n == 0) return RS_OK;
+  (void)hipSetDevice(c->device);
+  const rs::Sha256Args a{base, stride, nullptr, nullptr, len, static_cast<uint32_t>(n), digests};
+  if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
+  c->last_kernel.store("sha256_kernel");
+  return RS_OK;
+}
+
+int rs_sha256_batch_var(rs_ctx* c, const uint8_t* base, const uint64_t* offsets, const uint64_t* lens, size_t n,
+                        uint8_t* digests, void* stream) {
+  if (!c || (n && (!base || !offsets || !lens || !digests)) || n > 0xFFFFFFFFu ||
+      reinterpret_cast<uintptr_t>(digests) % 4)
+    return RS_ERR_INVALID_ARG;
+  if (n == 0) return RS_OK;
+  (void)hipSetDevice(c->device);
+  const rs::Sha256Args a{base, 0, offsets, lens, 0, static_cast<uint32_t>(n), digests};
+  if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
+  c->last_kernel.store("sha256_kernel");
   return RS_OK;
 }
 

@@ -180,3 +180,48 @@ def test_xoshiro_pinned():
         xoshiro_bytes(0x5EED0002, 4096)).hexdigest()
     assert xoshiro_bytes(1, 16) != xoshiro_bytes(2, 16)
     assert xoshiro_bytes(1, 24)[:16] == xoshiro_bytes(1, 16)
+
+
+# ---- SHA-256 restatement (cold_hash, writeservice.go:51-54) -------------------------
+FIPS_VECTORS = [  # FIPS 180-2 Appendix B / NIST examples
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+]
+
+
+def test_sha256_oracle_fips_vectors():
+    for msg, hexd in FIPS_VECTORS:
+        assert rs_oracle.sha256(msg).hex() == hexd
+
+
+def test_sha256_oracle_matches_hashlib_all_padding_cases():
+    import hashlib
+
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 130)) + [1000, 4096, 65537]:
+        msg = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert rs_oracle.sha256(msg) == hashlib.sha256(msg).digest(), n
+    base = rng.integers(0, 256, 40 * 100, dtype=np.uint8)
+    lens = rng.integers(0, 100, 40)
+    got = rs_oracle.sha256_batch(base, 100, 40, lens=lens)
+    for i in range(40):
+        assert got[i].tobytes() == hashlib.sha256(base[i * 100:i * 100 + lens[i]].tobytes()).digest()
+
+
+def test_sha256_cpu_baseline_matches_oracle():
+    """The bench's CPU baseline (SHA-NI when present, else scalar) = the oracle."""
+    import os
+
+    rng = np.random.default_rng(3)
+    for length in (0, 1, 55, 56, 64, 100, 4096):
+        base = rng.integers(0, 256, 300 * (length + 5) + 1, dtype=np.uint8)
+        got, _ = rs_oracle.baseline_sha256_batch(base, length + 5, length, 300, 4)
+        assert np.array_equal(got, rs_oracle.sha256_batch(base, length + 5, 300, length=length)), length
+    os.environ["RSO_BASELINE_LEVEL"] = "0"
+    try:
+        got, ni = rs_oracle.baseline_sha256_batch(base, 4101, 4096, 50, 2)
+        assert not ni and np.array_equal(got, rs_oracle.sha256_batch(base, 4101, 50, length=4096))
+    finally:
+        del os.environ["RSO_BASELINE_LEVEL"]

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed) {
     for (int i = 0; i < 8; ++i) {
       if constexpr (OP == 0) v[i] = __builtin_amdgcn_perm(t1, v[i], v[(i + 1) & 7] & 0x07070707u);  // perm + and
       if constexpr (OP == 1) v[i] = __builtin_amdgcn_bitop3_b32(v[i], v[(i + 3) & 7], t0, 0x96);
-      if constexpr (OP == 2) v[i] = (v[i] >> 3) & t0;
+      if constexpr (OP == 2) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(v[(i + 5) & 7]));
       if constexpr (OP == 3) v[i] = __builtin_amdgcn_perm(t1, t0, v[i]);  // perm only (sel = data)
     }
   }
@@ -39,8 +39,8 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  const char* names[] = {"v_perm+v_and (2 instr)", "v_bitop3", "v_lshrrev+v_and (2 instr)", "v_perm"};
-  const int per_iter[] = {16, 8, 16, 8};
+  const char* names[] = {"v_perm+v_and (2 instr)", "v_bitop3", "v_xor_b32", "v_perm"};
+  const int per_iter[] = {16, 8, 8, 8};
   for (int op = 0; op < 4; ++op) {
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: wps*4 waves per CU = wps blocks of 256
       const int grid = cus * wps;
