@@ -481,7 +481,13 @@ def main():
 
     rank, local, world = rdist.world()
     if world > 1:
-        rdist.init("nccl")  # RCCL; control collectives only (barrier, max time)
+        # RCCL; control collectives only (barrier, max time).  RSGPU_BENCH_BACKEND=gloo
+        # runs them on the CPU instead, so the N>1 path can be rehearsed with several
+        # ranks sharing one GPU (the driver's multi-GPU runs use the default).
+        backend = os.environ.get("RSGPU_BENCH_BACKEND", "nccl")
+        if backend == "gloo":
+            torch.cuda.set_device(local % torch.cuda.device_count())
+        rdist.init(backend)
     else:
         torch.cuda.set_device(0)
 
