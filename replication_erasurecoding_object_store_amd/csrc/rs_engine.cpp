@@ -174,6 +174,7 @@ struct rs_ctx {
   int k = 0, m = 0, device = 0, cu_count = 0;
   int blocks_per_cu = kDefaultBlocksPerCu;
   bool force_generic = false;
+  bool bitsliced = false;  // generated encode XOR program matches enc (rs_create)
   std::string backend;
   Matrix enc;
 
@@ -241,8 +242,11 @@ rs::KernelArgs make_args(rs_ctx* c, const Layout& L, size_t S, size_t N) {
 
 // e = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
 // #missing for per-stripe patterns).
-int launch(rs_ctx* c, const rs::KernelArgs& a, int e, bool per_stripe, hipStream_t s) {
-  if (a.n_stripes == 0 || a.shard_len == 0 || e <= 0) return RS_OK;
+int launch(rs_ctx* c, const rs::KernelArgs& args, int e, bool per_stripe, hipStream_t s) {
+  if (args.n_stripes == 0 || args.shard_len == 0 || e <= 0) return RS_OK;
+  rs::KernelArgs a = args;
+  // the encode plan with a verified generated XOR program -> bitsliced kernel
+  a.encode_net = (c->bitsliced && !per_stripe && a.plans == c->d_enc_plan.p) ? 1u : 0u;
   const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, e);
   const char* name = rs::launch_apply(a, e, per_stripe, static_cast<uint32_t>(bpc),
                                       static_cast<uint32_t>(c->cu_count), s, c->force_generic);
@@ -617,6 +621,13 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
   if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("RSGPU_FORCE_GENERIC")) c->force_generic = std::atoi(e) != 0;
   if (const char* e = std::getenv("RSGPU_HOST_ZERO_COPY")) c->host_zero_copy = std::atoi(e) != 0;
+  if (const uint8_t* rows = rs::bitsliced_encode_rows(k, m)) {
+    bool same = true;
+    for (int r = 0; r < m; ++r)
+      for (int q = 0; q < k; ++q) same = same && rows[r * k + q] == c->enc.at(k + r, q);
+    c->bitsliced = same;
+  }
+  if (const char* e = std::getenv("RSGPU_BITSLICED")) c->bitsliced = c->bitsliced && std::atoi(e) != 0;
   char name[160];
   std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
   c->backend = name;

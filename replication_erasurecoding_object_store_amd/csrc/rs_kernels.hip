@@ -375,6 +375,126 @@ __global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Bitsliced encode for the fixed encode matrices of the specialised shapes.
+//
+// GF(2^8) multiplication by a constant is an 8x8 matrix over GF(2).  With 32
+// bytes of a shard bitsliced into 8 dwords (plane j = bit j of each byte), a
+// parity plane is the XOR of the data planes its bit matrix selects: full-rate
+// v_xor_b32 where the lookup kernel spends half-rate v_perm_b32 / v_bitop3_b32
+// (tools/valu_probe.hip).  The encode matrix of RS(K, M) is fixed, so the XOR
+// program is generated at build time with shared subexpressions
+// (tools/gen_xor_networks.py -> rs_xor_networks.inc).  Per 32-byte column of a
+// stripe: one 8x8 bit transpose per data and per parity shard (3 delta-swap
+// stages, its own inverse) plus the program (RS(10+4): 682 XORs vs the lookup
+// kernel's 320 perms + 160 bitop3 + 80 index ops for the same bytes).
+template <int K, int M>
+struct BsNet {
+  static constexpr bool kAvailable = false;
+};
+template <int K, int M, int C>
+__device__ __forceinline__ void bs_step(const uint32_t (&x)[8], uint32_t (&y)[8 * M]);
+
+#include "rs_xor_networks.inc"
+
+// 8x8 bit transpose in every byte lane across 8 dwords: afterwards dword r, byte
+// b, bit q = bit r of byte b of the original dword q.  An involution.
+__device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
+  auto swap = [&](int a, int b, int sh, uint32_t mask) {
+    const uint32_t t = ((d[a] >> sh) ^ d[b]) & mask;
+    d[b] ^= t;
+    d[a] ^= t << sh;
+  };
+  swap(0, 4, 4, 0x0F0F0F0Fu);
+  swap(1, 5, 4, 0x0F0F0F0Fu);
+  swap(2, 6, 4, 0x0F0F0F0Fu);
+  swap(3, 7, 4, 0x0F0F0F0Fu);
+  swap(0, 2, 2, 0x33333333u);
+  swap(1, 3, 2, 0x33333333u);
+  swap(4, 6, 2, 0x33333333u);
+  swap(5, 7, 2, 0x33333333u);
+  swap(0, 1, 1, 0x55555555u);
+  swap(2, 3, 1, 0x55555555u);
+  swap(4, 5, 1, 0x55555555u);
+  swap(6, 7, 1, 0x55555555u);
+}
+
+// Inputs stream through a window of kBsWindow loads in flight: input c+W is
+// loaded once input c has been transposed, so only W inputs' raw bytes are live
+// (registers for more waves) while W 2 KiB loads per wave stay in flight.
+#ifndef RS_BS_WINDOW
+#define RS_BS_WINDOW 5
+#endif
+constexpr int kBsWindow = RS_BS_WINDOW;
+
+template <int K, int M, int C>
+__device__ __forceinline__ void bs_fold(const uint8_t* dbase, uint64_t pitch, uint32_t off_a, uint32_t off_b,
+                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&y)[8 * M]) {
+  if constexpr (C < K) {
+    constexpr int slot = C % kBsWindow;
+    uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
+                     xb[slot][0], xb[slot][1], xb[slot][2], xb[slot][3]};
+    if constexpr (C + kBsWindow < K) {
+      xa[slot] = load16(dbase + static_cast<uint64_t>(C + kBsWindow) * pitch + off_a);
+      xb[slot] = load16(dbase + static_cast<uint64_t>(C + kBsWindow) * pitch + off_b);
+    }
+    transpose8(d);
+    bs_step<K, M, C>(d, y);
+    bs_fold<K, M, C + 1>(dbase, pitch, off_a, off_b, xa, xb, y);
+  }
+}
+
+// Task = one stripe's 2 KiB column block: lane l owns the 16 B at l*16 and at
+// 1024 + l*16 of the block in every shard (two coalesced 1 KiB wave accesses per
+// shard).  Same branch-free memory discipline as apply_kernel: invalid halves load
+// from column 0 and store to the wave's scratch line.
+#ifndef RS_BS_MIN_WAVES
+#define RS_BS_MIN_WAVES 3
+#endif
+template <int K, int M>
+__global__ __launch_bounds__(256, RS_BS_MIN_WAVES) void encode_bitsliced_kernel(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t bps = (a.full_cols + 127u) / 128u;
+  const uint32_t ntasks = a.n_stripes * bps;
+  uint8_t* const dummy = a.scratch + (wave & 255u) * 1024u + lane * 16u;
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
+    const uint32_t col_a = blk * 128u + lane, col_b = col_a + 64u;
+    const bool va = col_a < a.full_cols, vb = col_b < a.full_cols;
+    const uint32_t off_a = va ? col_a * 16u : 0u, off_b = vb ? col_b * 16u : 0u;
+    const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
+    u32x4 xa[kBsWindow], xb[kBsWindow];
+#pragma unroll
+    for (int c = 0; c < kBsWindow && c < K; ++c) {
+      xa[c] = load16(dbase + static_cast<uint64_t>(c) * a.shard_pitch + off_a);
+      xb[c] = load16(dbase + static_cast<uint64_t>(c) * a.shard_pitch + off_b);
+    }
+    uint32_t y[8 * M];
+    bs_fold<K, M, 0>(dbase, a.shard_pitch, off_a, off_b, xa, xb, y);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      uint32_t d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
+      transpose8(d);
+      uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + static_cast<uint64_t>(r) * a.shard_pitch;
+      store16(va ? pbase + off_a : dummy, u32x4{d[0], d[1], d[2], d[3]});
+      store16(vb ? pbase + off_b : dummy, u32x4{d[4], d[5], d[6], d[7]});
+    }
+  }
+  if (a.full_cols * 16u != a.shard_len) {  // partial last column: the lookup path
+    const uint32_t ttasks = ((a.n_stripes + 63u) / 64u) * static_cast<uint32_t>(M);
+    for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
+      const uint32_t r = tt % static_cast<uint32_t>(M);
+      const uint32_t i = (tt / static_cast<uint32_t>(M)) * 64u + lane;
+      if (i < a.n_stripes) tail_task<K, M, false>(a, i, r);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Verify / scrub ([upstream reedsolomon.go Verify]: re-encode and compare; the
 // reference lists bit-rot detection as missing, docs/ARCHITECTURE.md:175-178).
 // Same lookup arithmetic as apply_kernel, but the M stored parity columns are
@@ -564,8 +684,53 @@ int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, 
   return nb;
 }
 
+template <int K, int M>
+static const void* bitsliced_fn() {
+  if constexpr (BsNet<K, M>::kAvailable) return reinterpret_cast<const void*>(&encode_bitsliced_kernel<K, M>);
+  return nullptr;
+}
+
+const uint8_t* bitsliced_encode_rows(int k, int m) {
+#define RS_BS(KK, MM) \
+  if (k == KK && m == MM) return BsNet<KK, MM>::kRows;
+  RS_BS(8, 4) RS_BS(10, 4)
+#undef RS_BS
+  return nullptr;
+}
+
+static const void* pick_bitsliced(int k, int m, const char** name) {
+#define RS_BS(KK, MM)                                   \
+  if (k == KK && m == MM) {                             \
+    *name = "encode_bitsliced_kernel<" #KK "," #MM ">"; \
+    return bitsliced_fn<KK, MM>();                      \
+  }
+  // (4,2) and (6,3) are memory-bound on the lookup kernel already, and the
+  // bitsliced one was slower / level there (profiles/r01_ab_bitsliced*.log)
+  RS_BS(8, 4) RS_BS(10, 4)
+#undef RS_BS
+  return nullptr;
+}
+
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
                          hipStream_t s, bool force_generic) {
+  if (a.encode_net && !per_stripe && !force_generic && e == a.m) {
+    const char* name = nullptr;
+    if (const void* fn = pick_bitsliced(a.k, a.m, &name)) {
+      const uint64_t bps = (static_cast<uint64_t>(a.full_cols) + 127u) / 128u;
+      uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
+      if (a.full_cols * 16u != a.shard_len) {
+        const uint64_t tail_tasks = (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * static_cast<uint64_t>(a.m);
+        if (tail_tasks > waves) waves = tail_tasks;
+      }
+      if (waves == 0) return name;
+      const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
+      const uint64_t need = (waves + 3) / 4;
+      const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
+      void* args[] = {const_cast<KernelArgs*>(&a)};
+      if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
+      return name;
+    }
+  }
   bool spec;
   const char* name;
   const void* tail;

@@ -81,7 +81,14 @@ struct KernelArgs {
   uint8_t* out;                    // null: outputs in place (slot addresses); else the
   uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
   uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
+  uint32_t encode_net;             // 1: uniform plan is the encode matrix and the generated
+                                   //    bitsliced XOR program for (k, m) matches it
 };
+
+// Parity rows the generated bitsliced encode program of (k, m) was derived from
+// (rs_xor_networks.inc), or nullptr if there is none.  The engine enables the
+// bitsliced kernel only if they equal its runtime encode matrix.
+const uint8_t* bitsliced_encode_rows(int k, int m);
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
 // e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or

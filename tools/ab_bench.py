@@ -49,6 +49,7 @@ def main():
         "rs104_64K_rec1p_out": (10, 4, 6554, 16384, "rec1p_out"),
         "rs104_64K_rec4p_out": (10, 4, 6554, 16384, "rec4p_out"),
         "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
+        "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),
         "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
         "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
     }

@@ -20,15 +20,20 @@ LINE = re.compile(r"^(\S+)\s+v\d+ bpc=\s*(\d+): median\s+([\d.]+) GB/s")
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--libs", required=True)
+    ap.add_argument("--libs", default="", help="comma-separated alternative builds of librsgpu.so")
+    ap.add_argument("--env-variants", default="",
+                    help="comma-separated VAR=VALUE settings, each run as its own variant on the default build")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--timeout", type=int, default=240, help="seconds per child run")
     args, rest = ap.parse_known_args()
-    libs = [os.path.abspath(x) for x in args.libs.split(",")]
+    variants = [(os.path.basename(x), {"RSGPU_LIB": os.path.abspath(x)}) for x in args.libs.split(",") if x]
+    for ev in [e for e in args.env_variants.split(",") if e]:
+        k, v = ev.split("=", 1)
+        variants.append((ev, {k: v}))
     res = defaultdict(list)
     for rnd in range(args.rounds):
-        for lib in libs:
-            env = dict(os.environ, RSGPU_LIB=lib)
+        for lib, extra in variants:
+            env = dict(os.environ, **extra)
             cmd = [sys.executable, os.path.join(HERE, "ab_bench.py"), "--rounds", "1", *rest]
             p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.timeout)
             if p.returncode != 0:
@@ -37,10 +42,10 @@ def main():
             for line in p.stdout.splitlines():
                 mm = LINE.match(line)
                 if mm:
-                    res[(mm.group(1), int(mm.group(2)), os.path.basename(lib))].append(float(mm.group(3)))
+                    res[(mm.group(1), int(mm.group(2)), lib)].append(float(mm.group(3)))
                 elif "parity-consistent" in line and "True" not in line:
                     raise SystemExit(f"parity check failed for {lib}: {line}")
-            print(f"round {rnd} {os.path.basename(lib)} done", flush=True)
+            print(f"round {rnd} {lib} done", flush=True)
     for key in sorted(res):
         v = res[key]
         print(f"{key[0]:20s} bpc={key[1]:2d} {key[2]:28s} median {np.median(v):7.1f} GB/s "

@@ -1,0 +1,177 @@
+"""Generates csrc/rs_xor_networks.inc: bitsliced encode XOR programs for the fixed
+encode matrices of the specialised (K, M) shapes.
+
+Why: GF(2^8) multiplication by a constant f is GF(2)-linear, an 8x8 bit matrix.
+With the data bitsliced (plane j = bit j of 32 bytes in one dword), one parity
+plane is the XOR of the data planes whose matrix bit is set: full-rate v_xor_b32
+instead of half-rate v_perm_b32 lookups (tools/valu_probe.hip).  The encode matrix
+of RS(K, M) is fixed ([upstream klauspost matrix.go buildMatrix]: vandermonde(K+M,
+K) x inv(top K x K)), so its XOR program is known at build time and common
+subexpressions can be shared.
+
+Inputs are streamed one at a time (input c's 8 planes are live only while its
+contributions are folded into the 8M output planes), and the common pairs inside
+one input's 8M row subsets are shared by Paar's greedy algorithm (repeatedly
+materialise the pair that occurs in the most rows).  The generated step for input
+c is straight-line code:  t_i = a ^ b; ...; y[p] = / ^= <one value>.
+
+Also emitted: the parity rows each program was derived from (rs_create checks
+them against the runtime encode matrix before the bitsliced kernel may run).
+
+Usage: python tools/gen_xor_networks.py  (writes the .inc; committed)
+"""
+from __future__ import annotations
+
+import os
+from collections import Counter
+
+SHAPES = [(4, 2), (8, 4), (10, 4), (6, 3)]
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "replication_erasurecoding_object_store_amd", "csrc", "rs_xor_networks.inc")
+
+# ---- GF(2^8), poly 0x11d, generator 2 ([upstream klauspost galois.go]) ------------
+EXP = [0] * 512
+LOG = [0] * 256
+x = 1
+for i in range(255):
+    EXP[i] = x
+    LOG[x] = i
+    x <<= 1
+    if x & 0x100:
+        x ^= 0x11D
+for i in range(255, 512):
+    EXP[i] = EXP[i - 255]
+
+
+def mul(a: int, b: int) -> int:
+    return 0 if a == 0 or b == 0 else EXP[LOG[a] + LOG[b]]
+
+
+def gpow(a: int, n: int) -> int:
+    if n == 0:
+        return 1
+    return 0 if a == 0 else EXP[(LOG[a] * n) % 255]
+
+
+def inv_matrix(a):
+    n = len(a)
+    w = [row[:] + [1 if i == r else 0 for i in range(n)] for r, row in enumerate(a)]
+    for col in range(n):
+        piv = next(r for r in range(col, n) if w[r][col])
+        w[col], w[piv] = w[piv], w[col]
+        s = EXP[255 - LOG[w[col][col]]]
+        w[col] = [mul(v, s) for v in w[col]]
+        for r in range(n):
+            if r != col and w[r][col]:
+                f = w[r][col]
+                w[r] = [v ^ mul(f, u) for v, u in zip(w[r], w[col])]
+    return [row[n:] for row in w]
+
+
+def parity_rows(k: int, m: int):
+    v = [[gpow(r, c) for c in range(k)] for r in range(k + m)]
+    ti = inv_matrix(v[:k])
+    enc = [[0] * k for _ in range(k + m)]
+    for r in range(k + m):
+        for c in range(k):
+            acc = 0
+            for i in range(k):
+                acc ^= mul(v[r][i], ti[i][c])
+            enc[r][c] = acc
+    return enc[k:]
+
+
+# ---- XOR programs ---------------------------------------------------------------
+def input_rows(rows, k, m, c):
+    """For input c: output plane p = (r*8 + i) needs XOR of planes {j : bit i of
+    f_rc * 2^j}."""
+    out = []
+    for r in range(m):
+        f = rows[r][c]
+        for i in range(8):
+            out.append(frozenset(j for j in range(8) if (mul(f, 1 << j) >> i) & 1))
+    return out
+
+
+def paar(subsets):
+    """Greedy common-pair elimination.  Returns (temps, rows): temps = list of
+    (name, a, b); rows = list of sets of operand names (x<j> / t<i>)."""
+    rows = [set(f"x{j}" for j in s) for s in subsets]
+    temps = []
+    while True:
+        cnt = Counter()
+        for r in rows:
+            ls = sorted(r)
+            for a in range(len(ls)):
+                for b in range(a + 1, len(ls)):
+                    cnt[(ls[a], ls[b])] += 1
+        if not cnt:
+            break
+        (a, b), n = max(cnt.items(), key=lambda kv: (kv[1], kv[0]))
+        if n < 2:
+            break
+        name = f"t{len(temps)}"
+        temps.append((name, a, b))
+        for r in rows:
+            if a in r and b in r:
+                r.discard(a)
+                r.discard(b)
+                r.add(name)
+    return temps, rows
+
+
+def emit_step(k, m, c, rows):
+    subsets = input_rows(rows, k, m, c)
+    temps, red = paar(subsets)
+    lines = [f"template <> __device__ __forceinline__ void bs_step<{k}, {m}, {c}>(const uint32_t (&x)[8], "
+             f"uint32_t (&y)[{8 * m}]) {{"]
+    nx = 0
+    for name, a, b in temps:
+        lines.append(f"  const uint32_t {name} = {a.replace('x', 'x[') + ']' if a[0] == 'x' else a} ^ "
+                     f"{b.replace('x', 'x[') + ']' if b[0] == 'x' else b};")
+        nx += 1
+    for p, r in enumerate(red):
+        ops = [o.replace("x", "x[") + "]" if o[0] == "x" else o for o in sorted(r)]
+        if not ops:
+            if c == 0:
+                lines.append(f"  y[{p}] = 0u;")
+            continue
+        expr = " ^ ".join(ops)
+        nx += len(ops) - 1
+        if c == 0:
+            lines.append(f"  y[{p}] = {expr};")
+        else:
+            lines.append(f"  y[{p}] ^= {expr};")
+            nx += 1
+    lines.append("}")
+    return lines, nx
+
+
+def main():
+    out = ["// rs_xor_networks.inc -- GENERATED by tools/gen_xor_networks.py; do not edit.",
+           "// Bitsliced encode XOR programs for the fixed RS(K, M) encode matrices",
+           "// ([upstream klauspost matrix.go buildMatrix]); see rs_kernels.hip.", ""]
+    summary = []
+    for k, m in SHAPES:
+        rows = parity_rows(k, m)
+        total = 0
+        out.append(f"// ---- RS({k}+{m}) parity rows: {rows}")
+        flat = ", ".join(str(v) for r in rows for v in r)
+        out.append(f"template <> struct BsNet<{k}, {m}> {{")
+        out.append("  static constexpr bool kAvailable = true;")
+        out.append(f"  static constexpr uint8_t kRows[{k * m}] = {{{flat}}};")
+        out.append("};")
+        for c in range(k):
+            lines, nx = emit_step(k, m, c, rows)
+            out += lines
+            total += nx
+        out.append("")
+        summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column")
+    out.insert(3, "// " + "; ".join(summary))
+    with open(OUT, "w") as f:
+        f.write("\n".join(out) + "\n")
+    print("\n".join(summary))
+
+
+if __name__ == "__main__":
+    main()
