@@ -49,13 +49,28 @@ using Clock = std::chrono::steady_clock;
 
 enum class Kind : int { kApply = 0, kVerify = 1 };
 
+// Slot reservation is one CAS on `ticket` = [generation:24 | closed:1 | count:39].
+// A batch is opened (generation bumped, count 0) under rs_coalescer::mu; from then
+// on callers of its shard length reserve slots WITHOUT the mutex (through
+// rs_coalescer::hot or the open map) until it is closed -- full, or by its leader.
+// With callers outnumbering cores, a reservation mutex convoys: a preempted holder
+// stalls every caller behind it.
+constexpr uint64_t kClosedBit = 1ull << 39;
+constexpr uint64_t kCountMask = kClosedBit - 1;
+constexpr int kGenShift = 40;
+
 struct Batch {
-  enum class State { kFree, kOpen, kClosed };
-  State state = State::kFree;  // guarded by rs_coalescer::mu
+  int index = 0;               // position in rs_coalescer::batches (the hot-slot id)
+  bool free = true;            // guarded by rs_coalescer::mu
+  uint32_t gen = 0;            // generation of the current / last open period (mu)
   Kind kind = Kind::kApply;
-  size_t S = 0, P = 0, cap = 0;
-  size_t reserved = 0;         // guarded by mu while open; fixed once closed
-  bool parity_in = false;      // some slot needs its parity shards uploaded
+  size_t S = 0, P = 0;
+  std::atomic<size_t> cap{0};
+  std::atomic<int> key_kind{-1};      // (kind, S) of the current generation, published
+  std::atomic<uint64_t> key_S{0};     //   before `ticket` (read racily by the fast path)
+  std::atomic<uint64_t> ticket{kClosedBit};
+  std::atomic<uint32_t> parity_in{0};  // some slot needs its parity shards uploaded
+  size_t n_final = 0;          // slots of the closed batch (published by done_gen)
   int rc = RS_OK;              // published by done_gen
   Clock::time_point deadline;
   // Lock-free completion: callers stage, wait and drain without the mutex, so a
@@ -69,6 +84,23 @@ struct Batch {
   // region offsets (same in host staging and device slab)
   size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_bad = 0, bytes = 0;
 };
+
+// Reserves up to `want` consecutive slots of batch b in generation gen.
+// Returns the number taken (0: closed, full or another generation).
+size_t try_reserve(Batch* b, uint32_t gen, size_t want, size_t* slot0) {
+  uint64_t t = b->ticket.load(std::memory_order_acquire);
+  for (;;) {
+    const size_t cap = b->cap.load(std::memory_order_relaxed);
+    const size_t cnt = static_cast<size_t>(t & kCountMask);
+    if (static_cast<uint32_t>(t >> kGenShift) != (gen & 0xFFFFFFu) || (t & kClosedBit) || cnt >= cap) return 0;
+    const size_t take = std::min(want, cap - cnt);
+    if (b->ticket.compare_exchange_weak(t, t + take, std::memory_order_acq_rel, std::memory_order_acquire)) {
+      *slot0 = cnt;
+      return take;
+    }
+  }
+}
+
 static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
 
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected) {
@@ -105,7 +137,8 @@ struct rs_coalescer {
   std::condition_variable leader_cv;  // batch full / an execution slot freed
   std::vector<std::unique_ptr<Batch>> batches;
   std::vector<Batch*> free_list;
-  std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots
+  std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots (mu)
+  std::atomic<uint64_t> hot{0};  // last opened batch: (gen << 8) | (index + 1); 0 = none
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
 
@@ -130,22 +163,26 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
   (void)hipSetDevice(co->device);
   const size_t per = b->P * (k + 2 * m) + 8;
-  b->cap = std::max<size_t>(1, std::min(co->max_batch, co->max_bytes / per));
+  const size_t cap = std::max<size_t>(1, std::min(co->max_batch, co->max_bytes / per));
+  b->cap.store(cap, std::memory_order_relaxed);
   b->o_data = 0;
-  b->o_parity = round_up(b->cap * k * b->P, 256);
-  b->o_out = b->o_parity + round_up(b->cap * m * b->P, 256);
-  b->o_masks = b->o_out + round_up(b->cap * m * b->P, 256);
-  b->o_bad = b->o_masks + round_up(b->cap * 4, 256);
-  b->bytes = b->o_bad + round_up(b->cap * 4, 256);
+  b->o_parity = round_up(cap * k * b->P, 256);
+  b->o_out = b->o_parity + round_up(cap * m * b->P, 256);
+  b->o_masks = b->o_out + round_up(cap * m * b->P, 256);
+  b->o_bad = b->o_masks + round_up(cap * 4, 256);
+  b->bytes = b->o_bad + round_up(cap * 4, 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
-  b->reserved = 0;
   b->filled.store(0, std::memory_order_relaxed);
   b->released.store(0, std::memory_order_relaxed);
-  b->parity_in = false;
+  b->parity_in.store(0, std::memory_order_relaxed);
   b->rc = RS_OK;
-  b->state = Batch::State::kOpen;
+  b->free = false;
   b->deadline = Clock::now() + co->max_wait;
+  b->gen = (b->gen + 1) & 0xFFFFFFu;
+  b->key_kind.store(static_cast<int>(kind), std::memory_order_relaxed);
+  b->key_S.store(S, std::memory_order_relaxed);
+  b->ticket.store(static_cast<uint64_t>(b->gen) << kGenShift, std::memory_order_release);  // open, count 0
   return RS_OK;
 }
 
@@ -164,7 +201,7 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
   auto at = [&](size_t off) { return base + off; };
   if (!zc) {
     RS_HIP(hipMemcpyAsync(dev_at(b, b->o_data), host_at(b, b->o_data), n * k * P, hipMemcpyHostToDevice, st));
-    if (b->parity_in || b->kind == Kind::kVerify)
+    if (b->parity_in.load(std::memory_order_relaxed) || b->kind == Kind::kVerify)
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_parity), host_at(b, b->o_parity), n * m * P, hipMemcpyHostToDevice, st));
     if (b->kind == Kind::kApply && co->per_stripe)
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
@@ -200,56 +237,91 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
 // since the batch opened (default 0).  Callers that arrive while earlier batches
 // are on the device pile into the open batch, so batches grow with the load and a
 // lone caller pays no timer.
+// Takes batch b (generation gen) out of the open map / hot slot (under mu).
+void unpublish(rs_coalescer* co, Batch* b, uint32_t gen) {
+  const auto key = std::make_pair(static_cast<int>(b->kind), b->S);
+  auto it = co->open.find(key);
+  if (it != co->open.end() && it->second == b) co->open.erase(it);
+  uint64_t h = co->hot.load(std::memory_order_relaxed);
+  const uint64_t mine = (static_cast<uint64_t>(gen) << 8) | static_cast<uint64_t>(b->index + 1);
+  if (h == mine) co->hot.compare_exchange_strong(h, 0, std::memory_order_relaxed);
+}
+
 template <class Fill, class Drain>
 int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity_in, Fill&& fill, Drain&& drain) {
   const auto key = std::make_pair(static_cast<int>(kind), S);
   int result = RS_OK;
   size_t done_items = 0;
   while (done_items < count) {
-    std::unique_lock<std::mutex> lk(co->mu);
+    const size_t want = count - done_items;
     Batch* b = nullptr;
-    for (;;) {
-      auto it = co->open.find(key);
-      if (it != co->open.end()) {
-        b = it->second;
-        break;
+    uint32_t gen = 0;
+    size_t slot0 = 0, take = 0;
+    // fast path: the most recently opened batch, no mutex
+    if (const uint64_t h = co->hot.load(std::memory_order_acquire)) {
+      Batch* hb = co->batches[(h & 0xFF) - 1].get();
+      const uint32_t hg = static_cast<uint32_t>(h >> 8);
+      if (hb->key_kind.load(std::memory_order_relaxed) == key.first &&
+          hb->key_S.load(std::memory_order_relaxed) == key.second && (take = try_reserve(hb, hg, want, &slot0))) {
+        b = hb;
+        gen = hg;
       }
-      if (!co->free_list.empty()) {
-        b = co->free_list.back();
-        co->free_list.pop_back();
-        const int rc = prepare(co, b, kind, S);
-        if (rc) {
-          b->state = Batch::State::kFree;
-          co->free_list.push_back(b);
-          co->free_cv.notify_all();
-          return rc;
+    }
+    std::unique_lock<std::mutex> lk(co->mu, std::defer_lock);
+    if (!b) {
+      lk.lock();
+      for (;;) {
+        auto it = co->open.find(key);
+        if (it != co->open.end()) {
+          Batch* ob = it->second;
+          if ((take = try_reserve(ob, ob->gen, want, &slot0))) {
+            b = ob;
+            gen = ob->gen;
+            break;
+          }
+          co->open.erase(it);  // closed or full: stop offering it
+          continue;
         }
-        co->open[key] = b;
-        co->free_cv.notify_all();  // waiters for this S may join it
-        break;
+        if (!co->free_list.empty()) {
+          Batch* nb = co->free_list.back();
+          co->free_list.pop_back();
+          const int rc = prepare(co, nb, kind, S);
+          if (rc) {
+            nb->free = true;
+            co->free_list.push_back(nb);
+            co->free_cv.notify_all();
+            return rc;
+          }
+          take = try_reserve(nb, nb->gen, want, &slot0);  // slot 0: this caller leads
+          b = nb;
+          gen = nb->gen;
+          co->open[key] = nb;
+          co->hot.store((static_cast<uint64_t>(gen) << 8) | static_cast<uint64_t>(nb->index + 1),
+                        std::memory_order_release);
+          co->free_cv.notify_all();  // waiters for this S may join it
+          break;
+        }
+        co->free_cv.wait(lk);  // every batch is in flight: back-pressure
       }
-      co->free_cv.wait(lk);  // every batch is in flight: back-pressure
+      lk.unlock();
     }
-    // reserve a run of slots for this caller's next objects
-    const size_t take = std::min(count - done_items, b->cap - b->reserved);
-    const size_t slot0 = b->reserved;
-    b->reserved += take;
     const bool leader = slot0 == 0;
-    const uint32_t gen = b->done_gen.load(std::memory_order_relaxed);
-    b->parity_in |= parity_in;
-    if (b->reserved == b->cap) {  // full: no more slots
-      co->open.erase(key);
-      b->state = Batch::State::kClosed;
+    const uint32_t dgen = b->done_gen.load(std::memory_order_relaxed);
+    if (parity_in) b->parity_in.store(1, std::memory_order_relaxed);
+    if (slot0 + take == b->cap.load(std::memory_order_relaxed)) {  // took the last slot: close it
+      b->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
+      lk.lock();
+      unpublish(co, b, gen);
       co->leader_cv.notify_all();
+      lk.unlock();
     }
-    lk.unlock();
     for (size_t j = 0; j < take; ++j) fill(b, slot0 + j, done_items + j);
     b->filled.fetch_add(static_cast<uint32_t>(take), std::memory_order_release);
     if (leader) {
       lk.lock();
       // gather: until full, or (an execution slot is free and the linger is over)
       for (;;) {
-        if (b->state != Batch::State::kOpen) break;
+        if (b->ticket.load(std::memory_order_acquire) & kClosedBit) break;
         const bool slot_free = co->executing < co->max_exec;
         if (slot_free && Clock::now() >= b->deadline) break;
         if (slot_free)
@@ -257,16 +329,14 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
         else
           co->leader_cv.wait(lk);
       }
-      if (b->state == Batch::State::kOpen) {
-        auto it = co->open.find(key);
-        if (it != co->open.end() && it->second == b) co->open.erase(it);
-        b->state = Batch::State::kClosed;
-      }
+      const uint64_t t = b->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
+      const size_t n = static_cast<size_t>(t & kCountMask);
+      unpublish(co, b, gen);
       while (co->executing >= co->max_exec) co->leader_cv.wait(lk);
       ++co->executing;
-      const size_t n = b->reserved;
       lk.unlock();
       while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
+      b->n_final = n;
       const int rc = execute(co, b, n);
       co->n_batches.fetch_add(1, std::memory_order_relaxed);
       co->stripes.fetch_add(n, std::memory_order_relaxed);
@@ -281,19 +351,20 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
       b->done_gen.fetch_add(1, std::memory_order_release);
       futex_wake_all(&b->done_gen);
     } else {
-      wait_change(&b->done_gen, gen);
+      wait_change(&b->done_gen, dgen);
     }
     const int rc = b->rc;
-    const size_t n = b->reserved;  // fixed since the batch closed (published by done_gen)
+    const size_t n = b->n_final;  // published by done_gen
     if (rc == RS_OK)
       for (size_t j = 0; j < take; ++j) drain(b, slot0 + j, done_items + j);
     else if (result == RS_OK)
       result = rc;
     if (b->released.fetch_add(static_cast<uint32_t>(take), std::memory_order_acq_rel) + take == n) {
       lk.lock();
-      b->state = Batch::State::kFree;
+      b->free = true;
       co->free_list.push_back(b);
       co->free_cv.notify_all();
+      lk.unlock();
     }
     done_items += take;
   }
@@ -424,6 +495,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->zero_copy = o.staged_dma == 0;
   for (int i = 0; i < o.inflight; ++i) {
     co->batches.push_back(std::make_unique<Batch>());
+    co->batches.back()->index = i;
     co->free_list.push_back(co->batches.back().get());
   }
   *out = co.release();

@@ -15,7 +15,7 @@ from replication_erasurecoding_object_store_amd.coalescer import CoalescingServi
 from replication_erasurecoding_object_store_amd.ec import ECError, ErrShardNoData, ErrShardSize, ErrTooFewShards
 from replication_erasurecoding_object_store_amd.xoshiro import xoshiro_bytes
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 
 def _run_threads(n, fn):
@@ -190,5 +190,35 @@ def test_batch_healer_poller_semantics(gpu):
                 for j in lost:
                     assert r.repaired[j] == bytes(full[j])
         assert svc.stats()["batches"] == 1, "100 repairs of one shard length -> one launch"
+    finally:
+        svc.close()
+
+
+@pytest.mark.parametrize("max_batch,inflight", [(5, 2), (64, 4), (4096, 16)])
+def test_reservation_stress(gpu, max_batch, inflight):
+    """64 threads x 60 encodes of two interleaved shard lengths: the lock-free slot
+    reservation (CAS ticket, hot batch), full-batch closes and batch recycling
+    under contention; every result checked, every call accounted for."""
+    svc = CoalescingService(4, 2, max_batch=max_batch, inflight=inflight)
+    try:
+        refs = {}
+        for length in (4096, 1000):
+            data = xoshiro_bytes(length, length)
+            ref = rs_oracle.split(4, 2, data)
+            rs_oracle.encode(4, 2, ref)
+            refs[length] = (data, [bytes(x) for x in ref])
+
+        def worker(t):
+            for j in range(60):
+                length = 4096 if (t + j) % 3 else 1000
+                data, ref = refs[length]
+                shards = svc.Split(data)
+                svc.Encode(shards)
+                assert [bytes(x) for x in shards] == ref
+
+        _run_threads(64, worker)
+        st = svc.stats()
+        assert st["calls"] == 64 * 60 and st["stripes"] == 64 * 60
+        assert st["max_batch"] <= max_batch
     finally:
         svc.close()
