@@ -13,7 +13,7 @@ import threading
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librsgpu.so")
 # A/B tooling only (tools/ab_libs.py): load an alternative build of the same ABI.
-LIB_PATH = os.environ.get("RSGPU_LIB", LIB_PATH)
+LIB_PATH = os.path.abspath(os.environ.get("RSGPU_LIB") or LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "rsgpu.h")
 
 RS_OK = 0

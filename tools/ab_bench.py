@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--bpc", default="1,2,3,4,8")
     ap.add_argument("--variants", default="0")
     ap.add_argument("--workloads", default="all")
+    ap.add_argument("--pads", default="0", help="comma-separated extra bytes added to the shard pitch "
+                                                "(multiples of 16), each its own workload line")
     args = ap.parse_args()
     import torch
 
@@ -59,12 +61,17 @@ def main():
     bpcs = [int(b) for b in args.bpc.split(",")]
     results = {}
     engines = {}
-    for name, (k, m, S, N, mode) in workloads.items():
+    pads = [int(x) for x in args.pads.split(",")]
+    if pads != [0]:
+        workloads = {(f"{n}+{pad}" if pad else n): (*w, pad) for n, w in workloads.items() for pad in pads}
+    else:
+        workloads = {n: (*w, 0) for n, w in workloads.items()}
+    for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
         eng = engines[(k, m)]
         t = k + m
-        P = shard_pitch_for(S)
+        P = shard_pitch_for(S) + pad
         nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))
         g = torch.Generator(device="cuda").manual_seed(1)
         bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
