@@ -460,16 +460,18 @@ def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
             "cpu_kind": "port (oracle/sha256_cpu_baseline.c, " + ("SHA-NI" if ni else "scalar") + ")"}
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if any."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            return json.load(f)
-    except Exception:
-        return None
+def pmc_traffic(workload):
+    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary of this
+    workload (profiles/<tag>_pmc.json written by tools/prof_summary.py), if any."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except Exception:
+            continue
+        if doc.get("workload") == workload:
+            return doc
+    return None
 
 
 def main():
@@ -511,8 +513,8 @@ def main():
     dom = max(km, key=km.get) if km else "reconstruct"
     achieved = alg[dom] / (km.get(dom, float("nan")) * 1e-3) / 1e9 if km else None
     traffic = None
-    pmc = pmc_traffic()
-    if pmc and pmc.get("workload") == f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split":
+    pmc = pmc_traffic(f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split")
+    if pmc:
         traffic = pmc.get("hbm_bytes_per_launch", {}).get(dom)
 
     out = {

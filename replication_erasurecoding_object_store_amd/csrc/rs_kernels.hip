@@ -47,6 +47,32 @@ constexpr bool kOpaqueInputTables = RS_OPAQUE_INPUT_TABLES != 0;
 #define RS_SPLIT_OUTPUTS 1
 #endif
 constexpr bool kSplitOutputs = RS_SPLIT_OUTPUTS != 0;
+// A/B knob: 1 = per-stripe kernels sized for E >= 4 outputs also skip row 1 when a
+// stripe's plan fills a single shard (rows [0,1) [1,E/2) [E/2,E)).
+#ifndef RS_SPLIT_ROW1
+#define RS_SPLIT_ROW1 1
+#endif
+constexpr bool kSplitRow1 = RS_SPLIT_ROW1 != 0;
+// A/B knob: 1 = lanes past the last full column load the last full column (the
+// same lines as the wave's valid lanes), and stores that must not land (those
+// lanes; rows beyond a stripe plan's n_out) are raw buffer stores the hardware
+// drops on its range check -- no branch, no traffic.  0 = loads from column 0 and
+// stores into a scratch sink, whose lines get written back to HBM (PMC: +35-60 MB
+// per RS(10+4) launch, profiles/r01h_kmsweep_pmc.md).
+#ifndef RS_NO_SINK
+#define RS_NO_SINK 1
+#endif
+constexpr bool kNoSink = RS_NO_SINK != 0;
+// A/B knob: 1 = a fused tail task is one lane per stripe doing every output row
+// (the inputs' lines come from HBM once); 0 = one task per (64 stripes, row), run by
+// different waves, which re-read the inputs' lines from HBM once per row (PMC:
+// +37 MB per RS(10+4) launch).  Off: a full-suite run with it on hit one illegal
+// address fault (test_reconstruct_out_of_place[100-8-4]) that the test alone,
+// serialized, did not repeat; unresolved, so the proven scheme stays the default.
+#ifndef RS_TAIL_ALL_ROWS
+#define RS_TAIL_ALL_ROWS 0
+#endif
+constexpr bool kTailAllRows = RS_TAIL_ALL_ROWS != 0;
 // A/B knob: 1 = the main kernel also does the partial last column (no tail launch).
 #ifndef RS_FUSED_TAIL
 #define RS_FUSED_TAIL 1
@@ -110,12 +136,25 @@ __device__ __forceinline__ void store_tail(uint8_t* p, u32x4 v, uint32_t nbytes)
 
 __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Offset past every descriptor's range: a buffer store there is dropped.
+constexpr uint32_t kDropOffset = 0x80000000u;
+
 // Pins a wave-uniform pointer into SGPRs so loads through it stay scalar.
 __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
   const uint64_t v = reinterpret_cast<uint64_t>(p);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
   return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// 16-B non-temporal store at base + off, or nothing at all when !live: a raw buffer
+// store (descriptor over [base, base + 2 GiB)) whose offset then fails the range
+// check, so the hardware drops it -- no branch around the store and no sink line
+// to write back.  base must be wave-uniform; off < 2 GiB.
+__device__ __forceinline__ void store16_or_drop(uint8_t* base, uint32_t off, bool live, u32x4 v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, 0x7FFFFFFF,
+                                                      0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, live ? off : kDropOffset, 0, 2 /* nt */);
 }
 
 // Shard slot s of stripe i (s < k: data region, else parity region).
@@ -134,6 +173,30 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
 
 template <int K, int M, bool PER_STRIPE>
 __device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint32_t r);
+template <int K, int M, int E, bool PER_STRIPE>
+__device__ __forceinline__ void tail_stripe(const KernelArgs& a, uint32_t i);
+
+// The fused tail pass of a main kernel: the partial last column (S % 16 != 0) of
+// every stripe, picked up by waves as they leave the main loop (saves a tail
+// launch and its gap; see tail_kernel).
+template <int K, int M, int E, bool PER_STRIPE>
+__device__ __forceinline__ void fused_tail(const KernelArgs& a, uint32_t wave, uint32_t nwaves, uint32_t lane) {
+  if (a.full_cols * 16u == a.shard_len) return;
+  const uint32_t groups = (a.n_stripes + 63u) / 64u;
+  if constexpr (kTailAllRows) {
+    for (uint32_t g = wave; g < groups; g += nwaves) {
+      const uint32_t i = g * 64u + lane;
+      if (i < a.n_stripes) tail_stripe<K, M, E, PER_STRIPE>(a, i);
+    }
+  } else {
+    const uint32_t ttasks = groups * static_cast<uint32_t>(E);
+    for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
+      const uint32_t r = tt % static_cast<uint32_t>(E);
+      const uint32_t i = (tt / static_cast<uint32_t>(E)) * 64u + lane;
+      if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, r);
+    }
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
@@ -178,7 +241,8 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const PlanView pv(plan, K, M);
     const uint32_t col = blk * 64u + lane;
     const bool valid = col < a.full_cols;
-    const uint32_t off = valid ? col * 16u : 0u;  // clamped, never branched
+    // clamped, never branched
+    const uint32_t off = valid ? col * 16u : (kNoSink ? (a.full_cols - 1u) * 16u : 0u);
 
     u32x4 x[K];
 #pragma unroll
@@ -197,7 +261,9 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     // input), so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs
     // do half the lookups.  Skipped rows are stored to scratch, never to memory.
     constexpr int kLo = (PER_STRIPE && kSplitOutputs && E >= 4) ? E / 2 : E;
+    constexpr int kLo1 = (kLo < E && kSplitRow1) ? 1 : kLo;  // rows [kLo1, kLo) when n_out > kLo1
     const bool hi_rows = kLo == E || pv.n_out() > static_cast<uint32_t>(kLo);
+    const bool mid_rows = kLo1 == kLo || pv.n_out() > static_cast<uint32_t>(kLo1);
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       Idx3 ix[4];
@@ -226,7 +292,14 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
           }
         }
       };
-      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo>{}, pc);
+      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo1>{}, pc);
+      if constexpr (kLo1 < kLo) {
+        if (mid_rows) {
+          const uint8_t* tmid = plan;
+          asm volatile("" : "+s"(tmid));
+          rows(std::integral_constant<int, kLo1>{}, std::integral_constant<int, kLo>{}, PlanView(tmid, K, M));
+        }
+      }
       if constexpr (kLo < E) {
         if (hi_rows) {
           const uint8_t* thi = plan;  // the high rows' tables load inside the branch
@@ -239,24 +312,17 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t n_out = pv.n_out();
 #pragma unroll
     for (int r = 0; r < E; ++r) {
-      uint8_t* real = out_ptr(a, K, stripe, r, pv.out_idx(r)) + off;
-      store16((valid && static_cast<uint32_t>(r) < n_out) ? real : dummy, y[r]);
-    }
-  }
-  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
-  if constexpr (kFusedTail) {
-    // the partial last column of every stripe (S % 16 != 0): tail tasks of 64
-    // stripes x one output row, picked up by waves as they leave the main loop
-    // (saves the tail launch and its gap; see tail_kernel)
-    if (a.full_cols * 16u != a.shard_len) {
-      const uint32_t ttasks = ((a.n_stripes + 63u) / 64u) * static_cast<uint32_t>(E);
-      for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
-        const uint32_t r = tt % static_cast<uint32_t>(E);
-        const uint32_t i = (tt / static_cast<uint32_t>(E)) * 64u + lane;
-        if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, r);
+      if constexpr (kNoSink) {
+        store16_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, valid && static_cast<uint32_t>(r) < n_out,
+                        y[r]);
+      } else {
+        uint8_t* real = out_ptr(a, K, stripe, r, pv.out_idx(r)) + off;
+        store16((valid && static_cast<uint32_t>(r) < n_out) ? real : dummy, y[r]);
       }
     }
   }
+  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
+  if constexpr (kFusedTail) fused_tail<K, M, E, PER_STRIPE>(a, wave, nwaves, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -368,6 +434,15 @@ __device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint3
   }
 }
 
+// All output rows of stripe i's partial last column by one lane, rows in sequence:
+// the rows after the first re-read the same K input lines from this CU's caches
+// instead of HBM (rolled, so the main loop's VGPR budget is untouched).
+template <int K, int M, int E, bool PER_STRIPE>
+__device__ __forceinline__ void tail_stripe(const KernelArgs& a, uint32_t i) {
+#pragma unroll 1
+  for (uint32_t r = 0; r < static_cast<uint32_t>(E); ++r) tail_task<K, M, PER_STRIPE>(a, i, r);
+}
+
 template <int K, int M, bool PER_STRIPE>
 __global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
@@ -463,7 +538,8 @@ __global__ __launch_bounds__(256, RS_BS_MIN_WAVES) void encode_bitsliced_kernel(
     const uint32_t blk = t - stripe * bps;
     const uint32_t col_a = blk * 128u + lane, col_b = col_a + 64u;
     const bool va = col_a < a.full_cols, vb = col_b < a.full_cols;
-    const uint32_t off_a = va ? col_a * 16u : 0u, off_b = vb ? col_b * 16u : 0u;
+    const uint32_t clamp = kNoSink ? (a.full_cols - 1u) * 16u : 0u;
+    const uint32_t off_a = va ? col_a * 16u : clamp, off_b = vb ? col_b * 16u : clamp;
     const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
     u32x4 xa[kBsWindow], xb[kBsWindow];
 #pragma unroll
@@ -480,18 +556,16 @@ __global__ __launch_bounds__(256, RS_BS_MIN_WAVES) void encode_bitsliced_kernel(
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
       transpose8(d);
       uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + static_cast<uint64_t>(r) * a.shard_pitch;
-      store16(va ? pbase + off_a : dummy, u32x4{d[0], d[1], d[2], d[3]});
-      store16(vb ? pbase + off_b : dummy, u32x4{d[4], d[5], d[6], d[7]});
+      if constexpr (kNoSink) {
+        store16_or_drop(pbase, off_a, va, u32x4{d[0], d[1], d[2], d[3]});
+        store16_or_drop(pbase, off_b, vb, u32x4{d[4], d[5], d[6], d[7]});
+      } else {
+        store16(va ? pbase + off_a : dummy, u32x4{d[0], d[1], d[2], d[3]});
+        store16(vb ? pbase + off_b : dummy, u32x4{d[4], d[5], d[6], d[7]});
+      }
     }
   }
-  if (a.full_cols * 16u != a.shard_len) {  // partial last column: the lookup path
-    const uint32_t ttasks = ((a.n_stripes + 63u) / 64u) * static_cast<uint32_t>(M);
-    for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
-      const uint32_t r = tt % static_cast<uint32_t>(M);
-      const uint32_t i = (tt / static_cast<uint32_t>(M)) * 64u + lane;
-      if (i < a.n_stripes) tail_task<K, M, false>(a, i, r);
-    }
-  }
+  fused_tail<K, M, M, false>(a, wave, nwaves, lane);  // partial last column: the lookup path
 }
 
 // ---------------------------------------------------------------------------
@@ -719,7 +793,8 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
       const uint64_t bps = (static_cast<uint64_t>(a.full_cols) + 127u) / 128u;
       uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
       if (a.full_cols * 16u != a.shard_len) {
-        const uint64_t tail_tasks = (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * static_cast<uint64_t>(a.m);
+        const uint64_t tail_tasks =
+            (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * (kTailAllRows ? 1u : static_cast<uint64_t>(a.m));
         if (tail_tasks > waves) waves = tail_tasks;
       }
       if (waves == 0) return name;
@@ -739,7 +814,8 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
   const bool has_tail = spec && a.full_cols * 16u != a.shard_len;
   uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
   if (has_tail && kFusedTail) {
-    const uint64_t tail_tasks = (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * static_cast<uint64_t>(e);
+    const uint64_t tail_tasks =
+        (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * (kTailAllRows ? 1u : static_cast<uint64_t>(e));
     if (tail_tasks > waves) waves = tail_tasks;
   }
   if (waves > 0) {

@@ -14,6 +14,46 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+WORKLOADS = {
+    # name: (k, m, S, N, mode)  mode: enc | rec2u (uniform {0,1}) | rec2p (per-stripe 2-erasure)
+    "rs42_4K_enc": (4, 2, 1024, 65536, "enc"),
+    "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
+    "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
+    "rs42_4K_rec45p": (4, 2, 1024, 65536, "rec45p"),
+    "rs42_4K_rec2p_out": (4, 2, 1024, 65536, "rec2p_out"),
+    "rs42_4K_rec2u_out": (4, 2, 1024, 65536, "rec2u_out"),
+    "rs42_64K_rec2p_out": (4, 2, 16384, 16384, "rec2p_out"),
+    "rs104_64K_rec2p_out": (10, 4, 6554, 16384, "rec2p_out"),
+    "rs42_4K_rec45u": (4, 2, 1024, 65536, "rec45u"),
+    "rs42_4K_rec14u": (4, 2, 1024, 65536, "rec14u"),
+    "rs42_64K_enc": (4, 2, 16384, 16384, "enc"),
+    "rs42_64K_rec2p": (4, 2, 16384, 16384, "rec2p"),
+    "rs104_64K_enc": (10, 4, 6554, 16384, "enc"),
+    "rs104_64K_rec2p": (10, 4, 6554, 16384, "rec2p"),
+    "rs84_64K_enc": (8, 4, 8192, 16384, "enc"),
+    "rs42_4K_ver": (4, 2, 1024, 65536, "ver"),
+    "rs42_4K_rec1p_out": (4, 2, 1024, 65536, "rec1p_out"),
+    "rs104_64K_rec1p_out": (10, 4, 6554, 16384, "rec1p_out"),
+    "rs104_64K_rec4p_out": (10, 4, 6554, 16384, "rec4p_out"),
+    "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
+    "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),
+    "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
+    "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
+    # tail-free shard lengths next to the real 64 KiB ones (S % 16 == 0)
+    "rs104_S6656_enc": (10, 4, 6656, 16384, "enc"),
+    "rs104_S6656_rec1p_out": (10, 4, 6656, 16384, "rec1p_out"),
+    "rs104_S6656_rec2p_out": (10, 4, 6656, 16384, "rec2p_out"),
+    "rs104_S6144_enc": (10, 4, 6144, 16384, "enc"),
+}
+
+
+def alg_bytes(name):
+    """Algorithmic HBM bytes of one launch of workload `name`."""
+    k, m, S, N, mode = WORKLOADS[name]
+    e = {"enc": m, "ver": m, "rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
+    return N * S * (k + e)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
@@ -29,32 +69,7 @@ def main():
     from replication_erasurecoding_object_store_amd.batch import BatchEngine, shard_pitch_for
 
     GiB = 1 << 30
-    workloads = {
-        # name: (k, m, S, N, mode)  mode: enc | rec2u (uniform {0,1}) | rec2p (per-stripe 2-erasure)
-        "rs42_4K_enc": (4, 2, 1024, 65536, "enc"),
-        "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
-        "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
-        "rs42_4K_rec45p": (4, 2, 1024, 65536, "rec45p"),
-        "rs42_4K_rec2p_out": (4, 2, 1024, 65536, "rec2p_out"),
-        "rs42_4K_rec2u_out": (4, 2, 1024, 65536, "rec2u_out"),
-        "rs42_64K_rec2p_out": (4, 2, 16384, 16384, "rec2p_out"),
-        "rs104_64K_rec2p_out": (10, 4, 6554, 16384, "rec2p_out"),
-        "rs42_4K_rec45u": (4, 2, 1024, 65536, "rec45u"),
-        "rs42_4K_rec14u": (4, 2, 1024, 65536, "rec14u"),
-        "rs42_64K_enc": (4, 2, 16384, 16384, "enc"),
-        "rs42_64K_rec2p": (4, 2, 16384, 16384, "rec2p"),
-        "rs104_64K_enc": (10, 4, 6554, 16384, "enc"),
-        "rs104_64K_rec2p": (10, 4, 6554, 16384, "rec2p"),
-        "rs84_64K_enc": (8, 4, 8192, 16384, "enc"),
-        "rs42_4K_ver": (4, 2, 1024, 65536, "ver"),
-        "rs42_4K_rec1p_out": (4, 2, 1024, 65536, "rec1p_out"),
-        "rs104_64K_rec1p_out": (10, 4, 6554, 16384, "rec1p_out"),
-        "rs104_64K_rec4p_out": (10, 4, 6554, 16384, "rec4p_out"),
-        "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
-        "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),
-        "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
-        "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
-    }
+    workloads = dict(WORKLOADS)
     if args.workloads != "all":
         workloads = {k: v for k, v in workloads.items() if k in args.workloads.split(",")}
     variants = [int(v) for v in args.variants.split(",")]
@@ -92,8 +107,7 @@ def main():
         masks4 = torch.from_numpy(four.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
-        e_out = {"rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
-        alg = N * S * (k + (m if mode in ("enc", "ver") else e_out))
+        alg = alg_bytes(name.split("+")[0])
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
         def run(i):

@@ -29,6 +29,13 @@ def short(name: str) -> str:
     return name.replace("void ", "").split("(")[0]
 
 
+def full_size(vals):
+    if not vals:
+        return vals
+    med = statistics.median(vals)
+    return [v for v in vals if v >= 0.5 * med]
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     workload = sys.argv[3] if len(sys.argv) > 3 else ""
@@ -57,9 +64,11 @@ def main():
         if "rs::" not in name:
             continue
         gmax = max(g for g, *_ in lst)
-        durs = [d for g, d, *_ in lst if g == gmax]
-        f = [v for g, v in fetch.get(name, []) if g == gmax]
-        w = [v for g, v in write.get(name, []) if g == gmax]
+        # the grid is capped (CUs x blocks/CU), so small launches can share it:
+        # keep the dispatches near the median
+        durs = full_size([d for g, d, *_ in lst if g == gmax])
+        f = full_size([v for g, v in fetch.get(name, []) if g == gmax])
+        w = full_size([v for g, v in write.get(name, []) if g == gmax])
         fetch_b = statistics.mean(f) * 1024 * 2 if f else None
         write_b = statistics.mean(w) * 1024 if w else None
         summary[short(name)] = {
