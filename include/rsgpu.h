@@ -17,8 +17,15 @@
  *  - Thread safety: every function may be called concurrently on one context
  *    (the reference shares one IEcDriver across all request goroutines and the
  *    healer's workers: cmd/api/main.go:206, cmd/healer/main.go:42, poller.go:49).
- *  - No CPU fallback: rs_create fails with RS_ERR_NO_DEVICE when no gfx950 GPU is
- *    visible.  The library never computes parity on the host.
+ *  - Devices: a context spans one GPU (rs_create) or several (rs_create_multi,
+ *    rs_create_devices).  Calls never change the calling thread's current HIP
+ *    device.  Per-object calls and host-memory batches are spread over the
+ *    context's GPUs by the library; a device-memory batch runs on the GPU its
+ *    `stream` belongs to (the calling thread's current device for the NULL
+ *    stream), which the context must span.
+ *  - No CPU fallback in the library: creation fails with RS_ERR_NO_DEVICE when no
+ *    gfx950 GPU is visible and the library never computes parity on the host.  The
+ *    Go shim then falls back to klauspost itself.
  */
 #ifndef RSGPU_H
 #define RSGPU_H
@@ -52,14 +59,28 @@ typedef struct rs_ctx rs_ctx;
 
 /* ---- lifecycle ---------------------------------------------------------
  * Replaces reedsolomon.New(config.K, config.M, WithAutoGoroutines(NumCPU))
- * at internal/ec/ec.go:26.  k >= 1, m >= 0, k+m <= 256 (klauspost limits; the GPU
- * engine additionally needs k <= 32, m <= 16, k+m <= 32).  device = HIP ordinal.
+ * at internal/ec/ec.go:26.  k >= 1, m >= 0, k+m <= 256 (klauspost limits, checked
+ * first, same order and sentinels); the GPU engine additionally needs k <= 32,
+ * m <= 16, k+m <= 32 (RS_ERR_NOT_SUPPORTED).
+ *   rs_create:         one GPU, HIP ordinal `device`.
+ *   rs_create_multi:   the GPUs whose bit is set in device_mask (bit d = ordinal
+ *                      d); 0 = every visible gfx950 GPU.  SURVEY.md §8b's
+ *                      rs_create(k, m, device_mask, flags): what the Go shim's
+ *                      NewService calls, so one IEcDriver drives the whole node.
+ *   rs_create_devices: an explicit list of n_devices ordinals; an ordinal may
+ *                      repeat (several engines, each with its own streams and
+ *                      staging, on one GPU).
+ * RS_ERR_NO_DEVICE: no GPU visible, or a named ordinal missing / not gfx950.
  */
 int rs_create(int k, int m, int device, int flags, rs_ctx **out);
+int rs_create_multi(int k, int m, uint64_t device_mask, int flags, rs_ctx **out);
+int rs_create_devices(int k, int m, const int *devices, int n_devices, int flags, rs_ctx **out);
 void rs_destroy(rs_ctx *ctx);
 int rs_data_shards(const rs_ctx *ctx);
 int rs_parity_shards(const rs_ctx *ctx);
-int rs_device(const rs_ctx *ctx);
+int rs_device(const rs_ctx *ctx);               /* the first engine's ordinal */
+int rs_device_count(const rs_ctx *ctx);         /* engines in the context */
+int rs_device_at(const rs_ctx *ctx, int i);     /* ordinal of engine i (-1 if none) */
 /* Description of the backend for NewService's log line (ec.go:32-41). */
 const char *rs_backend(const rs_ctx *ctx);
 const char *rs_strerror(int code);
@@ -94,10 +115,12 @@ int rs_verify(rs_ctx *ctx, uint8_t *const *shards, const size_t *lens, int *ok);
  * RS_MEM_DEVICE: pitches must be multiples of 16 and shard_pitch >= round_up(S, 16),
  *   bases 16-B aligned (the kernels read whole 16-B columns; bytes of a slot past S
  *   may be read, never written).  The call enqueues on `stream` and returns;
- *   synchronise with hipStreamSynchronize or rs_sync.
- * RS_MEM_HOST: any pitches; the engine stages through pinned device slabs with
- *   H2D / kernel / D2H overlapped on several streams and returns when the outputs
- *   are in host memory (pin the buffers with rs_host_register for full speed).
+ *   synchronise with hipStreamSynchronize or rs_sync.  S up to 0xFFFFFFF0.
+ * RS_MEM_HOST: any pitches; pinned shards (rs_host_register / hipHostMalloc) are
+ *   read and written in place by the kernels (zero-copy), others are staged
+ *   through device slabs with H2D / kernel / D2H overlapped on several streams.
+ *   Returns when the outputs are in host memory.  A multi-GPU context splits the
+ *   batch into contiguous stripe ranges, one per GPU, run in parallel.
  *
  * rs_encode_batch: reads data shards, writes every parity shard.
  * rs_reconstruct_batch: in place.  present_masks: host array of n_masks uint32
@@ -115,7 +138,9 @@ int rs_reconstruct_batch(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch, u
                          void *stream);
 /* Device-resident masks (RS_MEM_DEVICE only, k+m <= 16): present_masks_dev is a
  * device array of n_stripes uint32.  Stripes with < k present are left untouched
- * and reported by the next rs_sync on that stream as RS_ERR_TOO_FEW_SHARDS. */
+ * and reported by the next rs_sync on THAT stream as RS_ERR_TOO_FEW_SHARDS (each
+ * stream has its own deferred-error word; rs_sync on another stream neither sees
+ * nor clears it). */
 int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch,
                                  uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
                                  size_t shard_len, size_t n_stripes,
@@ -208,7 +233,7 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
                         const uint64_t *lens, size_t n, uint8_t *digests, void *stream);
 
 /* ---- host memory helpers ------------------------------------------------ */
-int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin: DMA + zero-copy */
+int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin for every GPU: DMA + zero-copy */
 int rs_host_unregister(rs_ctx *ctx, void *ptr);
 
 /* ---- measurement helpers (bench.py) ------------------------------------- */

@@ -12,8 +12,6 @@ import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librsgpu.so")
-# A/B tooling only (tools/ab_libs.py): load an alternative build of the same ABI.
-LIB_PATH = os.path.abspath(os.environ.get("RSGPU_LIB") or LIB_PATH)
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "rsgpu.h")
 
 RS_OK = 0
@@ -43,6 +41,10 @@ _i = ctypes.c_int
 # name -> (restype, argtypes); mirrors include/rsgpu.h one for one.
 SIGNATURES = {
     "rs_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "rs_create_multi": (_i, [_i, _i, ctypes.c_uint64, _i, ctypes.POINTER(_vp)]),
+    "rs_create_devices": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)]),
+    "rs_device_count": (_i, [_vp]),
+    "rs_device_at": (_i, [_vp, _i]),
     "rs_destroy": (None, [_vp]),
     "rs_data_shards": (_i, [_vp]),
     "rs_parity_shards": (_i, [_vp]),

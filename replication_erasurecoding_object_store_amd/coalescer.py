@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import ctypes
 
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Union
 
 from . import _lib
 from .ec import ECError, ErrTooFewShards, M, K, Service, _check, _shard_array
@@ -24,7 +24,8 @@ class CoalescerOpts(ctypes.Structure):
 
 
 class CoalescingService(Service):
-    def __init__(self, k: int = K, m: int = M, device: int = 0, max_batch: int = 0, max_wait_us: int = 0,
+    def __init__(self, k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0, max_batch: int = 0,
+                 max_wait_us: int = 0,
                  inflight: int = 0, max_batch_bytes: int = 0, max_exec: int = 0, staged_dma: bool = False):
         super().__init__(k, m, device)
         opts = CoalescerOpts(max_batch, max_wait_us, inflight, max_batch_bytes, max_exec, int(staged_dma))

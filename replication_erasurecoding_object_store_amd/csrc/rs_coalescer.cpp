@@ -22,6 +22,12 @@
 // Up to `inflight` batches exist at once (each with its own stream, pinned and
 // device slab), so one batch's transfers overlap the next batch's filling.  All
 // arithmetic is the device kernels'; the host only moves bytes.
+//
+// A context spanning several GPUs (rs_create_multi) gives each GPU its own
+// batches: batch i belongs to engine i % n_engines, with its pinned staging on that
+// GPU's NUMA node and its stream / slab on that GPU.  A new batch is opened on the
+// engine with the fewest batches open or executing, so concurrent callers spread
+// over every GPU while a lone caller still sees one batch at a time.
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
 #include <sys/syscall.h>
@@ -41,6 +47,7 @@
 #include <vector>
 
 #include "../../include/rsgpu.h"
+#include "rs_engine.hpp"
 #include "rs_host_util.hpp"
 
 namespace {
@@ -61,6 +68,7 @@ constexpr int kGenShift = 40;
 
 struct Batch {
   int index = 0;               // position in rs_coalescer::batches (the hot-slot id)
+  int engine = 0;              // the GPU (engine index in the context) this batch runs on
   bool free = true;            // guarded by rs_coalescer::mu
   uint32_t gen = 0;            // generation of the current / last open period (mu)
   Kind kind = Kind::kApply;
@@ -123,28 +131,32 @@ void wait_change(std::atomic<uint32_t>* w, uint32_t v) {
 
 struct rs_coalescer {
   rs_ctx* ctx = nullptr;
-  int k = 0, m = 0, device = 0;
+  int k = 0, m = 0;
   bool per_stripe = false;  // k+m <= 16: per-stripe masks (reconstruct coalesces)
   size_t max_batch = 0, max_bytes = 0;
   std::chrono::microseconds max_wait{0};
 
-  int max_exec = 2;   // batches on the device at once
+  int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
-  int executing = 0;
 
   std::mutex mu;
   std::condition_variable free_cv;    // a batch became free (or opened)
   std::condition_variable leader_cv;  // batch full / an execution slot freed
   std::vector<std::unique_ptr<Batch>> batches;
   std::vector<Batch*> free_list;
+  std::vector<int> engine_load;   // batches open or executing per engine (mu)
+  std::vector<int> engine_exec;   // batches executing per engine (mu)
   std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots (mu)
-  std::atomic<uint64_t> hot{0};  // last opened batch: (gen << 8) | (index + 1); 0 = none
+  std::atomic<uint64_t> hot{0};  // last opened batch: hot_word(gen, index); 0 = none
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
 
   ~rs_coalescer() {
-    for (auto& b : batches)
+    for (auto& b : batches) {
+      rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(ctx, b->engine)));
       if (b->stream) (void)hipStreamDestroy(b->stream);
+      b.reset();  // slabs freed on their device
+    }
   }
 };
 
@@ -161,7 +173,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->kind = kind;
   b->S = S;
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
-  (void)hipSetDevice(co->device);
+  rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, b->engine)));
   const size_t per = b->P * (k + 2 * m) + 8;
   const size_t cap = std::max<size_t>(1, std::min(co->max_batch, co->max_bytes / per));
   b->cap.store(cap, std::memory_order_relaxed);
@@ -186,10 +198,11 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   return RS_OK;
 }
 
-// Runs a closed batch of n slots on its stream and waits for the outputs.
+// Runs a closed batch of n slots on its engine's stream and waits for the outputs.
 int execute(rs_coalescer* co, Batch* b, size_t n) {
   const size_t k = co->k, m = co->m, P = b->P;
-  (void)hipSetDevice(co->device);
+  rs::Engine* eng = rs::ctx_engine(co->ctx, b->engine);
+  rs::DeviceScope ds(rs::engine_device(eng));
   hipStream_t st = b->stream;
   // Zero-copy (default): the staging is pinned host memory the GPU can address, so
   // the kernel reads the staged shards and writes its outputs there directly --
@@ -209,17 +222,17 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
   int rc;
   if (b->kind == Kind::kVerify) {
     // the mismatch words are OR-ed atomically: keep them in HBM, copy them back
-    rc = rs_verify_batch(co->ctx, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
-                         reinterpret_cast<uint32_t*>(dev_at(b, b->o_bad)), RS_MEM_DEVICE, st);
+    rc = rs::engine_verify_batch(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
+                                 reinterpret_cast<uint32_t*>(dev_at(b, b->o_bad)), st);
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(host_at(b, b->o_bad), dev_at(b, b->o_bad), n * 4, hipMemcpyDeviceToHost, st));
   } else {
     if (co->per_stripe) {
-      rc = rs_reconstruct_batch_out(co->ctx, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
-                                    reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, at(b->o_out), m * P,
-                                    st);
+      rc = rs::engine_reconstruct_batch_out(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
+                                            reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, at(b->o_out),
+                                            m * P, st);
     } else {  // encode-only batches (k+m > 16): parity straight into the out region
-      rc = rs_encode_batch(co->ctx, at(b->o_data), k * P, at(b->o_out), m * P, P, b->S, n, RS_MEM_DEVICE, st);
+      rc = rs::engine_encode_batch(eng, at(b->o_data), k * P, at(b->o_out), m * P, P, b->S, n, st);
     }
     if (rc) return rc;
     if (!zc)
@@ -237,13 +250,17 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
 // since the batch opened (default 0).  Callers that arrive while earlier batches
 // are on the device pile into the open batch, so batches grow with the load and a
 // lone caller pays no timer.
+uint64_t hot_word(uint32_t gen, int index) {
+  return (static_cast<uint64_t>(gen) << 16) | static_cast<uint64_t>(index + 1);
+}
+
 // Takes batch b (generation gen) out of the open map / hot slot (under mu).
 void unpublish(rs_coalescer* co, Batch* b, uint32_t gen) {
   const auto key = std::make_pair(static_cast<int>(b->kind), b->S);
   auto it = co->open.find(key);
   if (it != co->open.end() && it->second == b) co->open.erase(it);
   uint64_t h = co->hot.load(std::memory_order_relaxed);
-  const uint64_t mine = (static_cast<uint64_t>(gen) << 8) | static_cast<uint64_t>(b->index + 1);
+  const uint64_t mine = hot_word(gen, b->index);
   if (h == mine) co->hot.compare_exchange_strong(h, 0, std::memory_order_relaxed);
 }
 
@@ -259,8 +276,8 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     size_t slot0 = 0, take = 0;
     // fast path: the most recently opened batch, no mutex
     if (const uint64_t h = co->hot.load(std::memory_order_acquire)) {
-      Batch* hb = co->batches[(h & 0xFF) - 1].get();
-      const uint32_t hg = static_cast<uint32_t>(h >> 8);
+      Batch* hb = co->batches[(h & 0xFFFF) - 1].get();
+      const uint32_t hg = static_cast<uint32_t>(h >> 16);
       if (hb->key_kind.load(std::memory_order_relaxed) == key.first &&
           hb->key_S.load(std::memory_order_relaxed) == key.second && (take = try_reserve(hb, hg, want, &slot0))) {
         b = hb;
@@ -283,8 +300,13 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
           continue;
         }
         if (!co->free_list.empty()) {
-          Batch* nb = co->free_list.back();
-          co->free_list.pop_back();
+          // the free batch of the least-loaded engine (the most recently freed one
+          // among equals: its staging is warm)
+          size_t pick = co->free_list.size() - 1;
+          for (size_t i = co->free_list.size(); i-- > 0;)
+            if (co->engine_load[co->free_list[i]->engine] < co->engine_load[co->free_list[pick]->engine]) pick = i;
+          Batch* nb = co->free_list[pick];
+          co->free_list.erase(co->free_list.begin() + static_cast<std::ptrdiff_t>(pick));
           const int rc = prepare(co, nb, kind, S);
           if (rc) {
             nb->free = true;
@@ -292,12 +314,12 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
             co->free_cv.notify_all();
             return rc;
           }
+          ++co->engine_load[nb->engine];
           take = try_reserve(nb, nb->gen, want, &slot0);  // slot 0: this caller leads
           b = nb;
           gen = nb->gen;
           co->open[key] = nb;
-          co->hot.store((static_cast<uint64_t>(gen) << 8) | static_cast<uint64_t>(nb->index + 1),
-                        std::memory_order_release);
+          co->hot.store(hot_word(gen, nb->index), std::memory_order_release);
           co->free_cv.notify_all();  // waiters for this S may join it
           break;
         }
@@ -320,9 +342,10 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     if (leader) {
       lk.lock();
       // gather: until full, or (an execution slot is free and the linger is over)
+      int& exec = co->engine_exec[b->engine];
       for (;;) {
         if (b->ticket.load(std::memory_order_acquire) & kClosedBit) break;
-        const bool slot_free = co->executing < co->max_exec;
+        const bool slot_free = exec < co->max_exec;
         if (slot_free && Clock::now() >= b->deadline) break;
         if (slot_free)
           co->leader_cv.wait_until(lk, b->deadline);
@@ -332,8 +355,8 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
       const uint64_t t = b->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
       const size_t n = static_cast<size_t>(t & kCountMask);
       unpublish(co, b, gen);
-      while (co->executing >= co->max_exec) co->leader_cv.wait(lk);
-      ++co->executing;
+      while (exec >= co->max_exec) co->leader_cv.wait(lk);
+      ++exec;
       lk.unlock();
       while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
       b->n_final = n;
@@ -344,7 +367,7 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
       while (n > seen && !co->max_seen.compare_exchange_weak(seen, n)) {
       }
       lk.lock();
-      --co->executing;
+      --exec;
       co->leader_cv.notify_all();  // an execution slot is free
       lk.unlock();
       b->rc = rc;
@@ -362,6 +385,7 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     if (b->released.fetch_add(static_cast<uint32_t>(take), std::memory_order_acq_rel) + take == n) {
       lk.lock();
       b->free = true;
+      --co->engine_load[b->engine];
       co->free_list.push_back(b);
       co->free_cv.notify_all();
       lk.unlock();
@@ -472,7 +496,8 @@ extern "C" {
 int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer** out) {
   if (!ctx || !out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
-  rs_coalescer_opts o{4096, 0, 16, size_t(32) << 20, 2, 0};
+  const int ne = rs::ctx_engine_count(ctx);
+  rs_coalescer_opts o{4096, 0, std::max(16, 8 * ne), size_t(32) << 20, 2, 0};
   if (opts) {
     if (opts->max_batch) o.max_batch = opts->max_batch;
     o.max_wait_us = opts->max_wait_us;
@@ -481,22 +506,26 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
     if (opts->max_exec > 0) o.max_exec = opts->max_exec;
     o.staged_dma = opts->staged_dma;
   }
-  if (o.inflight > 64 || o.max_exec > o.inflight) return RS_ERR_INVALID_ARG;
+  if (o.inflight > 256 || o.max_exec > o.inflight || o.inflight < ne) return RS_ERR_INVALID_ARG;
   auto co = std::make_unique<rs_coalescer>();
   co->ctx = ctx;
   co->k = rs_data_shards(ctx);
   co->m = rs_parity_shards(ctx);
-  co->device = rs_device(ctx);
   co->per_stripe = co->k + co->m <= 16;
   co->max_batch = o.max_batch;
   co->max_bytes = o.max_batch_bytes;
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
+  co->engine_load.assign(static_cast<size_t>(ne), 0);
+  co->engine_exec.assign(static_cast<size_t>(ne), 0);
   for (int i = 0; i < o.inflight; ++i) {
     co->batches.push_back(std::make_unique<Batch>());
-    co->batches.back()->index = i;
-    co->free_list.push_back(co->batches.back().get());
+    Batch* b = co->batches.back().get();
+    b->index = i;
+    b->engine = i % ne;
+    b->host.numa = rs::device_numa_node(rs::engine_device(rs::ctx_engine(ctx, b->engine)));
+    co->free_list.push_back(b);
   }
   *out = co.release();
   return RS_OK;

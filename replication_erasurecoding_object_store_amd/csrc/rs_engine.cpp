@@ -4,26 +4,39 @@
 //   * encode matrix and per-erasure-pattern decode plans (the analogue of
 //     klauspost's inversion_tree.go cache, [upstream reedsolomon.go reconstruct]),
 //     built once per pattern and kept resident in HBM;
-//   * for k+m <= 16 every pattern with 1..m erasures is precomputed at rs_create and
+//   * for k+m <= 16 every pattern with 1..m erasures is precomputed at creation and
 //     indexed by a dense missing-mask -> plan LUT, so a batch may carry a different
 //     erasure pattern per stripe with no host work per stripe;
+//   * one context spans one or several GPUs (one Engine each): per-object calls go
+//     to the least-busy engine, host-resident batches split into contiguous stripe
+//     ranges across the engines (independent objects, no
+//     collective), device-resident batches run on the engine of the caller's
+//     stream;
 //   * per-object host calls (the IEcDriver drop-in: ec.go:54-61) run on a pool of
-//     "lanes" (stream + pinned staging + device slab) so concurrent goroutines do
-//     not serialise on one stream;
-//   * host-resident batches are pipelined H2D -> kernel -> D2H over 3 streams.
+//     "lanes" (stream + pinned staging + device slab) per engine so concurrent
+//     goroutines do not serialise on one stream;
+//   * host-resident batches run zero-copy (kernel reads / writes pinned host memory
+//     in place) or pipelined H2D -> kernel -> D2H over 4 streams.
 // No CPU arithmetic path exists: every parity / reconstructed byte comes from a
 // HIP kernel.
+#include "rs_engine.hpp"
+
 #include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -33,12 +46,67 @@
 #include "rs_plan.hpp"
 #include "rs_sha256.hpp"
 
-namespace {
+// ---- pinned host memory ------------------------------------------------------------
+namespace rs {
 
-using rs::Matrix;
+int device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  std::string id(bus);
+  for (char& ch : id) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+  int node = -1;
+  if (!(f >> node)) return -1;
+  return node;
+}
+
+void* pinned_alloc(size_t bytes, int node) {
+  // Place the pages on `node`: the allocating thread's memory policy is set to
+  // prefer that node around the allocation and hipHostMallocNumaUser makes the HIP
+  // runtime follow it; restored afterwards.
+  constexpr unsigned long kMaxNode = 1024;
+  unsigned long saved[kMaxNode / 64] = {0};
+  int saved_mode = 0;
+  bool policy_set = false;
+  unsigned flags = hipHostMallocPortable;  // one staging slab may serve any GPU
+  if (node >= 0 && node < static_cast<int>(kMaxNode) &&
+      syscall(SYS_get_mempolicy, &saved_mode, saved, kMaxNode, nullptr, 0) == 0) {
+    unsigned long want[kMaxNode / 64] = {0};
+    want[node / 64] = 1ul << (node % 64);
+    if (syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, want, kMaxNode) == 0) {
+      policy_set = true;
+      flags |= hipHostMallocNumaUser;
+    }
+  }
+  void* p = nullptr;
+  hipError_t err = hipHostMalloc(&p, bytes, flags);
+  if (err != hipSuccess && policy_set) {  // runtime without NUMA-user support: plain pinned
+    (void)hipGetLastError();
+    err = hipHostMalloc(&p, bytes, hipHostMallocPortable);
+  }
+  if (policy_set) syscall(SYS_set_mempolicy, saved_mode, saved_mode ? saved : nullptr, kMaxNode);
+  if (err != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void pinned_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
+}  // namespace rs
+
+namespace {
 
 using rs::check_shards;
 using rs::DevBuf;
+using rs::DeviceScope;
+using rs::Matrix;
 using rs::PinnedBuf;
 using rs::round_up;
 
@@ -46,7 +114,6 @@ using rs::round_up;
 // tools/ab_bench.py on MI355X (profiles/r01_ab_occupancy.log): the streaming
 // pattern wants few waves (tools/hbm_probe2.hip: 1-2 WG/CU beat higher occupancy)
 // until the per-byte VALU work (K*E lookups) needs more waves to hide latency.
-constexpr int kDefaultBlocksPerCu = 0;  // 0 = pick by shape
 int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
 
 // ---- plan construction -----------------------------------------------------
@@ -121,6 +188,8 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
   return RS_OK;
 }
 
+uint64_t full_mask64(int t) { return (t >= 64) ? ~0ull : ((1ull << t) - 1); }
+
 // ---- buffers -------------------------------------------------------------------
 // A lane serves one synchronous host call at a time.
 struct Lane {
@@ -129,12 +198,16 @@ struct Lane {
   PinnedBuf host;
 };
 
-// Upload slot for per-stripe masks passed in host memory (async device calls).
+// Staging for per-stripe masks passed in host memory to an asynchronous device
+// call.  A slot is reused only after the kernel that READ it has finished: `done`
+// is recorded on the launch stream after that kernel (upload_release), and `busy`
+// keeps a second caller off the slot between its upload and its launch.
 struct UploadSlot {
   PinnedBuf host;
   DevBuf dev;
   hipEvent_t done = nullptr;
   bool used = false;
+  bool busy = false;
 };
 
 // Split shard layout shared by host and device buffers (see rs_plan.hpp).
@@ -149,44 +222,53 @@ struct Layout {
                  : parity + stripe * parity_sp + static_cast<size_t>(s - k) * pitch;
   }
   size_t stripe_pitch(int k, int s) const { return s < k ? data_sp : parity_sp; }
+  // the same layout starting at stripe s0
+  Layout from(size_t s0) const {
+    return Layout{data + s0 * data_sp, data_sp, parity ? parity + s0 * parity_sp : nullptr, parity_sp, pitch};
+  }
+};
+
+// Host batch pipeline: chunks of stripes flow H2D -> kernel -> D2H on kHostStreams
+// streams; each stream has its own device slab (split layout), so chunk j+1's
+// copies overlap chunk j's kernel and D2H.  Kept in the engine: creating streams
+// and slabs per call cost more than a small call's transfers.
+constexpr int kHostStreams = 4;
+constexpr size_t kHostChunkBytes = size_t(16) << 20;  // device bytes per chunk
+constexpr size_t kUploadSlots = 8;
+constexpr uint32_t kStatusWords = 1024;  // per-stream deferred-error words per engine
+
+// Context-wide "what ran last" (measurement helpers).
+struct Shared {
+  std::atomic<const char*> last_kernel{"none"};
+  std::atomic<const char*> last_host_path{"none"};
 };
 
 }  // namespace
 
-// ---- host batch pipeline state ---------------------------------------------------
-// Chunks of stripes flow H2D -> kernel -> D2H on kHostStreams streams; each stream
-// has its own device slab (split layout), so chunk j+1's copies overlap chunk j's
-// kernel and D2H.  Kept in the context: creating streams and slabs per call cost
-// more than a small call's transfers.
-constexpr int kHostStreams = 4;
-constexpr size_t kHostChunkBytes = size_t(16) << 20;  // device bytes per chunk
+// ---- one GPU ----------------------------------------------------------------------
+namespace rs {
 
-struct HostPipe {
-  hipStream_t st[kHostStreams] = {};
-  DevBuf buf[kHostStreams];
-  ~HostPipe() {
-    for (auto& s : st)
-      if (s) (void)hipStreamDestroy(s);
-  }
-};
+struct Engine {
+  int k = 0, m = 0, device = 0, cu_count = 0, numa = -1;
+  const Matrix* enc = nullptr;            // the context's
+  const std::vector<uint32_t>* h_lut = nullptr;
+  Shared* shared = nullptr;
+  int blocks_per_cu = 0;                  // 0 = by shape
+  bool bitsliced = false;                 // generated encode XOR program matches enc
+  bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
+  std::string name;
 
-struct rs_ctx {
-  int k = 0, m = 0, device = 0, cu_count = 0;
-  int blocks_per_cu = kDefaultBlocksPerCu;
-  bool force_generic = false;
-  bool bitsliced = false;  // generated encode XOR program matches enc (rs_create)
-  std::string backend;
-  Matrix enc;
-
-  DevBuf d_enc_plan;              // encode plan (uniform)
-  DevBuf d_plans, d_lut;          // eager all-pattern plans + LUT (k+m <= 16)
-  uint32_t n_plans = 0;
-  std::vector<uint32_t> h_lut;    // missing mask -> plan index
+  DevBuf d_enc_plan;                      // encode plan (uniform)
+  DevBuf d_plans, d_lut;                  // eager all-pattern plans + LUT (k+m <= 16)
   bool have_lut = false;
-  std::mutex plan_mu;             // uniform plans built on demand (k+m > 16 / data-only)
+  std::mutex plan_mu;                     // uniform plans built on demand (k+m > 16 / data-only)
   std::unordered_map<uint64_t, std::unique_ptr<DevBuf>> plan_cache;
 
-  DevBuf d_status, d_scratch;     // device status word (per-stripe calls); store sink
+  // Deferred per-stripe errors (device-resident masks): one word per stream, so
+  // rs_sync(stream) reports and clears exactly the errors of kernels on that stream.
+  std::mutex status_mu;
+  std::unordered_map<hipStream_t, uint32_t> status_idx;
+  DevBuf d_status;
   PinnedBuf h_status;
 
   std::mutex lane_mu;
@@ -196,29 +278,152 @@ struct rs_ctx {
   int max_lanes = 8;
 
   std::mutex upload_mu;
-  static constexpr size_t kUploadSlots = 4;
+  std::condition_variable upload_cv;
   UploadSlot uploads[kUploadSlots];
   size_t upload_next = 0;
 
-  std::mutex host_mu;             // host-resident batches: one at a time per context
-  HostPipe host_pipe;
-  bool host_zero_copy = true;     // pinned host batches: kernel reads/writes them in place
-  DevBuf d_bad;                   // zero-copy verify: per-stripe result before D2H
-  std::atomic<const char*> last_host_path{"none"};
+  std::mutex host_mu;                     // host-resident batches: one at a time per engine
+  hipStream_t pipe_st[kHostStreams] = {};
+  DevBuf pipe_buf[kHostStreams];
+  DevBuf d_bad;                           // zero-copy verify: per-stripe result before D2H
 
-  std::atomic<const char*> last_kernel{"none"};
+  std::atomic<int> inflight{0};           // calls running on this engine (dispatch)
 
-  ~rs_ctx() {
+  ~Engine() {  // runs under the rs_ctx destructor's DeviceScope
+    (void)hipDeviceSynchronize();
     for (auto& s : uploads)
       if (s.done) (void)hipEventDestroy(s.done);
     for (auto& l : lanes)
       if (l->stream) (void)hipStreamDestroy(l->stream);
+    for (auto& s : pipe_st)
+      if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+}  // namespace rs
+
+using rs::Engine;
+
+struct rs_ctx {
+  int k = 0, m = 0;
+  Matrix enc;
+  std::vector<uint32_t> h_lut;            // missing mask -> plan index (k+m <= 16)
+  std::vector<std::unique_ptr<Engine>> engines;
+  Shared shared;
+  std::string backend;
+  std::atomic<uint32_t> rr{0};
+  ~rs_ctx() {
+    for (auto& e : engines) {  // each engine's buffers and streams freed on its device
+      DeviceScope ds(e->device);
+      e.reset();
+    }
   }
 };
 
 namespace {
 
-rs::KernelArgs make_args(rs_ctx* c, const Layout& L, size_t S, size_t N) {
+struct InflightGuard {
+  Engine* e;
+  explicit InflightGuard(Engine* en) : e(en) { e->inflight.fetch_add(1, std::memory_order_relaxed); }
+  ~InflightGuard() { e->inflight.fetch_sub(1, std::memory_order_relaxed); }
+};
+
+// Least-busy engine for a per-object call (round-robin among equals).
+Engine* pick_engine(rs_ctx* c) {
+  const size_t n = c->engines.size();
+  if (n == 1) return c->engines[0].get();
+  const uint32_t start = c->rr.fetch_add(1, std::memory_order_relaxed);
+  Engine* best = nullptr;
+  int best_load = 0;
+  for (size_t i = 0; i < n; ++i) {
+    Engine* e = c->engines[(start + i) % n].get();
+    const int load = e->inflight.load(std::memory_order_relaxed);
+    if (!best || load < best_load) {
+      best = e;
+      best_load = load;
+    }
+  }
+  return best;
+}
+
+// Engine of a device-resident call: the device the caller's stream belongs to
+// (the current device for the null stream).  Always the FIRST engine on that
+// device, so the stream's deferred errors are found by rs_sync.  nullptr if the
+// context does not span that device.
+Engine* engine_for_stream(rs_ctx* c, hipStream_t s) {
+  if (c->engines.size() == 1) return c->engines[0].get();
+  int dev = -1;
+  if (s) {
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+  } else if (hipGetDevice(&dev) != hipSuccess) {
+    return nullptr;
+  }
+  for (auto& e : c->engines)
+    if (e->device == dev) return e.get();
+  return nullptr;
+}
+
+// Runs fn(engine, first_stripe, n_stripes) over contiguous near-equal stripe
+// ranges, one per engine, in parallel (one host thread per engine).
+// Small batches stay on one engine: a share below ~8 MiB of user data is not worth
+// a thread and a second device's launch.
+template <class Fn>
+int fan_out(rs_ctx* c, size_t N, size_t user_bytes_per_stripe, Fn&& fn) {
+  const size_t ne = c->engines.size();
+  size_t use = 1;
+  if (ne > 1) {
+    const size_t want = N * user_bytes_per_stripe / (size_t(8) << 20);
+    use = std::max<size_t>(1, std::min({ne, want, N}));
+  }
+  if (use == 1) {
+    Engine* e = pick_engine(c);
+    InflightGuard ig(e);
+    DeviceScope ds(e->device);
+    if (!ds.ok()) return RS_ERR_DEVICE;
+    return fn(e, size_t(0), N);
+  }
+  const uint32_t start = c->rr.fetch_add(1, std::memory_order_relaxed);
+  std::vector<int> rcs(use, RS_OK);
+  auto run = [&](size_t j) {
+    Engine* e = c->engines[(start + j) % ne].get();
+    InflightGuard ig(e);
+    DeviceScope ds(e->device);
+    if (!ds.ok()) {
+      rcs[j] = RS_ERR_DEVICE;
+      return;
+    }
+    const size_t base = N / use, extra = N % use;
+    const size_t s0 = j * base + std::min(j, extra);
+    rcs[j] = fn(e, s0, base + (j < extra ? 1 : 0));
+  };
+  std::vector<std::thread> th;
+  th.reserve(use - 1);
+  for (size_t j = 1; j < use; ++j) th.emplace_back(run, j);
+  run(0);
+  for (auto& t : th) t.join();
+  for (int rc : rcs)
+    if (rc) return rc;
+  return RS_OK;
+}
+
+uint32_t* status_word(Engine* e, hipStream_t s) {
+  std::lock_guard<std::mutex> g(e->status_mu);
+  auto it = e->status_idx.find(s);
+  uint32_t idx;
+  if (it != e->status_idx.end()) {
+    idx = it->second;
+  } else {
+    // the last word is shared by streams beyond the first kStatusWords-1
+    idx = static_cast<uint32_t>(std::min<size_t>(e->status_idx.size(), kStatusWords - 1));
+    e->status_idx.emplace(s, idx);
+  }
+  return static_cast<uint32_t*>(e->d_status.p) + idx;
+}
+
+rs::KernelArgs make_args(Engine* e, const Layout& L, size_t S, size_t N) {
   rs::KernelArgs a{};
   a.data = L.data;
   a.parity = L.parity;
@@ -229,113 +434,109 @@ rs::KernelArgs make_args(rs_ctx* c, const Layout& L, size_t S, size_t N) {
   a.n_stripes = static_cast<uint32_t>(N);
   a.blocks_per_stripe = static_cast<uint32_t>((round_up(S, 16) / 16 + 63) / 64);
   a.full_cols = static_cast<uint32_t>(S / 16);
-  a.blocks_full = (a.full_cols + 63u) / 64u;
-  a.k = c->k;
-  a.m = c->m;
-  a.full_mask = (c->k + c->m >= 32) ? 0xFFFFFFFFu : ((1u << (c->k + c->m)) - 1u);
-  a.plan_bytes = rs::plan_stride(c->k, c->m);
-  a.scratch = static_cast<uint8_t*>(c->d_scratch.p);
-  a.status = static_cast<uint32_t*>(c->d_status.p);
-  a.lut = static_cast<const uint32_t*>(c->d_lut.p);
+  a.k = e->k;
+  a.m = e->m;
+  a.full_mask = (e->k + e->m >= 32) ? 0xFFFFFFFFu : ((1u << (e->k + e->m)) - 1u);
+  a.plan_bytes = rs::plan_stride(e->k, e->m);
+  a.lut = static_cast<const uint32_t*>(e->d_lut.p);
   return a;
 }
 
-// e = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
+// e_out = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
 // #missing for per-stripe patterns).
-int launch(rs_ctx* c, const rs::KernelArgs& args, int e, bool per_stripe, hipStream_t s) {
-  if (args.n_stripes == 0 || args.shard_len == 0 || e <= 0) return RS_OK;
+int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s) {
+  if (args.n_stripes == 0 || args.shard_len == 0 || e_out <= 0) return RS_OK;
   rs::KernelArgs a = args;
   // the encode plan with a verified generated XOR program -> bitsliced kernel
-  a.encode_net = (c->bitsliced && !per_stripe && a.plans == c->d_enc_plan.p) ? 1u : 0u;
-  const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, e);
-  const char* name = rs::launch_apply(a, e, per_stripe, static_cast<uint32_t>(bpc),
-                                      static_cast<uint32_t>(c->cu_count), s, c->force_generic);
+  a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
+  a.status = per_stripe ? status_word(e, s) : nullptr;
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
+  const char* name =
+      rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s, false);
   if (!name) return RS_ERR_DEVICE;
-  c->last_kernel.store(name);
+  e->shared->last_kernel.store(name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
 
-int launch_verify_args(rs_ctx* c, rs::KernelArgs& a, hipStream_t s) {
-  a.plans = static_cast<const uint8_t*>(c->d_enc_plan.p);
-  const int bpc = c->blocks_per_cu > 0 ? c->blocks_per_cu : default_blocks_per_cu(c->k, c->m);
-  const char* name = rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(c->cu_count), s,
-                                       c->force_generic);
+int launch_verify_args(Engine* e, rs::KernelArgs& a, hipStream_t s) {
+  a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e->m);
+  const char* name =
+      rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s, false);
   if (!name) return RS_ERR_DEVICE;
-  c->last_kernel.store(name);
+  e->shared->last_kernel.store(name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
 
-uint64_t full_mask64(int t) { return (t >= 64) ? ~0ull : ((1ull << t) - 1); }
-
-// Device pointer of the plan for one erasure pattern (cached).
-int uniform_plan(rs_ctx* c, uint64_t present, bool data_only, const uint8_t** plan_dev) {
-  const int t = c->k + c->m;
+// Device pointer of the plan for one erasure pattern (cached).  Caller holds a
+// DeviceScope for the engine.
+int uniform_plan(Engine* e, uint64_t present, bool data_only, const uint8_t** plan_dev) {
+  const int t = e->k + e->m;
   present &= full_mask64(t);
-  if (__builtin_popcountll(present) < c->k) return RS_ERR_TOO_FEW_SHARDS;
-  if (c->have_lut && !data_only) {
+  if (__builtin_popcountll(present) < e->k) return RS_ERR_TOO_FEW_SHARDS;
+  if (e->have_lut && !data_only) {
     const uint32_t missing = static_cast<uint32_t>(~present & full_mask64(t));
-    const uint32_t pid = c->h_lut[missing];
+    const uint32_t pid = (*e->h_lut)[missing];
     if (pid == rs::kPlanInvalid) return RS_ERR_TOO_FEW_SHARDS;
-    *plan_dev = static_cast<const uint8_t*>(c->d_plans.p) + static_cast<size_t>(pid) * rs::plan_stride(c->k, c->m);
+    *plan_dev = static_cast<const uint8_t*>(e->d_plans.p) + static_cast<size_t>(pid) * rs::plan_stride(e->k, e->m);
     return RS_OK;
   }
   const uint64_t key = present | (data_only ? (1ull << 63) : 0ull);
-  std::lock_guard<std::mutex> g(c->plan_mu);
-  auto it = c->plan_cache.find(key);
-  if (it == c->plan_cache.end()) {
+  std::lock_guard<std::mutex> g(e->plan_mu);
+  auto it = e->plan_cache.find(key);
+  if (it == e->plan_cache.end()) {
     std::vector<uint8_t> plan;
-    int rc = make_decode_plan(c->k, c->m, c->enc, present, data_only, &plan);
+    int rc = make_decode_plan(e->k, e->m, *e->enc, present, data_only, &plan);
     if (rc) return rc;
     auto buf = std::make_unique<DevBuf>();
     if (buf->ensure(plan.size())) return RS_ERR_DEVICE;
     RS_HIP(hipMemcpy(buf->p, plan.data(), plan.size(), hipMemcpyHostToDevice));
-    it = c->plan_cache.emplace(key, std::move(buf)).first;
+    it = e->plan_cache.emplace(key, std::move(buf)).first;
   }
   *plan_dev = static_cast<const uint8_t*>(it->second->p);
   return RS_OK;
 }
 
-// RAII lane checkout.
+// RAII lane checkout (caller holds a DeviceScope for the engine).
 struct LaneGuard {
-  rs_ctx* c;
+  Engine* e;
   Lane* lane = nullptr;
   int rc = RS_OK;
-  explicit LaneGuard(rs_ctx* ctx) : c(ctx) {
-    std::unique_lock<std::mutex> g(c->lane_mu);
-    if (c->free_lanes.empty() && static_cast<int>(c->lanes.size()) < c->max_lanes) {
+  explicit LaneGuard(Engine* en) : e(en) {
+    std::unique_lock<std::mutex> g(e->lane_mu);
+    if (e->free_lanes.empty() && static_cast<int>(e->lanes.size()) < e->max_lanes) {
       auto l = std::make_unique<Lane>();
-      if (hipSetDevice(c->device) != hipSuccess ||
-          hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) {
+      l->host.numa = e->numa;
+      if (hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking) != hipSuccess) {
         rc = RS_ERR_DEVICE;
         return;
       }
-      c->free_lanes.push_back(l.get());
-      c->lanes.push_back(std::move(l));
+      e->free_lanes.push_back(l.get());
+      e->lanes.push_back(std::move(l));
     }
-    c->lane_cv.wait(g, [&] { return !c->free_lanes.empty(); });
-    lane = c->free_lanes.back();
-    c->free_lanes.pop_back();
+    e->lane_cv.wait(g, [&] { return !e->free_lanes.empty(); });
+    lane = e->free_lanes.back();
+    e->free_lanes.pop_back();
   }
   ~LaneGuard() {
     if (!lane) return;
-    std::lock_guard<std::mutex> g(c->lane_mu);
-    c->free_lanes.push_back(lane);
-    c->lane_cv.notify_one();
+    std::lock_guard<std::mutex> g(e->lane_mu);
+    e->free_lanes.push_back(lane);
+    e->lane_cv.notify_one();
   }
 };
 
-// [upstream reedsolomon.go checkShards(shards, nilok)] + shardSize.
 // One object through a lane: pack inputs into pinned staging, H2D, one kernel,
 // D2H of the outputs, unpack.  in/out slots are shard indices into `shards`.
-int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
+int run_object(Engine* e, const uint8_t* plan_dev, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
                uint8_t* const* shards, size_t S) {
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
-  LaneGuard lg(c);
+  LaneGuard lg(e);
   if (lg.rc) return lg.rc;
   Lane* L = lg.lane;
-  const int t = c->k + c->m;
+  const int t = e->k + e->m;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t bytes = P * static_cast<size_t>(t);
   if (L->dev.ensure(bytes) || L->host.ensure(bytes)) return RS_ERR_DEVICE;
@@ -345,10 +546,10 @@ int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_id
   const int lo = *std::min_element(in_idx.begin(), in_idx.end());
   const int hi = *std::max_element(in_idx.begin(), in_idx.end());
   RS_HIP(hipMemcpyAsync(d + lo * P, h + lo * P, (hi - lo + 1) * P, hipMemcpyHostToDevice, L->stream));
-  const Layout dl{d, bytes, d + static_cast<size_t>(c->k) * P, bytes, P};
-  rs::KernelArgs a = make_args(c, dl, S, 1);
+  const Layout dl{d, bytes, d + static_cast<size_t>(e->k) * P, bytes, P};
+  rs::KernelArgs a = make_args(e, dl, S, 1);
   a.plans = plan_dev;
-  int rc = launch(c, a, static_cast<int>(out_idx.size()), false, L->stream);
+  int rc = launch(e, a, static_cast<int>(out_idx.size()), false, L->stream);
   if (rc) return rc;
   for (int s : out_idx)
     RS_HIP(hipMemcpyAsync(h + static_cast<size_t>(s) * P, d + static_cast<size_t>(s) * P, S, hipMemcpyDeviceToHost,
@@ -360,7 +561,7 @@ int run_object(rs_ctx* c, const uint8_t* plan_dev, const std::vector<int>& in_id
 
 int reconstruct_impl(rs_ctx* c, uint8_t* const* shards, size_t* lens, bool data_only) {
   if (!c || !shards || !lens) return RS_ERR_INVALID_ARG;
-  const int t = c->k + c->m;
+  const int k = c->k, t = c->k + c->m;
   size_t S = 0;
   int rc = check_shards(t, lens, true, &S);
   if (rc) return rc;
@@ -370,23 +571,27 @@ int reconstruct_impl(rs_ctx* c, uint8_t* const* shards, size_t* lens, bool data_
     if (lens[i]) {
       present |= 1ull << i;
       ++np;
-      if (i < c->k) ++data_present;
+      if (i < k) ++data_present;
     }
-  if (np == t || (data_only && data_present == c->k)) return RS_OK;
-  if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
+  if (np == t || (data_only && data_present == k)) return RS_OK;
+  if (np < k) return RS_ERR_TOO_FEW_SHARDS;
   std::vector<int> surv, miss;
   for (int i = 0; i < t; ++i) {
     if (lens[i]) {
-      if (static_cast<int>(surv.size()) < c->k) surv.push_back(i);
-    } else if (!data_only || i < c->k) {
+      if (static_cast<int>(surv.size()) < k) surv.push_back(i);
+    } else if (!data_only || i < k) {
       if (!shards[i]) return RS_ERR_INVALID_ARG;
       miss.push_back(i);
     }
   }
+  Engine* e = pick_engine(c);
+  InflightGuard ig(e);
+  DeviceScope ds(e->device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
   const uint8_t* plan = nullptr;
-  rc = uniform_plan(c, present, data_only, &plan);
+  rc = uniform_plan(e, present, data_only, &plan);
   if (rc) return rc;
-  rc = run_object(c, plan, surv, miss, shards, S);
+  rc = run_object(e, plan, surv, miss, shards, S);
   if (rc) return rc;
   for (int s : miss) lens[s] = S;
   return RS_OK;
@@ -413,8 +618,8 @@ bool out_layout_ok(size_t out_sp, size_t pitch, size_t S, size_t N, int e) {
 
 bool batch_sizes_ok(size_t S, size_t N, size_t pitch) {
   if (S > 0xFFFFFFF0u || N > 0xFFFFFFFFu || pitch < S) return false;
-  const uint64_t cols = round_up(S, 16) / 16;
-  return N * ((cols + 63) / 64) < 0xFFFFFFFFull;  // task ids fit 32 bits
+  const uint64_t cols = round_up(std::min<size_t>(S, rs::kColumnWindow), 16) / 16;
+  return N * ((cols + 63) / 64) < 0xFFFFFFFFull;  // task ids of one launch fit 32 bits
 }
 
 hipError_t copy2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
@@ -442,7 +647,56 @@ int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<in
   return RS_OK;
 }
 
-int upload_masks(rs_ctx* c, const uint32_t* masks, size_t n, hipStream_t s, const uint32_t** dev);
+// ---- per-stripe mask uploads ----------------------------------------------------
+// upload_acquire copies n host masks into a free slot and enqueues their H2D on s;
+// the caller launches the kernel that reads them, then the guard's release records
+// the slot's event on s AFTER that kernel -- the slot (pinned and device buffer)
+// cannot be rewritten or reallocated while any kernel still reads it.
+struct UploadGuard {
+  Engine* e = nullptr;
+  UploadSlot* u = nullptr;
+  hipStream_t s = nullptr;
+  ~UploadGuard() {
+    if (!u) return;
+    const bool rec = hipEventRecord(u->done, s) == hipSuccess;
+    std::lock_guard<std::mutex> g(e->upload_mu);
+    u->used = rec;
+    if (!rec) (void)hipStreamSynchronize(s);  // no event: make the slot safe the slow way
+    u->busy = false;
+    e->upload_cv.notify_one();
+  }
+};
+
+int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
+                   const uint32_t** dev) {
+  UploadSlot* u = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(e->upload_mu);
+    for (;;) {
+      for (size_t i = 0; i < kUploadSlots && !u; ++i) {
+        UploadSlot& c = e->uploads[(e->upload_next + i) % kUploadSlots];
+        if (!c.busy) {
+          u = &c;
+          e->upload_next = (e->upload_next + i + 1) % kUploadSlots;
+        }
+      }
+      if (u) break;
+      e->upload_cv.wait(lk);
+    }
+    u->busy = true;
+  }
+  g->e = e;
+  g->u = u;
+  g->s = s;
+  if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
+  if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
+  u->host.numa = e->numa;
+  if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
+  std::memcpy(u->host.p, masks, n * 4);
+  RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
+  *dev = static_cast<const uint32_t*>(u->dev.p);
+  return RS_OK;
+}
 
 // GPU address of a pinned host range [p, p+bytes) (hipHostMalloc'ed or
 // rs_host_register'ed), or nullptr if any part of it is pageable.
@@ -463,14 +717,19 @@ uint8_t* mapped(const void* p, size_t bytes) {
   return d;
 }
 
+int ensure_pipe_stream(Engine* e, int i) {
+  if (!e->pipe_st[i]) RS_HIP(hipStreamCreateWithFlags(&e->pipe_st[i], hipStreamNonBlocking));
+  return RS_OK;
+}
+
 // Zero-copy host batch: with the shards in pinned host memory the kernel itself
 // reads the K survivors and writes only the missing shards across PCIe, in place
 // -- per stripe exactly the bytes the codec needs, no staging slab, no DMA of
 // slots it does not touch (the staged pipeline must move every slot a stripe
 // might use).  Returns RS_ERR_NOT_SUPPORTED when the layout does not qualify.
-int host_zero_copy(rs_ctx* c, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
-                   const uint32_t* masks_host, int e, uint32_t* bad_host) {
-  const int k = c->k, m = c->m;
+int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
+                   const uint32_t* masks_host, int e_out, uint32_t* bad_host) {
+  const int k = e->k, m = e->m;
   const size_t dbytes = (N - 1) * hl.data_sp + static_cast<size_t>(k - 1) * hl.pitch + S;
   const size_t pbytes = m ? (N - 1) * hl.parity_sp + static_cast<size_t>(m - 1) * hl.pitch + S : 0;
   uint8_t* dd = mapped(hl.data, dbytes);
@@ -478,101 +737,260 @@ int host_zero_copy(rs_ctx* c, const Layout& hl, size_t S, size_t N, const uint8_
   if (!dd || (m && !pd)) return RS_ERR_NOT_SUPPORTED;
   const Layout dl{dd, hl.data_sp, pd, hl.parity_sp, hl.pitch};
   if (!device_layout_ok(dl, m, S)) return RS_ERR_NOT_SUPPORTED;
-  std::lock_guard<std::mutex> g(c->host_mu);
-  HostPipe& pipe = c->host_pipe;
-  if (!pipe.st[0]) RS_HIP(hipStreamCreateWithFlags(&pipe.st[0], hipStreamNonBlocking));
-  hipStream_t st = pipe.st[0];
-  rs::KernelArgs a = make_args(c, dl, S, N);
+  std::lock_guard<std::mutex> g(e->host_mu);
+  int rc = ensure_pipe_stream(e, 0);
+  if (rc) return rc;
+  hipStream_t st = e->pipe_st[0];
+  rs::KernelArgs a = make_args(e, dl, S, N);
   a.plans = plan_dev;
-  int rc;
   if (bad_host) {
-    if (c->d_bad.ensure(N * 4)) return RS_ERR_DEVICE;
-    a.bad = static_cast<uint32_t*>(c->d_bad.p);
-    rc = launch_verify_args(c, a, st);
+    if (e->d_bad.ensure(N * 4)) return RS_ERR_DEVICE;
+    a.bad = static_cast<uint32_t*>(e->d_bad.p);
+    rc = launch_verify_args(e, a, st);
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(bad_host, a.bad, N * 4, hipMemcpyDeviceToHost, st));
   } else {
+    UploadGuard ug;
     if (masks_host) {
       const uint32_t* dm = nullptr;
-      rc = upload_masks(c, masks_host, N, st, &dm);
+      rc = upload_acquire(e, masks_host, N, st, &ug, &dm);
       if (rc) return rc;
       a.present_masks = dm;
     }
-    rc = launch(c, a, e, masks_host != nullptr, st);
+    rc = launch(e, a, e_out, masks_host != nullptr, st);
     if (rc) return rc;
   }
   RS_HIP(hipStreamSynchronize(st));
-  c->last_host_path.store("zero-copy");
+  e->shared->last_host_path.store("zero-copy");
   return RS_OK;
 }
 
-int host_batch(rs_ctx* c, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
-               size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e,
+// One engine's share of a host-resident batch (caller holds its DeviceScope).
+int host_batch(Engine* e, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
+               size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e_out,
                uint32_t* bad_host = nullptr) {
-  if (c->host_zero_copy) {
-    const int rc = host_zero_copy(c, hl, S, N, plan_dev, masks_host, e, bad_host);
+  if (N == 0) return RS_OK;
+  if (e->host_zero_copy) {
+    const int rc = host_zero_copy(e, hl, S, N, plan_dev, masks_host, e_out, bad_host);
     if (rc != RS_ERR_NOT_SUPPORTED) return rc;
   }
-  c->last_host_path.store("staged");
-  const int k = c->k, m = c->m;
+  e->shared->last_host_path.store("staged");
+  const int k = e->k, m = e->m;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t per_stripe = P * static_cast<size_t>(k + m) + ((masks_host || bad_host) ? 4 : 0);
   const size_t chunk = std::min(N, std::max<size_t>(1, kHostChunkBytes / per_stripe));
-  std::lock_guard<std::mutex> g(c->host_mu);
-  HostPipe& pipe = c->host_pipe;
+  std::lock_guard<std::mutex> g(e->host_mu);
   for (int i = 0; i < kHostStreams; ++i) {
-    if (!pipe.st[i]) RS_HIP(hipStreamCreateWithFlags(&pipe.st[i], hipStreamNonBlocking));
+    int rc = ensure_pipe_stream(e, i);
+    if (rc) return rc;
     // sized for a full chunk whatever N is, so a small call never leaves slabs that
     // a later large call has to reallocate
-    if (pipe.buf[i].ensure(std::max(kHostChunkBytes, per_stripe) + per_stripe + 256)) return RS_ERR_DEVICE;
+    if (e->pipe_buf[i].ensure(std::max(kHostChunkBytes, per_stripe) + per_stripe + 256)) return RS_ERR_DEVICE;
   }
   int j = 0;
   for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
     const size_t n = std::min(chunk, N - s0);
-    hipStream_t st = pipe.st[j % kHostStreams];
-    uint8_t* d = static_cast<uint8_t*>(pipe.buf[j % kHostStreams].p);
+    hipStream_t st = e->pipe_st[j % kHostStreams];
+    uint8_t* d = static_cast<uint8_t*>(e->pipe_buf[j % kHostStreams].p);
     const Layout dl{d, P * k, d + chunk * P * k, P * m, P};
     int rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
     if (rc) return rc;
-    rs::KernelArgs a = make_args(c, dl, S, n);
+    rs::KernelArgs a = make_args(e, dl, S, n);
     a.plans = plan_dev;
+    // masks / mismatch words live in the slab itself: stream-ordered with the chunk
+    uint32_t* aux = reinterpret_cast<uint32_t*>(d + round_up(chunk * P * (k + m), 256));
     if (masks_host) {
-      uint32_t* dm = reinterpret_cast<uint32_t*>(d + round_up(chunk * P * (k + m), 256));
-      RS_HIP(hipMemcpyAsync(dm, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
-      a.present_masks = dm;
+      RS_HIP(hipMemcpyAsync(aux, masks_host + s0, n * 4, hipMemcpyHostToDevice, st));
+      a.present_masks = aux;
     }
     if (bad_host) {
-      uint32_t* db = reinterpret_cast<uint32_t*>(d + round_up(chunk * P * (k + m), 256));
-      a.bad = db;
-      rc = launch_verify_args(c, a, st);
+      a.bad = aux;
+      rc = launch_verify_args(e, a, st);
       if (rc) return rc;
-      RS_HIP(hipMemcpyAsync(bad_host + s0, db, n * 4, hipMemcpyDeviceToHost, st));
+      RS_HIP(hipMemcpyAsync(bad_host + s0, aux, n * 4, hipMemcpyDeviceToHost, st));
       continue;
     }
-    rc = launch(c, a, e, masks_host != nullptr, st);
+    rc = launch(e, a, e_out, masks_host != nullptr, st);
     if (rc) return rc;
     rc = copy_slots(hl, dl, k, out_slots, s0, 0, n, S, hipMemcpyDeviceToHost, st);
     if (rc) return rc;
   }
-  for (int i = 0; i < kHostStreams; ++i) RS_HIP(hipStreamSynchronize(pipe.st[i]));
+  for (int i = 0; i < kHostStreams; ++i) RS_HIP(hipStreamSynchronize(e->pipe_st[i]));
   return RS_OK;
 }
 
-int upload_masks(rs_ctx* c, const uint32_t* masks, size_t n, hipStream_t s, const uint32_t** dev) {
-  std::lock_guard<std::mutex> g(c->upload_mu);
-  UploadSlot& u = c->uploads[c->upload_next++ % rs_ctx::kUploadSlots];
-  if (!u.done) RS_HIP(hipEventCreateWithFlags(&u.done, hipEventDisableTiming));
-  if (u.used) RS_HIP(hipEventSynchronize(u.done));
-  if (u.host.ensure(n * 4) || u.dev.ensure(n * 4)) return RS_ERR_DEVICE;
-  std::memcpy(u.host.p, masks, n * 4);
-  RS_HIP(hipMemcpyAsync(u.dev.p, u.host.p, n * 4, hipMemcpyHostToDevice, s));
-  RS_HIP(hipEventRecord(u.done, s));
-  u.used = true;
-  *dev = static_cast<const uint32_t*>(u.dev.p);
+// ---- engine creation ----------------------------------------------------------------
+struct PlanSet {
+  std::vector<uint8_t> enc_plan, all_plans;
+  bool have_lut = false;
+};
+
+int create_engine(rs_ctx* c, int device, const PlanSet& ps, std::unique_ptr<Engine>* out) {
+  DeviceScope ds(device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RS_ERR_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RS_ERR_NO_DEVICE;
+  auto e = std::make_unique<Engine>();
+  e->k = c->k;
+  e->m = c->m;
+  e->device = device;
+  e->cu_count = prop.multiProcessorCount;
+  e->numa = rs::device_numa_node(device);
+  e->enc = &c->enc;
+  e->h_lut = &c->h_lut;
+  e->shared = &c->shared;
+  if (const uint8_t* rows = rs::bitsliced_encode_rows(c->k, c->m)) {
+    bool same = true;
+    for (int r = 0; r < c->m; ++r)
+      for (int q = 0; q < c->k; ++q) same = same && rows[r * c->k + q] == c->enc.at(c->k + r, q);
+    e->bitsliced = same;
+  }
+  char name[200];
+  std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU:dev%d:numa%d", prop.gcnArchName, prop.name, e->cu_count, device,
+                e->numa);
+  e->name = name;
+  if (e->d_enc_plan.ensure(ps.enc_plan.size()) ||
+      hipMemcpy(e->d_enc_plan.p, ps.enc_plan.data(), ps.enc_plan.size(), hipMemcpyHostToDevice) != hipSuccess)
+    return RS_ERR_DEVICE;
+  if (ps.have_lut) {
+    if (e->d_plans.ensure(ps.all_plans.size()) || e->d_lut.ensure(c->h_lut.size() * 4)) return RS_ERR_DEVICE;
+    if (hipMemcpy(e->d_plans.p, ps.all_plans.data(), ps.all_plans.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(e->d_lut.p, c->h_lut.data(), c->h_lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      return RS_ERR_DEVICE;
+    e->have_lut = true;
+  }
+  e->h_status.numa = e->numa;
+  if (e->d_status.ensure(kStatusWords * 4) || e->h_status.ensure(kStatusWords * 4)) return RS_ERR_DEVICE;
+  if (hipMemset(e->d_status.p, 0, kStatusWords * 4) != hipSuccess) return RS_ERR_DEVICE;
+  *out = std::move(e);
   return RS_OK;
+}
+
+// Host-side plans shared by every engine of a context.
+PlanSet build_plans(rs_ctx* c) {
+  const int k = c->k, m = c->m, t = k + m;
+  PlanSet ps;
+  // Encode plan: in = data slots 0..k-1, out = parity slots k..k+m-1.
+  {
+    std::vector<int> in_idx(k), out_idx(m);
+    for (int i = 0; i < k; ++i) in_idx[i] = i;
+    for (int p = 0; p < m; ++p) out_idx[p] = k + p;
+    std::vector<uint8_t> rows(static_cast<size_t>(m) * k);
+    for (int p = 0; p < m; ++p)
+      for (int i = 0; i < k; ++i) rows[p * k + i] = c->enc.at(k + p, i);
+    ps.enc_plan = make_plan(k, m, in_idx, out_idx, rows);
+  }
+  // Eager all-pattern plans + LUT for k+m <= 16.  Plan 0 = nothing missing.
+  if (t <= 16 && m > 0) {
+    const uint32_t full = (1u << t) - 1u;
+    c->h_lut.assign(size_t(1) << t, rs::kPlanInvalid);
+    {
+      std::vector<int> in_idx(k), none;
+      for (int i = 0; i < k; ++i) in_idx[i] = i;
+      std::vector<uint8_t> p = make_plan(k, m, in_idx, none, {});
+      ps.all_plans.insert(ps.all_plans.end(), p.begin(), p.end());
+      c->h_lut[0] = 0;
+    }
+    uint32_t count = 1;
+    bool ok = true;
+    for (uint32_t missing = 1; missing <= full && ok; ++missing) {
+      if (__builtin_popcount(missing) > m) continue;
+      std::vector<uint8_t> p;
+      if (make_decode_plan(k, m, c->enc, full & ~missing, false, &p) != RS_OK) continue;
+      if (ps.all_plans.size() + p.size() > (size_t(64) << 20)) {
+        ok = false;
+        break;
+      }
+      ps.all_plans.insert(ps.all_plans.end(), p.begin(), p.end());
+      c->h_lut[missing] = count++;
+    }
+    ps.have_lut = ok;
+    if (!ok) c->h_lut.clear();
+  }
+  return ps;
 }
 
 }  // namespace
+
+// ---- internal interface for the coalescer (rs_engine.hpp) ---------------------------
+namespace rs {
+
+int ctx_engine_count(const rs_ctx* c) { return c ? static_cast<int>(c->engines.size()) : 0; }
+Engine* ctx_engine(rs_ctx* c, int i) { return c->engines[static_cast<size_t>(i)].get(); }
+int engine_device(const Engine* e) { return e->device; }
+
+int engine_encode_batch(Engine* e, const uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
+                        size_t pitch, size_t S, size_t N, hipStream_t s) {
+  if (N == 0 || e->m == 0) return RS_OK;
+  const Layout L{const_cast<uint8_t*>(data), data_sp, parity, parity_sp, pitch};
+  if (!batch_sizes_ok(S, N, pitch) || !device_layout_ok(L, e->m, S)) return RS_ERR_INVALID_ARG;
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);
+  return launch(e, a, e->m, false, s);
+}
+
+int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                 size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
+                                 size_t n_masks, int masks_on_device, uint8_t* out, size_t out_sp, hipStream_t s) {
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!batch_sizes_ok(S, N, pitch)) return RS_ERR_INVALID_ARG;
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, pitch};
+  if (!device_layout_ok(L, e->m, S) || reinterpret_cast<uintptr_t>(out) % 16 || out_sp % 16) return RS_ERR_INVALID_ARG;
+  const int t = e->k + e->m;
+  const uint32_t full = static_cast<uint32_t>(full_mask64(t));
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.out = out;
+  a.out_sp = out_sp;
+  if (masks_on_device) {
+    if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
+    if (!out_layout_ok(out_sp, pitch, S, N, e->m)) return RS_ERR_INVALID_ARG;
+    a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+    a.present_masks = masks;
+    return launch(e, a, e->m, true, s);
+  }
+  if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
+  int max_missing = 0;
+  for (size_t i = 0; i < n_masks; ++i) {
+    const int np = __builtin_popcount(masks[i] & full);
+    if (np < e->k) return RS_ERR_TOO_FEW_SHARDS;
+    max_missing = std::max(max_missing, t - np);
+  }
+  if (max_missing == 0) return RS_OK;
+  if (!out_layout_ok(out_sp, pitch, S, N, max_missing)) return RS_ERR_INVALID_ARG;
+  if (n_masks == 1) {
+    const uint8_t* plan = nullptr;
+    int rc = uniform_plan(e, masks[0] & full, false, &plan);
+    if (rc) return rc;
+    a.plans = plan;
+    return launch(e, a, max_missing, false, s);
+  }
+  if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
+  UploadGuard ug;
+  const uint32_t* dm = nullptr;
+  int rc = upload_acquire(e, masks, N, s, &ug, &dm);
+  if (rc) return rc;
+  a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+  a.present_masks = dm;
+  return launch(e, a, max_missing, true, s);
+}
+
+int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
+                        size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s) {
+  if (N == 0) return RS_OK;
+  if (e->m == 0) {
+    RS_HIP(hipMemsetAsync(bad_dev, 0, N * 4, s));
+    return RS_OK;
+  }
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, pitch};
+  if (!batch_sizes_ok(S, N, pitch) || !device_layout_ok(L, e->m, S)) return RS_ERR_INVALID_ARG;
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.bad = bad_dev;
+  return launch_verify_args(e, a, s);
+}
+
+}  // namespace rs
 
 // =============================================================================
 extern "C" {
@@ -596,7 +1014,7 @@ const char* rs_strerror(int code) {
   }
 }
 
-int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
+int rs_create_devices(int k, int m, const int* devices, int n_devices, int flags, rs_ctx** out) {
   (void)flags;
   if (!out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
@@ -604,99 +1022,77 @@ int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
   if (k <= 0 || m < 0) return RS_ERR_INV_SHARD_NUM;
   if (k + m > 256) return RS_ERR_MAX_SHARD_NUM;
   if (k > rs::kMaxK || m > rs::kMaxM || k + m > 32) return RS_ERR_NOT_SUPPORTED;
+  if (!devices || n_devices <= 0 || n_devices > 64) return RS_ERR_INVALID_ARG;
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RS_ERR_NO_DEVICE;
-  if (device < 0 || device >= ndev) return RS_ERR_NO_DEVICE;
-  if (hipSetDevice(device) != hipSuccess) return RS_ERR_DEVICE;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RS_ERR_DEVICE;
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RS_ERR_NO_DEVICE;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    (void)hipGetLastError();
+    return RS_ERR_NO_DEVICE;
+  }
+  for (int i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= ndev) return RS_ERR_NO_DEVICE;
 
   auto c = std::make_unique<rs_ctx>();
   c->k = k;
   c->m = m;
-  c->device = device;
-  c->cu_count = prop.multiProcessorCount;
   c->enc = rs::build_encode_matrix(k, m);
-  if (const char* e = std::getenv("RSGPU_BLOCKS_PER_CU")) c->blocks_per_cu = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("RSGPU_FORCE_GENERIC")) c->force_generic = std::atoi(e) != 0;
-  if (const char* e = std::getenv("RSGPU_HOST_ZERO_COPY")) c->host_zero_copy = std::atoi(e) != 0;
-  if (const uint8_t* rows = rs::bitsliced_encode_rows(k, m)) {
-    bool same = true;
-    for (int r = 0; r < m; ++r)
-      for (int q = 0; q < k; ++q) same = same && rows[r * k + q] == c->enc.at(k + r, q);
-    c->bitsliced = same;
+  const PlanSet ps = build_plans(c.get());
+  for (int i = 0; i < n_devices; ++i) {
+    std::unique_ptr<Engine> e;
+    const int rc = create_engine(c.get(), devices[i], ps, &e);
+    if (rc) return rc;
+    c->engines.push_back(std::move(e));
   }
-  if (const char* e = std::getenv("RSGPU_BITSLICED")) c->bitsliced = c->bitsliced && std::atoi(e) != 0;
-  char name[160];
-  std::snprintf(name, sizeof(name), "hip:%s:%s:%dCU", prop.gcnArchName, prop.name, c->cu_count);
-  c->backend = name;
-
-  // Encode plan: in = data slots 0..k-1, out = parity slots k..k+m-1.
-  {
-    std::vector<int> in_idx(k), out_idx(m);
-    for (int i = 0; i < k; ++i) in_idx[i] = i;
-    for (int p = 0; p < m; ++p) out_idx[p] = k + p;
-    std::vector<uint8_t> rows(static_cast<size_t>(m) * k);
-    for (int p = 0; p < m; ++p)
-      for (int i = 0; i < k; ++i) rows[p * k + i] = c->enc.at(k + p, i);
-    std::vector<uint8_t> p0 = make_plan(k, m, in_idx, out_idx, rows);
-    if (c->d_enc_plan.ensure(p0.size())) return RS_ERR_DEVICE;
-    if (hipMemcpy(c->d_enc_plan.p, p0.data(), p0.size(), hipMemcpyHostToDevice) != hipSuccess) return RS_ERR_DEVICE;
+  c->backend = c->engines[0]->name;
+  if (n_devices > 1) {
+    c->backend += " x" + std::to_string(n_devices) + " [devices";
+    for (int i = 0; i < n_devices; ++i) c->backend += " " + std::to_string(devices[i]);
+    c->backend += "]";
   }
-  // Eager all-pattern plans + LUT for k+m <= 16.  Plan 0 = nothing missing.
-  const int t = k + m;
-  if (t <= 16 && m > 0) {
-    const uint32_t full = (1u << t) - 1u;
-    c->h_lut.assign(size_t(1) << t, rs::kPlanInvalid);
-    std::vector<uint8_t> all;
-    {
-      std::vector<int> in_idx(k), none;
-      for (int i = 0; i < k; ++i) in_idx[i] = i;
-      std::vector<uint8_t> p = make_plan(k, m, in_idx, none, {});
-      all.insert(all.end(), p.begin(), p.end());
-      c->h_lut[0] = 0;
-    }
-    uint32_t count = 1;
-    bool ok = true;
-    for (uint32_t missing = 1; missing <= full && ok; ++missing) {
-      if (__builtin_popcount(missing) > m) continue;
-      std::vector<uint8_t> p;
-      if (make_decode_plan(k, m, c->enc, full & ~missing, false, &p) != RS_OK) continue;
-      if (all.size() + p.size() > (size_t(64) << 20)) {
-        ok = false;
-        break;
-      }
-      all.insert(all.end(), p.begin(), p.end());
-      c->h_lut[missing] = count++;
-    }
-    if (ok) {
-      if (c->d_plans.ensure(all.size()) || c->d_lut.ensure(c->h_lut.size() * 4)) return RS_ERR_DEVICE;
-      if (hipMemcpy(c->d_plans.p, all.data(), all.size(), hipMemcpyHostToDevice) != hipSuccess ||
-          hipMemcpy(c->d_lut.p, c->h_lut.data(), c->h_lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-        return RS_ERR_DEVICE;
-      c->n_plans = count;
-      c->have_lut = true;
-    }
-  }
-  if (c->d_status.ensure(256) || c->h_status.ensure(256) || c->d_scratch.ensure(256 * 1024)) return RS_ERR_DEVICE;
-  if (hipMemset(c->d_status.p, 0, 256) != hipSuccess) return RS_ERR_DEVICE;
   *out = c.release();
   return RS_OK;
 }
 
-void rs_destroy(rs_ctx* ctx) {
-  if (!ctx) return;
-  (void)hipSetDevice(ctx->device);
-  (void)hipDeviceSynchronize();
-  delete ctx;
+int rs_create(int k, int m, int device, int flags, rs_ctx** out) {
+  return rs_create_devices(k, m, &device, 1, flags, out);
 }
+
+int rs_create_multi(int k, int m, uint64_t device_mask, int flags, rs_ctx** out) {
+  if (!out) return RS_ERR_INVALID_ARG;
+  *out = nullptr;
+  if (k <= 0 || m < 0) return RS_ERR_INV_SHARD_NUM;
+  if (k + m > 256) return RS_ERR_MAX_SHARD_NUM;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    (void)hipGetLastError();
+    return RS_ERR_NO_DEVICE;
+  }
+  std::vector<int> devs;
+  for (int d = 0; d < std::min(ndev, 64); ++d) {
+    if (device_mask && !((device_mask >> d) & 1u)) continue;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d) != hipSuccess) return RS_ERR_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      if (device_mask) return RS_ERR_NO_DEVICE;  // an explicitly named device must be usable
+      continue;
+    }
+    devs.push_back(d);
+  }
+  if (device_mask >> std::min(ndev, 64)) return RS_ERR_NO_DEVICE;  // names a device that does not exist
+  if (devs.empty()) return RS_ERR_NO_DEVICE;
+  return rs_create_devices(k, m, devs.data(), static_cast<int>(devs.size()), flags, out);
+}
+
+void rs_destroy(rs_ctx* ctx) { delete ctx; }
 
 int rs_data_shards(const rs_ctx* c) { return c ? c->k : 0; }
 int rs_parity_shards(const rs_ctx* c) { return c ? c->m : 0; }
-int rs_device(const rs_ctx* c) { return c ? c->device : -1; }
+int rs_device(const rs_ctx* c) { return c ? c->engines[0]->device : -1; }
+int rs_device_count(const rs_ctx* c) { return c ? static_cast<int>(c->engines.size()) : 0; }
+int rs_device_at(const rs_ctx* c, int i) {
+  return (c && i >= 0 && i < static_cast<int>(c->engines.size())) ? c->engines[static_cast<size_t>(i)]->device : -1;
+}
 const char* rs_backend(const rs_ctx* c) { return c ? c->backend.c_str() : "none"; }
-const char* rs_last_kernel(const rs_ctx* c) { return c ? c->last_kernel.load() : "none"; }
+const char* rs_last_kernel(const rs_ctx* c) { return c ? c->shared.last_kernel.load() : "none"; }
 
 int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
   if (!c || !out) return RS_ERR_INVALID_ARG;
@@ -720,7 +1116,11 @@ int rs_encode(rs_ctx* c, uint8_t* const* shards, const size_t* lens) {
   std::vector<int> in_idx(c->k), out_idx(c->m);
   for (int i = 0; i < c->k; ++i) in_idx[i] = i;
   for (int p = 0; p < c->m; ++p) out_idx[p] = c->k + p;
-  return run_object(c, static_cast<const uint8_t*>(c->d_enc_plan.p), in_idx, out_idx, shards, S);
+  Engine* e = pick_engine(c);
+  InflightGuard ig(e);
+  DeviceScope ds(e->device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
+  return run_object(e, static_cast<const uint8_t*>(e->d_enc_plan.p), in_idx, out_idx, shards, S);
 }
 
 int rs_reconstruct(rs_ctx* c, uint8_t* const* shards, size_t* lens) { return reconstruct_impl(c, shards, lens, false); }
@@ -728,8 +1128,8 @@ int rs_reconstruct_data(rs_ctx* c, uint8_t* const* shards, size_t* lens) {
   return reconstruct_impl(c, shards, lens, true);
 }
 
-// [upstream reedsolomon.go Verify]: recompute parity on the GPU into scratch and
-// compare on the host against the caller's parity shards.
+// [upstream reedsolomon.go Verify]: recompute parity on the GPU into temporary
+// shards and compare on the host against the caller's parity shards.
 int rs_verify(rs_ctx* c, uint8_t* const* shards, const size_t* lens, int* ok) {
   if (!c || !shards || !lens || !ok) return RS_ERR_INVALID_ARG;
   size_t S = 0;
@@ -743,7 +1143,11 @@ int rs_verify(rs_ctx* c, uint8_t* const* shards, const size_t* lens, int* ok) {
   std::vector<int> in_idx(c->k), out_idx(c->m);
   for (int i = 0; i < c->k; ++i) in_idx[i] = i;
   for (int p = 0; p < c->m; ++p) out_idx[p] = c->k + p;
-  rc = run_object(c, static_cast<const uint8_t*>(c->d_enc_plan.p), in_idx, out_idx, view.data(), S);
+  Engine* e = pick_engine(c);
+  InflightGuard ig(e);
+  DeviceScope ds(e->device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
+  rc = run_object(e, static_cast<const uint8_t*>(e->d_enc_plan.p), in_idx, out_idx, view.data(), S);
   if (rc) return rc;
   for (int p = 0; p < c->m; ++p)
     if (std::memcmp(tmp[p].data(), shards[c->k + p], S) != 0) *ok = 0;
@@ -757,20 +1161,21 @@ int rs_encode_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, uint8_t* par
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
   if (!batch_sizes_ok(S, N, shard_pitch)) return RS_ERR_INVALID_ARG;
   if (c->m == 0) return RS_OK;
-  (void)hipSetDevice(c->device);
   const Layout L{const_cast<uint8_t*>(data), data_sp, parity, parity_sp, shard_pitch};
-  const uint8_t* plan = static_cast<const uint8_t*>(c->d_enc_plan.p);
   if (mem == RS_MEM_DEVICE) {
-    if (!device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
-    rs::KernelArgs a = make_args(c, L, S, N);
-    a.plans = plan;
-    return launch(c, a, c->m, false, as_stream(stream));
+    Engine* e = engine_for_stream(c, as_stream(stream));
+    if (!e) return RS_ERR_INVALID_ARG;
+    DeviceScope ds(e->device);
+    return rs::engine_encode_batch(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, as_stream(stream));
   }
   if (mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
   std::vector<int> in_slots(c->k), out_slots(c->m);
   for (int i = 0; i < c->k; ++i) in_slots[i] = i;
   for (int p = 0; p < c->m; ++p) out_slots[p] = c->k + p;
-  return host_batch(c, L, in_slots, out_slots, S, N, plan, nullptr, c->m);
+  return fan_out(c, N, static_cast<size_t>(c->k) * S, [&](Engine* e, size_t s0, size_t n) {
+    return host_batch(e, L.from(s0), in_slots, out_slots, S, n, static_cast<const uint8_t*>(e->d_enc_plan.p),
+                      nullptr, c->m);
+  });
 }
 
 int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
@@ -793,18 +1198,29 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
   if (mem != RS_MEM_DEVICE && mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
   const Layout L{data, data_sp, parity, parity_sp, shard_pitch};
   if (mem == RS_MEM_DEVICE && !device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
+  if (n_masks != 1 && c->h_lut.empty()) return RS_ERR_NOT_SUPPORTED;
+  if (mem == RS_MEM_DEVICE) {
+    hipStream_t s = as_stream(stream);
+    Engine* e = engine_for_stream(c, s);
+    if (!e) return RS_ERR_INVALID_ARG;
+    DeviceScope ds(e->device);
+    rs::KernelArgs a = make_args(e, L, S, N);
+    if (n_masks == 1) {
+      int rc = uniform_plan(e, masks[0] & full, false, &a.plans);
+      if (rc) return rc;
+      return launch(e, a, max_missing, false, s);
+    }
+    UploadGuard ug;
+    const uint32_t* dm = nullptr;
+    int rc = upload_acquire(e, masks, N, s, &ug, &dm);
+    if (rc) return rc;
+    a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+    a.present_masks = dm;
+    return launch(e, a, max_missing, true, s);
+  }
+  std::vector<int> in_slots, out_slots;
   if (n_masks == 1) {
     const uint32_t present = masks[0] & full;
-    const uint8_t* plan = nullptr;
-    int rc = uniform_plan(c, present, false, &plan);
-    if (rc) return rc;
-    if (mem == RS_MEM_DEVICE) {
-      rs::KernelArgs a = make_args(c, L, S, N);
-      a.plans = plan;
-      return launch(c, a, max_missing, false, as_stream(stream));
-    }
-    std::vector<int> in_slots, out_slots;
     for (int i = 0; i < t; ++i) {
       if ((present >> i) & 1u) {
         if (static_cast<int>(in_slots.size()) < c->k) in_slots.push_back(i);
@@ -812,24 +1228,23 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
         out_slots.push_back(i);
       }
     }
-    return host_batch(c, L, in_slots, out_slots, S, N, plan, nullptr, max_missing);
+  } else {
+    // per-stripe patterns: every slot travels both ways on the staged path (present
+    // slots come back unchanged); the zero-copy path touches only what it needs
+    for (int i = 0; i < t; ++i) in_slots.push_back(i);
+    out_slots = in_slots;
   }
-  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
-  if (mem == RS_MEM_DEVICE) {
-    hipStream_t s = as_stream(stream);
-    const uint32_t* dm = nullptr;
-    int rc = upload_masks(c, masks, N, s, &dm);
-    if (rc) return rc;
-    rs::KernelArgs a = make_args(c, L, S, N);
-    a.plans = static_cast<const uint8_t*>(c->d_plans.p);
-    a.present_masks = dm;
-    return launch(c, a, max_missing, true, s);
-  }
-  // host, per-stripe patterns: every slot travels both ways (present slots come back
-  // unchanged); selective copies per pattern are a later optimisation.
-  std::vector<int> all(t);
-  for (int i = 0; i < t; ++i) all[i] = i;
-  return host_batch(c, L, all, all, S, N, static_cast<const uint8_t*>(c->d_plans.p), masks, max_missing);
+  return fan_out(c, N, static_cast<size_t>(c->k) * S, [&](Engine* e, size_t s0, size_t n) {
+    const uint8_t* plan = static_cast<const uint8_t*>(e->d_plans.p);
+    const uint32_t* mk = nullptr;
+    if (n_masks == 1) {
+      int rc = uniform_plan(e, masks[0] & full, false, &plan);
+      if (rc) return rc;
+    } else {
+      mk = masks + s0;
+    }
+    return host_batch(e, L.from(s0), in_slots, out_slots, S, n, plan, mk, max_missing);
+  });
 }
 
 int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
@@ -837,47 +1252,11 @@ int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, con
                              int masks_on_device, uint8_t* out, size_t out_sp, void* stream) {
   if (!c || !data || (c->m > 0 && !parity) || !masks || !out) return RS_ERR_INVALID_ARG;
   if (N == 0) return RS_OK;
-  if (S == 0) return RS_ERR_SHARD_NO_DATA;
-  if (!batch_sizes_ok(S, N, shard_pitch)) return RS_ERR_INVALID_ARG;
-  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, shard_pitch};
-  if (!device_layout_ok(L, c->m, S) || reinterpret_cast<uintptr_t>(out) % 16 || out_sp % 16) return RS_ERR_INVALID_ARG;
-  const int t = c->k + c->m;
-  const uint32_t full = static_cast<uint32_t>(full_mask64(t));
-  (void)hipSetDevice(c->device);
-  hipStream_t s = as_stream(stream);
-  rs::KernelArgs a = make_args(c, L, S, N);
-  a.out = out;
-  a.out_sp = out_sp;
-  if (masks_on_device) {
-    if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
-    if (!out_layout_ok(out_sp, shard_pitch, S, N, c->m)) return RS_ERR_INVALID_ARG;
-    a.plans = static_cast<const uint8_t*>(c->d_plans.p);
-    a.present_masks = masks;
-    return launch(c, a, c->m, true, s);
-  }
-  if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
-  int max_missing = 0;
-  for (size_t i = 0; i < n_masks; ++i) {
-    const int np = __builtin_popcount(masks[i] & full);
-    if (np < c->k) return RS_ERR_TOO_FEW_SHARDS;
-    max_missing = std::max(max_missing, t - np);
-  }
-  if (max_missing == 0) return RS_OK;
-  if (!out_layout_ok(out_sp, shard_pitch, S, N, max_missing)) return RS_ERR_INVALID_ARG;
-  if (n_masks == 1) {
-    const uint8_t* plan = nullptr;
-    int rc = uniform_plan(c, masks[0] & full, false, &plan);
-    if (rc) return rc;
-    a.plans = plan;
-    return launch(c, a, max_missing, false, s);
-  }
-  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
-  const uint32_t* dm = nullptr;
-  int rc = upload_masks(c, masks, N, s, &dm);
-  if (rc) return rc;
-  a.plans = static_cast<const uint8_t*>(c->d_plans.p);
-  a.present_masks = dm;
-  return launch(c, a, max_missing, true, s);
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
+  return rs::engine_reconstruct_batch_out(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, masks, n_masks,
+                                          masks_on_device, out, out_sp, as_stream(stream));
 }
 
 int rs_verify_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
@@ -887,25 +1266,22 @@ int rs_verify_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
   if (!batch_sizes_ok(S, N, shard_pitch) || reinterpret_cast<uintptr_t>(bad) % 4) return RS_ERR_INVALID_ARG;
   if (mem != RS_MEM_DEVICE && mem != RS_MEM_HOST) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
+  if (mem == RS_MEM_DEVICE) {
+    Engine* e = engine_for_stream(c, as_stream(stream));
+    if (!e) return RS_ERR_INVALID_ARG;
+    DeviceScope ds(e->device);
+    return rs::engine_verify_batch(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, bad, as_stream(stream));
+  }
   if (c->m == 0) {  // nothing to verify
-    if (mem == RS_MEM_HOST) {
-      std::memset(bad, 0, N * 4);
-      return RS_OK;
-    }
-    RS_HIP(hipMemsetAsync(bad, 0, N * 4, as_stream(stream)));
+    std::memset(bad, 0, N * 4);
     return RS_OK;
   }
   const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, shard_pitch};
-  if (mem == RS_MEM_DEVICE) {
-    if (!device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
-    rs::KernelArgs a = make_args(c, L, S, N);
-    a.bad = bad;
-    return launch_verify_args(c, a, as_stream(stream));
-  }
   std::vector<int> all(c->k + c->m), none;
   for (int i = 0; i < c->k + c->m; ++i) all[i] = i;
-  return host_batch(c, L, all, none, S, N, nullptr, nullptr, c->m, bad);
+  return fan_out(c, N, static_cast<size_t>(c->k) * S, [&](Engine* e, size_t s0, size_t n) {
+    return host_batch(e, L.from(s0), all, none, S, n, nullptr, nullptr, c->m, bad + s0);
+  });
 }
 
 int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
@@ -913,41 +1289,57 @@ int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8
   if (!c || !data || (c->m > 0 && !parity) || !masks_dev) return RS_ERR_INVALID_ARG;
   if (N == 0) return RS_OK;
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
-  if (!c->have_lut) return RS_ERR_NOT_SUPPORTED;
+  if (c->h_lut.empty()) return RS_ERR_NOT_SUPPORTED;
   const Layout L{data, data_sp, parity, parity_sp, shard_pitch};
   if (!batch_sizes_ok(S, N, shard_pitch) || !device_layout_ok(L, c->m, S)) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
-  rs::KernelArgs a = make_args(c, L, S, N);
-  a.plans = static_cast<const uint8_t*>(c->d_plans.p);
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.plans = static_cast<const uint8_t*>(e->d_plans.p);
   a.present_masks = masks_dev;
-  return launch(c, a, c->m, true, as_stream(stream));
+  return launch(e, a, c->m, true, as_stream(stream));
 }
 
 int rs_sync(rs_ctx* c, void* stream) {
   if (!c) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
   hipStream_t s = as_stream(stream);
-  RS_HIP(hipMemcpyAsync(c->h_status.p, c->d_status.p, 4, hipMemcpyDeviceToHost, s));
+  Engine* e = engine_for_stream(c, s);
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
+  uint32_t idx;
+  {
+    std::lock_guard<std::mutex> g(e->status_mu);
+    auto it = e->status_idx.find(s);
+    if (it == e->status_idx.end()) {  // no per-stripe launch on this stream yet
+      RS_HIP(hipStreamSynchronize(s));
+      return RS_OK;
+    }
+    idx = it->second;
+  }
+  uint32_t* dw = static_cast<uint32_t*>(e->d_status.p) + idx;
+  volatile uint32_t* hw = static_cast<uint32_t*>(e->h_status.p) + idx;
+  RS_HIP(hipMemcpyAsync(const_cast<uint32_t*>(hw), dw, 4, hipMemcpyDeviceToHost, s));
   RS_HIP(hipStreamSynchronize(s));
-  const uint32_t st = *static_cast<uint32_t*>(c->h_status.p);
-  if (st) {
-    RS_HIP(hipMemsetAsync(c->d_status.p, 0, 4, s));
+  if (*hw) {
+    RS_HIP(hipMemsetAsync(dw, 0, 4, s));
     RS_HIP(hipStreamSynchronize(s));
     return RS_ERR_TOO_FEW_SHARDS;
   }
   return RS_OK;
 }
 
+// Pins for every GPU of the process (portable) and maps into their address spaces.
 int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
   if (!c || !ptr) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
-  RS_HIP(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+  DeviceScope ds(c->engines[0]->device);
+  RS_HIP(hipHostRegister(ptr, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
   return RS_OK;
 }
 
 int rs_host_unregister(rs_ctx* c, void* ptr) {
   if (!c || !ptr) return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
+  DeviceScope ds(c->engines[0]->device);
   RS_HIP(hipHostUnregister(ptr));
   return RS_OK;
 }
@@ -956,11 +1348,13 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   if (!c || !dst || !src || bytes % 16 || reinterpret_cast<uintptr_t>(dst) % 16 ||
       reinterpret_cast<uintptr_t>(src) % 16)
     return RS_ERR_INVALID_ARG;
-  (void)hipSetDevice(c->device);
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
   const uint32_t grid = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(c->cu_count) * 2, (bytes / 16 + 1023) / 1024)));
+      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count) * 2, (bytes / 16 + 1023) / 1024)));
   rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
-  c->last_kernel.store("copy_kernel");
+  c->shared.last_kernel.store("copy_kernel");
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -973,10 +1367,12 @@ int rs_sha256_batch(rs_ctx* c, const uint8_t* base, size_t stride, size_t len, s
       reinterpret_cast<uintptr_t>(digests) % 4)
     return RS_ERR_INVALID_ARG;
   if (n == 0) return RS_OK;
-  (void)hipSetDevice(c->device);
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
   const rs::Sha256Args a{base, stride, nullptr, nullptr, len, static_cast<uint32_t>(n), digests};
   if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
-  c->last_kernel.store("sha256_kernel");
+  c->shared.last_kernel.store("sha256_kernel");
   return RS_OK;
 }
 
@@ -986,24 +1382,26 @@ int rs_sha256_batch_var(rs_ctx* c, const uint8_t* base, const uint64_t* offsets,
       reinterpret_cast<uintptr_t>(digests) % 4)
     return RS_ERR_INVALID_ARG;
   if (n == 0) return RS_OK;
-  (void)hipSetDevice(c->device);
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
   const rs::Sha256Args a{base, 0, offsets, lens, 0, static_cast<uint32_t>(n), digests};
   if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
-  c->last_kernel.store("sha256_kernel");
+  c->shared.last_kernel.store("sha256_kernel");
   return RS_OK;
 }
 
 int rs_set_host_zero_copy(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
-  c->host_zero_copy = enable != 0;
+  for (auto& e : c->engines) e->host_zero_copy = enable != 0;
   return RS_OK;
 }
 
-const char* rs_last_host_path(const rs_ctx* c) { return c ? c->last_host_path.load() : "none"; }
+const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_path.load() : "none"; }
 
 int rs_set_blocks_per_cu(rs_ctx* c, int bpc) {
   if (!c || bpc < 0) return RS_ERR_INVALID_ARG;
-  c->blocks_per_cu = bpc;  // 0 = by shape
+  for (auto& e : c->engines) e->blocks_per_cu = bpc;  // 0 = by shape
   return RS_OK;
 }
 

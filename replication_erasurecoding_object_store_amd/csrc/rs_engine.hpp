@@ -1,0 +1,62 @@
+// rs_engine.hpp -- internal interface between the context / dispatch layer
+// (rs_engine.cpp) and the batch coalescer (rs_coalescer.cpp).  Not part of the
+// C-ABI.
+//
+// An rs_ctx owns one Engine per device it spans (rs_create: one; rs_create_multi /
+// rs_create_devices: several, one process driving several GPUs the way the
+// reference's single IEcDriver serves every request goroutine,
+// cmd/api/main.go:206).  An Engine is everything one GPU needs: plans and LUT in
+// its HBM, streams, staging, status words.  The coalescer stages batches in
+// portable pinned memory and hands each one to the least-loaded Engine.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/rsgpu.h"
+
+namespace rs {
+
+struct Engine;
+
+int ctx_engine_count(const rs_ctx* c);
+Engine* ctx_engine(rs_ctx* c, int i);
+int engine_device(const Engine* e);
+
+// Makes `device` current for the scope and restores the caller's device after, so
+// library calls never change the calling thread's HIP device (a Go thread or a
+// torch program may be using another GPU).
+class DeviceScope {
+ public:
+  explicit DeviceScope(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    if (prev_ != device) ok_ = hipSetDevice(device) == hipSuccess;
+    else prev_ = -1;  // nothing to restore
+  }
+  ~DeviceScope() {
+    if (prev_ >= 0) (void)hipSetDevice(prev_);
+  }
+  bool ok() const { return ok_; }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+
+ private:
+  int prev_ = -1;
+  bool ok_ = true;
+};
+
+// Device-resident batch entry points on one Engine (asynchronous on s, which must
+// belong to the engine's device; the caller holds a DeviceScope for it).
+// Contracts as rs_encode_batch / rs_reconstruct_batch_out / rs_verify_batch with
+// RS_MEM_DEVICE; the pointers may also be GPU-mapped pinned host memory.
+int engine_encode_batch(Engine* e, const uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
+                        size_t pitch, size_t S, size_t N, hipStream_t s);
+int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                 size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
+                                 size_t n_masks, int masks_on_device, uint8_t* out, size_t out_sp, hipStream_t s);
+int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
+                        size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s);
+
+}  // namespace rs

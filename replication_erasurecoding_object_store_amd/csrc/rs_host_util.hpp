@@ -33,6 +33,17 @@ inline int check_shards(int n, const size_t* lens, bool nilok, size_t* S) {
   return RS_OK;
 }
 
+// Pinned host allocation usable by every GPU of the process (portable), placed on
+// `numa_node` when >= 0 (the GPU's own node, so its DMA and zero-copy traffic stays
+// off the inter-socket link).  Returns nullptr on failure.  (rs_engine.cpp)
+void* pinned_alloc(size_t bytes, int numa_node);
+void pinned_free(void* p);
+// NUMA node of a GPU from sysfs (-1 if unknown).
+int device_numa_node(int device);
+
+// Device memory on the calling thread's current device (callers hold a
+// DeviceScope).  ensure() only grows; hipFree synchronises the device first, so
+// growing under in-flight work is safe, just slow.
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
@@ -56,12 +67,13 @@ struct DevBuf {
 struct PinnedBuf {
   void* p = nullptr;
   size_t n = 0;
+  int numa = -1;  // NUMA node to place the pages on (-1: the allocating thread's)
   int ensure(size_t bytes) {
     if (bytes <= n) return RS_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
+    if (p) pinned_free(p);
     n = 0;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return RS_ERR_DEVICE;
+    p = pinned_alloc(bytes, numa);
+    if (!p) return RS_ERR_DEVICE;
     n = bytes;
     return RS_OK;
   }
@@ -69,7 +81,7 @@ struct PinnedBuf {
   PinnedBuf(const PinnedBuf&) = delete;
   PinnedBuf& operator=(const PinnedBuf&) = delete;
   ~PinnedBuf() {
-    if (p) (void)hipHostFree(p);
+    if (p) pinned_free(p);
   }
 };
 

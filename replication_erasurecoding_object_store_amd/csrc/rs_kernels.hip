@@ -23,11 +23,14 @@
 //     the 16 B at column 64*blk + l of every shard), 1-2 workgroups per CU;
 //   * 16-B non-temporal loads and stores (one 1 KiB wave instruction each).
 // Every loop trip issues the same vector-memory sequence -- [mask(t+1)] [K loads]
-// [E stores] -- with no branch around any of them (lanes past the last full column
-// and outputs beyond a plan's n_out store to a per-wave scratch line), so the
-// compiler's s_waitcnt vmcnt(N) counts stay exact and the per-stripe plan lookup of
-// the NEXT task overlaps the current task.  Partial tail columns (S % 16) are done
-// by tail_kernel.
+// [E stores] -- with no branch around any of them (lanes past the last column load
+// the last column again, and stores that must not land are raw buffer stores the
+// hardware drops on its range check), so the compiler's s_waitcnt vmcnt(N) counts
+// stay exact and the per-stripe plan lookup of the NEXT task overlaps the current
+// task.  A partial last column (S % 16 != 0) is loaded and computed like any other
+// (its 16-B column lies inside the slot) and stored byte-exact by the lane that
+// holds it, in a wave-uniform branch taken only by a stripe's last block.  Every
+// store is a buffer store: in order in vmcnt, unlike flat stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,48 +39,6 @@
 #include "rs_plan.hpp"
 
 namespace rs {
-
-// A/B knob (tools/ab_libs.py): 0 restores one plan base for all of a trip's inputs.
-#ifndef RS_OPAQUE_INPUT_TABLES
-#define RS_OPAQUE_INPUT_TABLES 1
-#endif
-constexpr bool kOpaqueInputTables = RS_OPAQUE_INPUT_TABLES != 0;
-// A/B knob: 0 = per-stripe kernels always compute all E outputs.
-#ifndef RS_SPLIT_OUTPUTS
-#define RS_SPLIT_OUTPUTS 1
-#endif
-constexpr bool kSplitOutputs = RS_SPLIT_OUTPUTS != 0;
-// A/B knob: 1 = per-stripe kernels sized for E >= 4 outputs also skip row 1 when a
-// stripe's plan fills a single shard (rows [0,1) [1,E/2) [E/2,E)).
-#ifndef RS_SPLIT_ROW1
-#define RS_SPLIT_ROW1 1
-#endif
-constexpr bool kSplitRow1 = RS_SPLIT_ROW1 != 0;
-// A/B knob: 1 = lanes past the last full column load the last full column (the
-// same lines as the wave's valid lanes), and stores that must not land (those
-// lanes; rows beyond a stripe plan's n_out) are raw buffer stores the hardware
-// drops on its range check -- no branch, no traffic.  0 = loads from column 0 and
-// stores into a scratch sink, whose lines get written back to HBM (PMC: +35-60 MB
-// per RS(10+4) launch, profiles/r01h_kmsweep_pmc.md).
-#ifndef RS_NO_SINK
-#define RS_NO_SINK 1
-#endif
-constexpr bool kNoSink = RS_NO_SINK != 0;
-// A/B knob: 1 = a fused tail task is one lane per stripe doing every output row
-// (the inputs' lines come from HBM once); 0 = one task per (64 stripes, row), run by
-// different waves, which re-read the inputs' lines from HBM once per row (PMC:
-// +37 MB per RS(10+4) launch).  Off: a full-suite run with it on hit one illegal
-// address fault (test_reconstruct_out_of_place[100-8-4]) that the test alone,
-// serialized, did not repeat; unresolved, so the proven scheme stays the default.
-#ifndef RS_TAIL_ALL_ROWS
-#define RS_TAIL_ALL_ROWS 0
-#endif
-constexpr bool kTailAllRows = RS_TAIL_ALL_ROWS != 0;
-// A/B knob: 1 = the main kernel also does the partial last column (no tail launch).
-#ifndef RS_FUSED_TAIL
-#define RS_FUSED_TAIL 1
-#endif
-constexpr bool kFusedTail = RS_FUSED_TAIL != 0;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -147,14 +108,43 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
   return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
+// Raw buffer descriptor over [base, base + 2 GiB); base must be wave-uniform.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(uint8_t* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, 0x7FFFFFFF, 0x00020000);
+}
+
 // 16-B non-temporal store at base + off, or nothing at all when !live: a raw buffer
-// store (descriptor over [base, base + 2 GiB)) whose offset then fails the range
-// check, so the hardware drops it -- no branch around the store and no sink line
-// to write back.  base must be wave-uniform; off < 2 GiB.
+// store whose offset then fails the range check, so the hardware drops it -- no
+// branch around the store and no sink line to write back.  off < 2 GiB.
 __device__ __forceinline__ void store16_or_drop(uint8_t* base, uint32_t off, bool live, u32x4 v) {
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, 0x7FFFFFFF,
-                                                      0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, live ? off : kDropOffset, 0, 2 /* nt */);
+  __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc(base), live ? off : kDropOffset, 0, 2 /* nt */);
+}
+
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+// The first nb (1..15, wave-uniform) bytes of v at base + off in at most four
+// naturally aligned buffer stores (8, 4, 2, 1 B), landing only for `live` lanes.
+__device__ __forceinline__ void store_part_or_drop(uint8_t* base, uint32_t off, bool live, u32x4 v, uint32_t nb) {
+  const auto rsrc = out_rsrc(base);
+  const uint32_t o = live ? off : kDropOffset;
+  uint32_t q = 0;  // bytes stored so far
+  if (nb & 8u) {
+    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, rsrc, o, 0, 2);
+    q = 8;
+  }
+  uint32_t w = q ? v[2] : v[0];  // dword holding byte q
+  if (nb & 4u) {
+    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
+    q += 4;
+    w = q == 12u ? v[3] : v[1];
+  }
+  if (nb & 2u) {
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
+    q += 2;
+    w >>= 16;
+  }
+  if (nb & 1u)
+    __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
 }
 
 // Shard slot s of stripe i (s < k: data region, else parity region).
@@ -171,33 +161,6 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
                : slot_ptr(a, k, stripe, slot);
 }
 
-template <int K, int M, bool PER_STRIPE>
-__device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint32_t r);
-template <int K, int M, int E, bool PER_STRIPE>
-__device__ __forceinline__ void tail_stripe(const KernelArgs& a, uint32_t i);
-
-// The fused tail pass of a main kernel: the partial last column (S % 16 != 0) of
-// every stripe, picked up by waves as they leave the main loop (saves a tail
-// launch and its gap; see tail_kernel).
-template <int K, int M, int E, bool PER_STRIPE>
-__device__ __forceinline__ void fused_tail(const KernelArgs& a, uint32_t wave, uint32_t nwaves, uint32_t lane) {
-  if (a.full_cols * 16u == a.shard_len) return;
-  const uint32_t groups = (a.n_stripes + 63u) / 64u;
-  if constexpr (kTailAllRows) {
-    for (uint32_t g = wave; g < groups; g += nwaves) {
-      const uint32_t i = g * 64u + lane;
-      if (i < a.n_stripes) tail_stripe<K, M, E, PER_STRIPE>(a, i);
-    }
-  } else {
-    const uint32_t ttasks = groups * static_cast<uint32_t>(E);
-    for (uint32_t tt = wave; tt < ttasks; tt += nwaves) {
-      const uint32_t r = tt % static_cast<uint32_t>(E);
-      const uint32_t i = (tt / static_cast<uint32_t>(E)) * 64u + lane;
-      if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, r);
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
 // #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
@@ -206,9 +169,10 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t bps = a.blocks_full;
+  const uint32_t bps = a.blocks_per_stripe;   // the partial last column included
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
-  uint8_t* const dummy = a.scratch + (wave & 255u) * 1024u + lane * 16u;
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t nb = a.shard_len & 15u;      // bytes of a partial last column (0: none)
   uint32_t bad = 0u;
 
   // mask of task t's stripe; every lane loads the same word (one request)
@@ -229,7 +193,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       const uint32_t missing = (~present) & a.full_mask;
       uint32_t pid = as_const<uint32_t>(a.lut)[missing];
       bad |= (pid == kPlanInvalid) ? 1u : 0u;
-      pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> scratch stores
+      pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     }
     if constexpr (K * E * 5 > 48) {
@@ -240,9 +204,10 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     }
     const PlanView pv(plan, K, M);
     const uint32_t col = blk * 64u + lane;
-    const bool valid = col < a.full_cols;
-    // clamped, never branched
-    const uint32_t off = valid ? col * 16u : (kNoSink ? (a.full_cols - 1u) * 16u : 0u);
+    const bool full = col < a.full_cols;
+    // clamped, never branched: a lane past the end re-reads the last column (lines
+    // the wave's other lanes fetch anyway) and its stores are dropped
+    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
 
     u32x4 x[K];
 #pragma unroll
@@ -259,9 +224,9 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     // Per-stripe batches carry mixed patterns: rows [kLo, E) are only computed
     // when this task's plan fills more than kLo shards (a wave-uniform branch per
     // input), so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs
-    // do half the lookups.  Skipped rows are stored to scratch, never to memory.
-    constexpr int kLo = (PER_STRIPE && kSplitOutputs && E >= 4) ? E / 2 : E;
-    constexpr int kLo1 = (kLo < E && kSplitRow1) ? 1 : kLo;  // rows [kLo1, kLo) when n_out > kLo1
+    // do half the lookups.  Skipped rows' stores are dropped.
+    constexpr int kLo = (PER_STRIPE && E >= 4) ? E / 2 : E;
+    constexpr int kLo1 = kLo < E ? 1 : kLo;  // rows [kLo1, kLo) when n_out > kLo1
     const bool hi_rows = kLo == E || pv.n_out() > static_cast<uint32_t>(kLo);
     const bool mid_rows = kLo1 == kLo || pv.n_out() > static_cast<uint32_t>(kLo1);
 #pragma unroll
@@ -272,7 +237,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       // one opaque base per input: the scalar load merger cannot fuse this
       // input's table loads with later inputs' (which would pin them in SGPRs)
       const uint8_t* tcol = plan;
-      if constexpr (kOpaqueInputTables && K * E * 5 > 48) asm volatile("" : "+s"(tcol));
+      if constexpr (K * E * 5 > 48) asm volatile("" : "+s"(tcol));
       const PlanView pc(tcol, K, M);
       auto rows = [&](auto lo_tag, auto hi_tag, const PlanView& pt) {
         constexpr int R0 = decltype(lo_tag)::value, R1 = decltype(hi_tag)::value;
@@ -311,18 +276,17 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     }
     const uint32_t n_out = pv.n_out();
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-      if constexpr (kNoSink) {
-        store16_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, valid && static_cast<uint32_t>(r) < n_out,
-                        y[r]);
-      } else {
-        uint8_t* real = out_ptr(a, K, stripe, r, pv.out_idx(r)) + off;
-        store16((valid && static_cast<uint32_t>(r) < n_out) ? real : dummy, y[r]);
-      }
+    for (int r = 0; r < E; ++r)
+      store16_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, full && static_cast<uint32_t>(r) < n_out, y[r]);
+    if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
+      const bool part = col == a.full_cols;
+#pragma unroll
+      for (int r = 0; r < E; ++r)
+        store_part_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, part && static_cast<uint32_t>(r) < n_out,
+                           y[r], nb);
     }
   }
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
-  if constexpr (kFusedTail) fused_tail<K, M, E, PER_STRIPE>(a, wave, nwaves, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -389,67 +353,6 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
 }
 
 // ---------------------------------------------------------------------------
-// Partial last column of every shard (S % 16 != 0) for the specialised kernels.
-// Thread (stripe i, output r): r = blockIdx.y is wave-uniform, so a uniform plan's
-// tables for row r come through scalar loads; stripes spread over the lanes.  The
-// whole 16-B column lies inside the shard slot (shard_pitch >= round_up(S, 16)),
-// so inputs are read as one 16-B load each; only the nb valid output bytes are
-// stored.  Keeps the main loop branch-free.
-template <int K, int M, bool PER_STRIPE>
-__device__ __forceinline__ void tail_task(const KernelArgs& a, uint32_t i, uint32_t r) {
-  const uint32_t off = a.full_cols * 16u;
-  const uint32_t nb = a.shard_len - off;  // 1..15
-  u32x4 y = u32x4{0u, 0u, 0u, 0u};
-  if constexpr (PER_STRIPE) {
-    const uint32_t missing = (~a.present_masks[i]) & a.full_mask;
-    const uint32_t pid = a.lut[missing];
-    if (pid == kPlanInvalid) {
-      if (r == 0) atomicOr(a.status, 1u);
-      return;
-    }
-    const uint8_t* plan = a.plans + static_cast<uint64_t>(pid) * a.plan_bytes;
-    const uint32_t* pw = reinterpret_cast<const uint32_t*>(plan);
-    if (r >= pw[0]) return;
-    const uint32_t* tab = reinterpret_cast<const uint32_t*>(plan + plan_tab_offset(K, M)) + r * K * 5;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, pw[2 + c]) + off);
-      const uint32_t* tb = tab + c * 5;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), tb[0], tb[1], tb[2], tb[3], tb[4]);
-    }
-    store_tail(out_ptr(a, K, i, r, pw[2 + K + r]) + off, y, nb);
-  } else {
-    const PlanView pv(uniform_ptr(a.plans), K, M);
-    if (r >= pv.n_out()) return;
-#pragma unroll
-    for (int c = 0; c < K; ++c) {
-      const u32x4 x = *reinterpret_cast<const u32x4*>(slot_ptr(a, K, i, pv.in_idx(c)) + off);
-      const RS_CONST uint32_t* tb = pv.tab(static_cast<int>(r), c);
-      const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) y[d] ^= lookup3(split3(x[d]), q0, q1, q2, q3, q4);
-    }
-    store_tail(out_ptr(a, K, i, r, pv.out_idx(static_cast<int>(r))) + off, y, nb);
-  }
-}
-
-// All output rows of stripe i's partial last column by one lane, rows in sequence:
-// the rows after the first re-read the same K input lines from this CU's caches
-// instead of HBM (rolled, so the main loop's VGPR budget is untouched).
-template <int K, int M, int E, bool PER_STRIPE>
-__device__ __forceinline__ void tail_stripe(const KernelArgs& a, uint32_t i) {
-#pragma unroll 1
-  for (uint32_t r = 0; r < static_cast<uint32_t>(E); ++r) tail_task<K, M, PER_STRIPE>(a, i, r);
-}
-
-template <int K, int M, bool PER_STRIPE>
-__global__ __launch_bounds__(64) void tail_kernel(const KernelArgs a) {
-  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
-  if (i < a.n_stripes) tail_task<K, M, PER_STRIPE>(a, i, blockIdx.y);
-}
-
-// ---------------------------------------------------------------------------
 // Bitsliced encode for the fixed encode matrices of the specialised shapes.
 //
 // GF(2^8) multiplication by a constant is an 8x8 matrix over GF(2).  With 32
@@ -496,10 +399,7 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 // Inputs stream through a window of kBsWindow loads in flight: input c+W is
 // loaded once input c has been transposed, so only W inputs' raw bytes are live
 // (registers for more waves) while W 2 KiB loads per wave stay in flight.
-#ifndef RS_BS_WINDOW
-#define RS_BS_WINDOW 5
-#endif
-constexpr int kBsWindow = RS_BS_WINDOW;
+constexpr int kBsWindow = 5;  // profiles/r01_ab_bs_window_occupancy.log
 
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_fold(const uint8_t* dbase, uint64_t pitch, uint32_t off_a, uint32_t off_b,
@@ -520,26 +420,25 @@ __device__ __forceinline__ void bs_fold(const uint8_t* dbase, uint64_t pitch, ui
 
 // Task = one stripe's 2 KiB column block: lane l owns the 16 B at l*16 and at
 // 1024 + l*16 of the block in every shard (two coalesced 1 KiB wave accesses per
-// shard).  Same branch-free memory discipline as apply_kernel: invalid halves load
-// from column 0 and store to the wave's scratch line.
-#ifndef RS_BS_MIN_WAVES
-#define RS_BS_MIN_WAVES 3
-#endif
+// shard).  Same memory discipline as apply_kernel: halves past the end re-read the
+// last column and their stores are dropped; the partial column is stored
+// byte-exact in the last block's wave-uniform branch.
 template <int K, int M>
-__global__ __launch_bounds__(256, RS_BS_MIN_WAVES) void encode_bitsliced_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t bps = (a.full_cols + 127u) / 128u;
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
+  const uint32_t bps = (cols + 127u) / 128u;
   const uint32_t ntasks = a.n_stripes * bps;
-  uint8_t* const dummy = a.scratch + (wave & 255u) * 1024u + lane * 16u;
   for (uint32_t t = wave; t < ntasks; t += nwaves) {
     const uint32_t stripe = t / bps;
     const uint32_t blk = t - stripe * bps;
     const uint32_t col_a = blk * 128u + lane, col_b = col_a + 64u;
     const bool va = col_a < a.full_cols, vb = col_b < a.full_cols;
-    const uint32_t clamp = kNoSink ? (a.full_cols - 1u) * 16u : 0u;
-    const uint32_t off_a = va ? col_a * 16u : clamp, off_b = vb ? col_b * 16u : clamp;
+    const uint32_t off_a = (col_a < cols ? col_a : cols - 1u) * 16u;
+    const uint32_t off_b = (col_b < cols ? col_b : cols - 1u) * 16u;
     const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
     u32x4 xa[kBsWindow], xb[kBsWindow];
 #pragma unroll
@@ -556,16 +455,14 @@ __global__ __launch_bounds__(256, RS_BS_MIN_WAVES) void encode_bitsliced_kernel(
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
       transpose8(d);
       uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + static_cast<uint64_t>(r) * a.shard_pitch;
-      if constexpr (kNoSink) {
-        store16_or_drop(pbase, off_a, va, u32x4{d[0], d[1], d[2], d[3]});
-        store16_or_drop(pbase, off_b, vb, u32x4{d[4], d[5], d[6], d[7]});
-      } else {
-        store16(va ? pbase + off_a : dummy, u32x4{d[0], d[1], d[2], d[3]});
-        store16(vb ? pbase + off_b : dummy, u32x4{d[4], d[5], d[6], d[7]});
+      store16_or_drop(pbase, off_a, va, u32x4{d[0], d[1], d[2], d[3]});
+      store16_or_drop(pbase, off_b, vb, u32x4{d[4], d[5], d[6], d[7]});
+      if (nb != 0u && blk + 1u == bps) {  // wave-uniform: the stripe's partial column is in this task
+        store_part_or_drop(pbase, off_a, col_a == a.full_cols, u32x4{d[0], d[1], d[2], d[3]}, nb);
+        store_part_or_drop(pbase, off_b, col_b == a.full_cols, u32x4{d[4], d[5], d[6], d[7]}, nb);
       }
     }
   }
-  fused_tail<K, M, M, false>(a, wave, nwaves, lane);  // partial last column: the lookup path
 }
 
 // ---------------------------------------------------------------------------
@@ -711,19 +608,17 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src
 // ---------------------------------------------------------------------------
 // Host-side launch dispatch.
 template <int K, int M, int E>
-static const void* spec_fn(bool per_stripe, const void** tail) {
-  *tail = per_stripe ? reinterpret_cast<const void*>(&tail_kernel<K, M, true>)
-                     : reinterpret_cast<const void*>(&tail_kernel<K, M, false>);
+static const void* spec_fn(bool per_stripe) {
   return per_stripe ? reinterpret_cast<const void*>(&apply_kernel<K, M, E, true>)
                     : reinterpret_cast<const void*>(&apply_kernel<K, M, E, false>);
 }
 
 // Specialised kernels: (K, M, E) with E <= M.
-static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name, const void** tail) {
-#define RS_SPEC(KK, MM, EE)                                  \
-  if (k == KK && m == MM && e == EE) {                       \
-    *name = "apply_kernel<" #KK "," #MM "," #EE ">";         \
-    return spec_fn<KK, MM, EE>(per_stripe, tail);            \
+static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name) {
+#define RS_SPEC(KK, MM, EE)                          \
+  if (k == KK && m == MM && e == EE) {               \
+    *name = "apply_kernel<" #KK "," #MM "," #EE ">"; \
+    return spec_fn<KK, MM, EE>(per_stripe);          \
   }
   RS_SPEC(4, 2, 1) RS_SPEC(4, 2, 2)
   RS_SPEC(8, 4, 1) RS_SPEC(8, 4, 2) RS_SPEC(8, 4, 3) RS_SPEC(8, 4, 4)
@@ -731,31 +626,6 @@ static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** 
   RS_SPEC(6, 3, 1) RS_SPEC(6, 3, 2) RS_SPEC(6, 3, 3)
 #undef RS_SPEC
   return nullptr;
-}
-
-static const void* pick(const KernelArgs& a, int e, bool per_stripe, bool force_generic, bool* spec,
-                        const char** name, const void** tail) {
-  *spec = false;
-  *tail = nullptr;
-  if (!force_generic) {
-    if (const void* f = pick_spec(a.k, a.m, e, per_stripe, name, tail)) {
-      *spec = true;
-      return f;
-    }
-  }
-  *name = "apply_kernel_generic";
-  return per_stripe ? reinterpret_cast<const void*>(&apply_kernel_generic<true>)
-                    : reinterpret_cast<const void*>(&apply_kernel_generic<false>);
-}
-
-int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic) {
-  bool spec;
-  const char* name;
-  const void* tail;
-  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name, &tail);
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, 0) != hipSuccess || nb < 1) nb = 1;
-  return nb;
 }
 
 template <int K, int M>
@@ -785,50 +655,63 @@ static const void* pick_bitsliced(int k, int m, const char** name) {
   return nullptr;
 }
 
-const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
-                         hipStream_t s, bool force_generic) {
+// Grid for `waves` wave-tasks: 4 waves per workgroup, at most blocks_per_cu
+// workgroups per CU (the kernels grid-stride over the rest).
+static dim3 grid_for(uint64_t waves, uint32_t blocks_per_cu, uint32_t cu_count) {
+  const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
+  const uint64_t need = (waves + 3) / 4;
+  const uint64_t g = need < cap ? need : cap;
+  return dim3(static_cast<uint32_t>(g > 0 ? g : 1));
+}
+
+// One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
+// the dropped-store descriptors cover 2 GiB from the shard base).
+static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
+                                 uint32_t cu_count, hipStream_t s, bool force_generic) {
+  void* args[] = {const_cast<KernelArgs*>(&a)};
+  const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
+  const char* name = nullptr;
   if (a.encode_net && !per_stripe && !force_generic && e == a.m) {
-    const char* name = nullptr;
     if (const void* fn = pick_bitsliced(a.k, a.m, &name)) {
-      const uint64_t bps = (static_cast<uint64_t>(a.full_cols) + 127u) / 128u;
-      uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
-      if (a.full_cols * 16u != a.shard_len) {
-        const uint64_t tail_tasks =
-            (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * (kTailAllRows ? 1u : static_cast<uint64_t>(a.m));
-        if (tail_tasks > waves) waves = tail_tasks;
-      }
+      const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * ((cols + 127u) / 128u);
       if (waves == 0) return name;
-      const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
-      const uint64_t need = (waves + 3) / 4;
-      const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
-      void* args[] = {const_cast<KernelArgs*>(&a)};
-      if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
+      if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+        return nullptr;
       return name;
     }
   }
-  bool spec;
-  const char* name;
-  const void* tail;
-  const void* fn = pick(a, e, per_stripe, force_generic, &spec, &name, &tail);
-  const uint32_t bps = spec ? a.blocks_full : a.blocks_per_stripe;
-  const bool has_tail = spec && a.full_cols * 16u != a.shard_len;
-  uint64_t waves = static_cast<uint64_t>(a.n_stripes) * bps;
-  if (has_tail && kFusedTail) {
-    const uint64_t tail_tasks =
-        (static_cast<uint64_t>(a.n_stripes) + 63u) / 64u * (kTailAllRows ? 1u : static_cast<uint64_t>(e));
-    if (tail_tasks > waves) waves = tail_tasks;
+  const void* fn = force_generic ? nullptr : pick_spec(a.k, a.m, e, per_stripe, &name);
+  if (!fn) {
+    name = "apply_kernel_generic";
+    fn = per_stripe ? reinterpret_cast<const void*>(&apply_kernel_generic<true>)
+                    : reinterpret_cast<const void*>(&apply_kernel_generic<false>);
   }
-  if (waves > 0) {
-    const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
-    const uint64_t need = (waves + 3) / 4;
-    const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
-    void* args[] = {const_cast<KernelArgs*>(&a)};
-    if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
-  }
-  if (has_tail && !kFusedTail) {
-    void* args[] = {const_cast<KernelArgs*>(&a)};
-    const dim3 g((a.n_stripes + 63u) / 64u, static_cast<uint32_t>(e));
-    if (hipLaunchKernel(tail, g, dim3(64), args, 0, s) != hipSuccess) return nullptr;
+  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  if (waves == 0) return name;
+  if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+    return nullptr;
+  return name;
+}
+
+const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
+                         hipStream_t s, bool force_generic) {
+  if (a.shard_len <= kColumnWindow)
+    return launch_window(a, e, per_stripe, blocks_per_cu, cu_count, s, force_generic);
+  // Shards of 1 GiB or more (one huge Encode of an object of several GiB): the
+  // codec is column-wise, so columns [x, x + W) of every shard are an independent
+  // batch whose slots all start x bytes later.  Windows run in order on s.
+  const char* name = nullptr;
+  for (uint64_t x = 0; x < a.shard_len; x += kColumnWindow) {
+    KernelArgs w = a;
+    w.data += x;
+    if (w.parity) w.parity += x;
+    if (w.out) w.out += x;
+    const uint64_t len = a.shard_len - x < kColumnWindow ? a.shard_len - x : kColumnWindow;
+    w.shard_len = static_cast<uint32_t>(len);
+    w.full_cols = w.shard_len / 16u;
+    w.blocks_per_stripe = ((w.shard_len + 15u) / 16u + 63u) / 64u;
+    name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s, force_generic);
+    if (!name) return nullptr;
   }
   return name;
 }

@@ -21,6 +21,10 @@ namespace rs {
 constexpr int kMaxK = 32;
 constexpr int kMaxM = 16;
 constexpr uint32_t kPlanInvalid = 0xFFFFu;
+// Largest column range one launch covers: the kernels' dropped-store descriptors
+// span 2 GiB from a shard base, so launch_apply runs longer shards as a sequence of
+// 1 GiB column windows (the codec is column-wise).
+constexpr uint32_t kColumnWindow = 1u << 30;
 
 __host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
   return (8u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
@@ -67,9 +71,8 @@ struct KernelArgs {
   uint64_t shard_pitch;
   uint32_t shard_len;
   uint32_t n_stripes;
-  uint32_t blocks_per_stripe;  // ceil(ceil(S/16) / 64): all columns (generic kernel)
+  uint32_t blocks_per_stripe;  // ceil(ceil(S/16) / 64): 64-column blocks, a partial column included
   uint32_t full_cols;          // S / 16: full 16-B columns
-  uint32_t blocks_full;        // ceil(full_cols / 64) (specialised kernels)
   int32_t k, m;
   uint32_t full_mask;          // (1 << (k+m)) - 1
   uint32_t plan_bytes;
@@ -77,7 +80,6 @@ struct KernelArgs {
   const uint32_t* present_masks;   // PER_STRIPE: bit s = shard s present
   const uint32_t* lut;             // PER_STRIPE: missing mask -> plan index
   uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards
-  uint8_t* scratch;                // 256 KiB sink for stores that must not land
   uint8_t* out;                    // null: outputs in place (slot addresses); else the
   uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
   uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
@@ -92,7 +94,7 @@ const uint8_t* bitsliced_encode_rows(int k, int m);
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
 // e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or
-// nullptr if the launch failed.
+// nullptr if the launch failed.  Any shard_len up to 0xFFFFFFF0 (column windows).
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s, bool force_generic);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
@@ -101,6 +103,5 @@ void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_block
 // a.bad must be zeroed first (launch_verify does it on s).
 const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s,
                           bool force_generic);
-int apply_kernel_max_blocks_per_cu(const KernelArgs& a, int e, bool per_stripe, bool force_generic);
 
 }  // namespace rs

@@ -17,7 +17,7 @@ computed by the HIP kernels behind the C-ABI; this module only marshals.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Union
 
 from . import _lib
 
@@ -68,13 +68,27 @@ def _shard_array(shards: Sequence[Optional[bytearray]], S: int, fill_missing: bo
     return ptrs, lens, keep
 
 
+def _create(k: int, m: int, device: Union[int, str, Sequence[int]]) -> ctypes.c_void_p:
+    """device: an ordinal (rs_create), "all" (rs_create_multi over every visible
+    GPU) or a list of ordinals (rs_create_devices; repeats allowed)."""
+    handle = ctypes.c_void_p()
+    if isinstance(device, str):
+        if device != "all":
+            raise ValueError(f"device must be an ordinal, 'all' or a list, not {device!r}")
+        _check(_lib.lib().rs_create_multi(k, m, 0, 0, ctypes.byref(handle)))
+    elif isinstance(device, int):
+        _check(_lib.lib().rs_create(k, m, device, 0, ctypes.byref(handle)))
+    else:
+        devs = (ctypes.c_int * len(device))(*device)
+        _check(_lib.lib().rs_create_devices(k, m, devs, len(device), 0, ctypes.byref(handle)))
+    return handle
+
+
 class Service:
     """IEcDriver implementation on the MI355X engine (internal/ec/ec.go:15-17)."""
 
-    def __init__(self, k: int = K, m: int = M, device: int = 0):
-        handle = ctypes.c_void_p()
-        _check(_lib.lib().rs_create(k, m, device, 0, ctypes.byref(handle)))
-        self._ctx = handle
+    def __init__(self, k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0):
+        self._ctx = _create(k, m, device)
         self.k, self.m = k, m
 
     def close(self) -> None:
@@ -94,6 +108,11 @@ class Service:
 
     def backend(self) -> str:
         return _lib.lib().rs_backend(self._ctx).decode()
+
+    def devices(self) -> List[int]:
+        """HIP ordinals of the context's engines (one per GPU, or repeats)."""
+        L = _lib.lib()
+        return [L.rs_device_at(self._ctx, i) for i in range(L.rs_device_count(self._ctx))]
 
     def encode_matrix(self) -> List[List[int]]:
         t = self.k + self.m
@@ -155,6 +174,7 @@ class Service:
         return bool(ok.value)
 
 
-def NewService(k: int = K, m: int = M, device: int = 0) -> Service:
-    """internal/ec/ec.go:21 NewService(): RS(K=4, M=2) on the GPU engine."""
+def NewService(k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0) -> Service:
+    """internal/ec/ec.go:21 NewService(): RS(K=4, M=2) on the GPU engine
+    (device="all": one driver over every GPU of the node, as the Go shim builds it)."""
     return Service(k, m, device)
