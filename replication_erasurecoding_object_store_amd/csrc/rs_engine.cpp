@@ -134,18 +134,26 @@ void perm_tables(uint8_t f, uint32_t* t) {
   t[4] = pack4(0, 6);
 }
 
-// rows: n_out x k coefficient matrix (row-major).
-std::vector<uint8_t> make_plan(int k, int m, const std::vector<int>& in_idx, const std::vector<int>& out_idx,
-                               const std::vector<uint8_t>& rows) {
+// rows: n_out x k coefficient matrix (row-major); in_idx = the first k shards of
+// `present`, out_idx = the shards of `out_mask` missing from it (both in index order:
+// the kernels re-derive them from the masks).
+std::vector<uint8_t> make_plan(int k, int m, uint32_t present, uint32_t out_mask, const std::vector<int>& in_idx,
+                               const std::vector<int>& out_idx, const std::vector<uint8_t>& rows) {
   std::vector<uint8_t> p(rs::plan_stride(k, m), 0);
-  const uint32_t n_out = static_cast<uint32_t>(out_idx.size());
-  std::memcpy(p.data(), &n_out, 4);
-  uint32_t* ii = reinterpret_cast<uint32_t*>(p.data() + 8);
+  const uint32_t hdr[4] = {static_cast<uint32_t>(out_idx.size()), present, out_mask, 0u};
+  std::memcpy(p.data(), hdr, sizeof(hdr));
+  uint32_t* ii = reinterpret_cast<uint32_t*>(p.data() + 16);
   for (int c = 0; c < k; ++c) ii[c] = static_cast<uint32_t>(in_idx[c]);
   for (size_t r = 0; r < out_idx.size(); ++r) ii[k + r] = static_cast<uint32_t>(out_idx[r]);
-  uint32_t* tab = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
+  uint32_t* quad = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
+  uint32_t* c4 = reinterpret_cast<uint32_t*>(p.data() + rs::plan_c4_offset(k, m));
   for (size_t r = 0; r < out_idx.size(); ++r)
-    for (int c = 0; c < k; ++c) perm_tables(rows[r * k + c], tab + (r * k + c) * 5);
+    for (int c = 0; c < k; ++c) {
+      uint32_t t[5];
+      perm_tables(rows[r * k + c], t);
+      std::memcpy(quad + (r * k + c) * 4, t, 16);
+      c4[r * k + c] = t[4];
+    }
   return p;
 }
 
@@ -184,7 +192,9 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
       rows[r * k + c] = v;
     }
   }
-  *out = make_plan(k, m, surv, miss, rows);
+  const uint32_t full = static_cast<uint32_t>((t >= 32) ? ~0ull : ((1ull << t) - 1));
+  const uint32_t data = static_cast<uint32_t>((1ull << k) - 1);
+  *out = make_plan(k, m, static_cast<uint32_t>(present) & full, data_only ? data : full, surv, miss, rows);
   return RS_OK;
 }
 
@@ -879,7 +889,8 @@ PlanSet build_plans(rs_ctx* c) {
     std::vector<uint8_t> rows(static_cast<size_t>(m) * k);
     for (int p = 0; p < m; ++p)
       for (int i = 0; i < k; ++i) rows[p * k + i] = c->enc.at(k + p, i);
-    ps.enc_plan = make_plan(k, m, in_idx, out_idx, rows);
+    ps.enc_plan = make_plan(k, m, static_cast<uint32_t>((1ull << k) - 1), static_cast<uint32_t>(full_mask64(t)),
+                            in_idx, out_idx, rows);
   }
   // Eager all-pattern plans + LUT for k+m <= 16.  Plan 0 = nothing missing.
   if (t <= 16 && m > 0) {
@@ -888,7 +899,7 @@ PlanSet build_plans(rs_ctx* c) {
     {
       std::vector<int> in_idx(k), none;
       for (int i = 0; i < k; ++i) in_idx[i] = i;
-      std::vector<uint8_t> p = make_plan(k, m, in_idx, none, {});
+      std::vector<uint8_t> p = make_plan(k, m, full, full, in_idx, none, {});
       ps.all_plans.insert(ps.all_plans.end(), p.begin(), p.end());
       c->h_lut[0] = 0;
     }

@@ -8,9 +8,15 @@
 //                  shard (data then parity, index order), C = composed decode rows
 //                  ([upstream reedsolomon.go reconstruct] phases 1+2 folded).
 // Byte layout (plan_bytes = plan_stride(K, M), 16-B aligned):
-//   u32 n_out; u32 reserved; u32 in_idx[K]; u32 out_idx[M]; pad to 16;
-//   u32 tab[M][K][5]   -- per coefficient f: 3-chunk v_perm tables
-//                         {A_lo, A_hi, B_lo, B_hi, C_lo} (see rs_kernels.hip).
+//   u32 n_out; u32 present; u32 out_mask; u32 reserved; u32 in_idx[K]; u32 out_idx[M];
+//   pad to 16;   (present: the shards the plan reads from; out_mask: the shards it
+//                 may fill -- all, or the data shards for ReconstructData)
+//   u32x4 quad[M][K]  -- per coefficient f: 3-chunk v_perm tables {A_lo, A_hi, B_lo,
+//                        B_hi} (see rs_kernels.hip), 16-B aligned for ds_read_b128
+//   u32   c4[M][K]    -- per coefficient f: C_lo
+// The kernels derive the input / output slots from the present mask itself (first
+// K present in index order / every missing one), which is exactly how these plans
+// are built; in_idx / out_idx are kept for the generic kernel and for checks.
 #pragma once
 
 #include <stdint.h>
@@ -27,11 +33,13 @@ constexpr uint32_t kPlanInvalid = 0xFFFFu;
 constexpr uint32_t kColumnWindow = 1u << 30;
 
 __host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
-  return (8u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
+  return (16u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
+}
+__host__ __device__ constexpr uint32_t plan_c4_offset(int k, int m) {
+  return plan_tab_offset(k, m) + 16u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m);
 }
 __host__ __device__ constexpr uint32_t plan_stride(int k, int m) {
-  return (plan_tab_offset(k, m) + 20u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) &
-         ~15u;
+  return (plan_c4_offset(k, m) + 4u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) & ~15u;
 }
 
 // Plans, masks and LUT are written by the host before a launch and never by a
@@ -52,11 +60,15 @@ struct PlanView {
   int k, m;
   __host__ __device__ PlanView(const uint8_t* plan, int kk, int mm) : p(plan), k(kk), m(mm) {}
   __host__ __device__ uint32_t n_out() const { return *as_const<uint32_t>(p); }
-  __host__ __device__ uint32_t in_idx(int c) const { return as_const<uint32_t>(p + 8)[c]; }
-  __host__ __device__ uint32_t out_idx(int r) const { return as_const<uint32_t>(p + 8 + 4 * k)[r]; }
-  __host__ __device__ const RS_CONST uint32_t* tab(int r, int c) const {
-    return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (r * k + c) * 5;
+  __host__ __device__ uint32_t present() const { return as_const<uint32_t>(p)[1]; }
+  __host__ __device__ uint32_t out_mask() const { return as_const<uint32_t>(p)[2]; }
+  __host__ __device__ uint32_t in_idx(int c) const { return as_const<uint32_t>(p + 16)[c]; }
+  __host__ __device__ uint32_t out_idx(int r) const { return as_const<uint32_t>(p + 16 + 4 * k)[r]; }
+  // the five table dwords of coefficient (r, c): quad(r, c)[0..3] and c4(r, c)
+  __host__ __device__ const RS_CONST uint32_t* quad(int r, int c) const {
+    return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (r * k + c) * 4;
   }
+  __host__ __device__ uint32_t c4(int r, int c) const { return as_const<uint32_t>(p + plan_c4_offset(k, m))[r * k + c]; }
 };
 
 // Shard slot s of stripe i lives at

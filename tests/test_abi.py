@@ -71,6 +71,27 @@ def test_create_argument_checks_before_device():
     assert L.rs_create(40, 4, 0, 0, ctypes.byref(h)) == _lib.RS_ERR_NOT_SUPPORTED
 
 
+def test_multi_device_creation_checks():
+    """rs_create_multi / rs_create_devices: klauspost's argument checks first, then
+    devices; without a GPU (or with a bad ordinal) RS_ERR_NO_DEVICE."""
+    import torch
+
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.rs_create_multi(0, 2, 0, 0, ctypes.byref(h)) == _lib.RS_ERR_INV_SHARD_NUM
+    assert L.rs_create_multi(200, 100, 0, 0, ctypes.byref(h)) == _lib.RS_ERR_MAX_SHARD_NUM
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert L.rs_create_devices(4, -1, devs, 2, 0, ctypes.byref(h)) == _lib.RS_ERR_INV_SHARD_NUM
+    assert L.rs_create_devices(4, 2, devs, 0, 0, ctypes.byref(h)) == _lib.RS_ERR_INVALID_ARG
+    bad = (ctypes.c_int * 1)(63)
+    assert L.rs_create_devices(4, 2, bad, 1, 0, ctypes.byref(h)) == _lib.RS_ERR_NO_DEVICE
+    if not torch.cuda.is_available():
+        assert L.rs_create_multi(4, 2, 0, 0, ctypes.byref(h)) == _lib.RS_ERR_NO_DEVICE
+        assert L.rs_create_devices(4, 2, devs, 2, 0, ctypes.byref(h)) == _lib.RS_ERR_NO_DEVICE
+    assert not h.value
+    assert L.rs_device_count(None) == 0 and L.rs_device_at(None, 0) == -1
+
+
 def test_no_gpu_fails_loudly():
     import torch
 

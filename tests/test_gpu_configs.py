@@ -1,0 +1,145 @@
+"""BASELINE.json's configs through the drop-in, each checked against the CPU oracle.
+
+configs[0]  one 1 MiB object (xoshiro256**, seed 0x5EED0001) through internal/ec:
+            Split + Encode as writeservice.go:218-222 calls them, Reconstruct as
+            readservice.go:285 does -- parity pinned by tests/golden/kat.json.
+configs[1/2] 65 536 x 4 KiB RS(4+2) encode / 1- and 2-erasure reconstruct:
+            test_gpu_parity.py::test_config2_full_size_roundtrip.
+configs[3]  RS(4+2), RS(8+4), RS(10+4) at 64 KiB stripes, 16 384 stripes (one GPU's
+            share of the K/M sweep): oracle on sampled stripes, round trip on all.
+configs[4]  healer repair mix: 1 M objects x 4 KiB RS(4+2), 50/50 encode and
+            1-erasure repair (seed 0x5EED0005), shards in pinned host memory, one
+            batched call (cmd/healer/poller.go:282 per object in the reference).
+"""
+import hashlib
+import itertools
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rs_oracle
+from replication_erasurecoding_object_store_amd.batch import BatchEngine, shard_pitch_for
+from replication_erasurecoding_object_store_amd.ec import NewService
+from replication_erasurecoding_object_store_amd.xoshiro import xoshiro_bytes
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+
+KAT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kat.json")
+
+
+def test_config1_dropin_split_encode_reconstruct(gpu):
+    c = json.load(open(KAT))["config1"]
+    data = xoshiro_bytes(c["seed"], c["len"])
+    assert hashlib.sha256(data).hexdigest() == c["data_sha256"]
+    svc = NewService()  # internal/ec/ec.go:21: RS(config.K=4, config.M=2)
+    try:
+        shards = svc.Split(data)  # writeservice.go:218
+        assert [len(s) for s in shards] == [c["shard_len"]] * 6
+        svc.Encode(shards)  # writeservice.go:222
+        assert [hashlib.sha256(bytes(s)).hexdigest() for s in shards[4:]] == c["parity_sha256"]
+        assert b"".join(bytes(s) for s in shards[:4])[:len(data)] == data
+        assert svc.Verify(shards)
+        # degraded reads (readservice.go:285): any 1 or 2 lost shards come back
+        for lost in [c for e in (1, 2) for c in itertools.combinations(range(6), e)]:
+            got = [None if i in lost else bytearray(s) for i, s in enumerate(shards)]
+            svc.Reconstruct(got)
+            assert all(bytes(g) == bytes(s) for g, s in zip(got, shards)), lost
+    finally:
+        svc.close()
+
+
+def _two_erasure_masks(rng, n, t):
+    pairs = np.array(list(itertools.combinations(range(t), 2)))
+    ch = pairs[rng.integers(0, len(pairs), n)]
+    return (((1 << t) - 1) & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))).astype(np.uint32)
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (8, 4), (10, 4)])
+def test_config4_kmsweep_64KiB(gpu, k, m):
+    import torch
+
+    S, N = -(-65536 // k), 16384  # 16 384 / 8 192 / 6 554 (4 B pad at RS(10+4))
+    t, P = k + m, shard_pitch_for(S)
+    eng = BatchEngine(k, m, 0)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(0x5EED0004 + k)
+        data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+        parity = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+        eng.encode(data, parity, S, N)
+        torch.cuda.synchronize()
+        assert (parity[:, :, S:] == 0xC3).all(), "encode writes exactly S bytes per parity shard"
+        # oracle on sampled stripes (first, last, random)
+        rng = np.random.default_rng(k * 31 + m)
+        idx = np.unique(np.concatenate([[0, N - 1], rng.choice(N, 62, replace=False)]))
+        it = torch.from_numpy(idx).cuda()
+        d_s = data[it, :, :S].cpu().numpy()
+        p_s = parity[it, :, :S].cpu().numpy()
+        buf = np.zeros((len(idx), t, S), np.uint8)
+        buf[:, :k] = d_s
+        rs_oracle.encode_batch_scalar(k, m, buf.reshape(-1), t * S, S, S, len(idx))
+        assert np.array_equal(p_s, buf[:, k:])
+        # per-stripe 2-erasure reconstruct, out of place, device masks (the bench path)
+        masks = _two_erasure_masks(np.random.default_rng(0x5EED0003), N, t)
+        out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+        eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
+        eng.sync()
+        full = torch.cat([data[:, :, :S], parity[:, :, :S]], dim=1)
+        lost = torch.from_numpy(((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0).cuda()
+        assert torch.equal(out[:, :2, :S], full[lost].view(N, 2, S)), "round trip on every stripe"
+        assert (out[:, :, S:] == 0xC3).all() and (out[:, 2:] == 0xC3).all()
+        # the oracle's own decode on sampled stripes
+        o_s = out[it, :2, :S].cpu().numpy()
+        for j, i in enumerate(idx[:24]):
+            sh = [bytearray(buf[j, s].tobytes()) if (masks[i] >> s) & 1 else None for s in range(t)]
+            assert rs_oracle.reconstruct(k, m, sh) == 0
+            miss = [s for s in range(t) if not (masks[i] >> s) & 1]
+            for r, s in enumerate(miss):
+                assert bytes(sh[s]) == o_s[j, r].tobytes(), (i, s)
+    finally:
+        eng.close()
+
+
+def test_config5_healer_mix_pinned_host(gpu):
+    import torch
+
+    k, m, S, N = 4, 2, 1024, 1 << 20
+    t, full = k + m, (1 << (k + m)) - 1
+    eng = BatchEngine(k, m, 0)
+    try:
+        rng = np.random.default_rng(0x5EED0005)
+        is_rec = rng.random(N) < 0.5
+        lost = rng.integers(0, t, N)
+        # encode = "all parity missing"; repair = one lost shard anywhere
+        masks = np.where(is_rec, full & ~(1 << lost), (1 << k) - 1).astype(np.uint32)
+        data = torch.empty((N, k, S), dtype=torch.uint8, pin_memory=True)
+        parity = torch.empty((N, m, S), dtype=torch.uint8, pin_memory=True)
+        g = torch.Generator(device="cuda").manual_seed(0x5EED0005)
+        d_true = torch.randint(0, 256, (N, k, S), dtype=torch.uint8, device="cuda", generator=g)
+        p_true = torch.empty((N, m, S), dtype=torch.uint8, device="cuda")
+        eng.encode(d_true, p_true, S, N)
+        torch.cuda.synchronize()
+        # the device truth itself against the oracle on a sample
+        sample = np.sort(rng.choice(N, 256, replace=False))
+        st = torch.from_numpy(sample).cuda()
+        buf = np.concatenate([d_true[st].cpu().numpy(), p_true[st].cpu().numpy()], axis=1)
+        ref = buf.copy()
+        ref[:, k:] = 0
+        rs_oracle.encode_batch_scalar(k, m, ref.reshape(-1), t * S, S, S, len(sample))
+        assert np.array_equal(ref, buf)
+        dn, pn = data.numpy(), parity.numpy()
+        lost_d = ((~masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
+        lost_p = ((~masks[:, None] >> np.arange(k, t)[None, :]) & 1).astype(bool)
+        for zc in (True, False):
+            eng.set_host_zero_copy(zc)
+            data.copy_(d_true)
+            parity.copy_(p_true)
+            dn[lost_d] = 0
+            pn[lost_p] = 0
+            eng.reconstruct_host(dn, pn, S, N, masks)
+            assert eng.last_host_path() == ("zero-copy" if zc else "staged")
+            assert torch.equal(data.cuda(), d_true) and torch.equal(parity.cuda(), p_true), zc
+        eng.set_host_zero_copy(True)
+    finally:
+        eng.close()

@@ -1,0 +1,55 @@
+"""Shards of 2 GiB and more (the kernels' dropped-store descriptors span
+2 GiB from a shard base, so a single launch could silently drop stores past it).
+The reference passes whole objects to Split/Encode (writeservice.go:218-222): an
+8 GiB object at RS(4+2) has 2 GiB shards.  launch_apply runs such shards as 1 GiB
+column windows; RS is column-wise, so any column slice of the data shards encodes
+to the same column slice of the parity, which the oracle checks around every
+window boundary and at the partial last column."""
+import numpy as np
+import pytest
+
+from oracle import rs_oracle
+from replication_erasurecoding_object_store_amd.batch import BatchEngine, shard_pitch_for
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
+
+
+def _oracle_cols(k, m, data_cols):
+    """parity of a [k, n] column slice."""
+    n = data_cols.shape[1]
+    buf = np.zeros((1, k + m, n), np.uint8)
+    buf[0, :k] = data_cols
+    rs_oracle.encode_batch_scalar(k, m, buf.reshape(-1), (k + m) * n, n, n, 1)
+    return buf[0, k:]
+
+
+def test_encode_and_reconstruct_past_2GiB_shards(gpu):
+    import torch
+
+    k, m = 4, 2
+    S = (1 << 31) + 4096 + 5  # past 2 GiB, partial last column
+    P = shard_pitch_for(S)
+    eng = BatchEngine(k, m, 0)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(0x5EED0042)
+        data = torch.randint(0, 256, (1, k, P), dtype=torch.uint8, device="cuda", generator=g)
+        parity = torch.full((1, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+        eng.encode(data, parity, S, 1)
+        torch.cuda.synchronize()
+        assert (parity[0, :, S:] == 0xC3).all(), "nothing written past S"
+        W = 1 << 30
+        windows = [(0, 64), (W - 48, W + 48), (2 * W - 48, 2 * W + 48), (S - 70, S)]
+        for lo, hi in windows:
+            want = _oracle_cols(k, m, data[0, :, lo:hi].cpu().numpy())
+            assert np.array_equal(parity[0, :, lo:hi].cpu().numpy(), want), (lo, hi)
+        # 2-erasure reconstruct, out of place: data shard 1 and parity shard 5 lost
+        out = torch.full((1, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+        eng.reconstruct_out(data, parity, out, S, 1, present_masks=0b011101)
+        torch.cuda.synchronize()
+        for lo, hi in windows:
+            assert torch.equal(out[0, 0, lo:hi], data[0, 1, lo:hi]), (lo, hi)
+            assert torch.equal(out[0, 1, lo:hi], parity[0, 1, lo:hi]), (lo, hi)
+        assert torch.equal(out[0, 0, :S], data[0, 1, :S]) and torch.equal(out[0, 1, :S], parity[0, 1, :S])
+        assert (out[0, :, S:] == 0xC3).all()
+    finally:
+        eng.close()

@@ -44,13 +44,19 @@ WORKLOADS = {
     "rs104_S6656_rec1p_out": (10, 4, 6656, 16384, "rec1p_out"),
     "rs104_S6656_rec2p_out": (10, 4, 6656, 16384, "rec2p_out"),
     "rs104_S6144_enc": (10, 4, 6144, 16384, "enc"),
+    # diagnostics: plan working set (one pattern for every stripe vs random), E
+    "rs104_64K_rec01p_out": (10, 4, 6554, 16384, "rec01p_out"),    # devmask, all stripes miss {0,1}
+    "rs104_64K_rec2u_out": (10, 4, 6554, 16384, "rec2u_out"),      # uniform host mask {0,1}
+    "rs104_64K_rec2ph_out": (10, 4, 6554, 16384, "rec2ph_out"),    # per-stripe host masks -> E=2 kernel
+    "rs104_64K_encu_out": (10, 4, 6554, 16384, "encu_out"),        # lookup encode (uniform data-only mask)
+    "rs84_64K_encu_out": (8, 4, 8192, 16384, "encu_out"),
 }
 
 
 def alg_bytes(name):
     """Algorithmic HBM bytes of one launch of workload `name`."""
     k, m, S, N, mode = WORKLOADS[name]
-    e = {"enc": m, "ver": m, "rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
+    e = {"enc": m, "ver": m, "encu_out": m, "rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
     return N * S * (k + e)
 
 
@@ -106,6 +112,7 @@ def main():
                          for _ in range(N)], np.uint32)
         masks4 = torch.from_numpy(four.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
+        m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
         outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
         alg = alg_bytes(name.split("+")[0])
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
@@ -130,6 +137,12 @@ def main():
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks4)
             elif mode == "rec2p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
+            elif mode == "rec01p_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=m01)
+            elif mode == "rec2ph_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=masks_np[i % nb])
+            elif mode == "encu_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=(1 << k) - 1)
             elif mode == "rec2u_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=((1 << t) - 1) & ~3)
             else:

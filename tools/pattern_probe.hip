@@ -1,0 +1,463 @@
+// pattern_probe.hip -- compute-free ceilings of the RS kernels' HBM access patterns
+// (split layout: data [N, K, P], parity [N, M, P]), to separate memory-pattern
+// limits from compute / issue limits.  Every kernel reads K shards and writes M
+// per stripe with a trivial dependence (y = x[r] ^ x[c]*(r+1)) so no load is dead.
+//
+//   A  1 KiB tasks (64 columns x 16 B), all K loads then M stores, plain stores
+//      behind `if (col < cols)` (round-1 hbm_probe4 shape)
+//   B  as A, stores as raw buffer stores dropped by offset for lanes past the end
+//      (apply_kernel's discipline), lanes past the end re-read the last column
+//   C  2 KiB tasks (columns c and c+64 per lane), buffer stores (bitsliced shape)
+//   D  as B, software-pipelined: task t+1's K loads are issued before task t's
+//      stores (two register sets, loop unrolled by 2)
+//   E  as B but one task = the whole stripe (loop over its blocks inside the wave)
+//   copy: streaming copy of 1 GiB, U loads in flight per lane, G blocks per CU
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/pattern_probe tools/pattern_probe.hip
+// Run:   tools/pattern_probe   (prints GB/s of algorithmic bytes N*S*(K+M))
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define CHECK(x)                                                         \
+  do {                                                                   \
+    hipError_t e_ = (x);                                                 \
+    if (e_ != hipSuccess) {                                              \
+      std::printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); \
+      std::exit(1);                                                      \
+    }                                                                    \
+  } while (0)
+
+struct Geo {
+  const uint8_t* d;
+  uint8_t* p;
+  uint32_t N, S, P, cols, full;  // cols = ceil(S/16), full = S/16
+};
+
+__device__ __forceinline__ u32x4 ld(const uint8_t* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)); }
+
+__device__ __forceinline__ const uint8_t* uni(const uint8_t* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ void st_drop(uint8_t* base, uint32_t off, bool live, u32x4 v) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uni(base)), 0, 0x7FFFFFFF, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, live ? off : 0x80000000u, 0, 2);
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void pA(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t s = t / bps, b = t - s * bps, col = b * 64 + lane;
+    if (col >= g.cols) continue;
+    const uint8_t* ip = g.d + (uint64_t)s * K * g.P + col * 16;
+    uint8_t* op = g.p + (uint64_t)s * M * g.P + col * 16;
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = ld(ip + (uint64_t)c * g.P);
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      u32x4 y = x[r];
+#pragma unroll
+      for (int c = 0; c < K; ++c) y ^= x[c] * (r + 1);
+      __builtin_nontemporal_store(y, reinterpret_cast<u32x4*>(op + (uint64_t)r * g.P));
+    }
+  }
+}
+
+template <int K, int M>
+__device__ __forceinline__ void task_load(const Geo& g, uint32_t s, uint32_t col, u32x4 (&x)[K], uint32_t* off) {
+  *off = (col < g.cols ? col : g.cols - 1) * 16;
+  const uint8_t* ip = uni(g.d + (uint64_t)s * K * g.P);
+#pragma unroll
+  for (int c = 0; c < K; ++c) x[c] = ld(ip + (uint64_t)c * g.P + *off);
+}
+
+template <int K, int M>
+__device__ __forceinline__ void task_store(const Geo& g, uint32_t s, uint32_t col, uint32_t off, const u32x4 (&x)[K]) {
+  uint8_t* ob = g.p + (uint64_t)s * M * g.P;
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    u32x4 y = x[r];
+#pragma unroll
+    for (int c = 0; c < K; ++c) y ^= x[c] * (r + 1);
+    st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y);
+  }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void pB(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t s = t / bps, b = t - s * bps, col = b * 64 + lane;
+    u32x4 x[K];
+    uint32_t off;
+    task_load<K, M>(g, s, col, x, &off);
+    task_store<K, M>(g, s, col, off, x);
+  }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void pC(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 127) / 128, tasks = g.N * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t s = t / bps, b = t - s * bps, ca = b * 128 + lane, cb = ca + 64;
+    u32x4 xa[K], xb[K];
+    uint32_t oa, ob;
+    task_load<K, M>(g, s, ca, xa, &oa);
+    task_load<K, M>(g, s, cb, xb, &ob);
+    task_store<K, M>(g, s, ca, oa, xa);
+    task_store<K, M>(g, s, cb, ob, xb);
+  }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void pD(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  u32x4 xa[K], xb[K];
+  uint32_t oa = 0, ob = 0, sa = 0, sb = 0, ca = 0, cb = 0;
+  uint32_t t = wave;
+  if (t < tasks) {
+    sa = t / bps;
+    ca = (t - sa * bps) * 64 + lane;
+    task_load<K, M>(g, sa, ca, xa, &oa);
+  }
+  while (t < tasks) {
+    const uint32_t t1 = t + nw;
+    if (t1 < tasks) {
+      sb = t1 / bps;
+      cb = (t1 - sb * bps) * 64 + lane;
+      task_load<K, M>(g, sb, cb, xb, &ob);
+    }
+    task_store<K, M>(g, sa, ca, oa, xa);
+    if (t1 >= tasks) break;
+    const uint32_t t2 = t1 + nw;
+    if (t2 < tasks) {
+      sa = t2 / bps;
+      ca = (t2 - sa * bps) * 64 + lane;
+      task_load<K, M>(g, sa, ca, xa, &oa);
+    }
+    task_store<K, M>(g, sb, cb, ob, xb);
+    t = t2;
+  }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256) void pE(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64;
+  for (uint32_t s = wave; s < g.N; s += nw) {
+    for (uint32_t b = 0; b < bps; ++b) {
+      const uint32_t col = b * 64 + lane;
+      u32x4 x[K];
+      uint32_t off;
+      task_load<K, M>(g, s, col, x, &off);
+      task_store<K, M>(g, s, col, off, x);
+    }
+  }
+}
+
+// ---- the same patterns with the engine's GF(2^8) lookup arithmetic ----------------
+// E outputs x K inputs, 3 v_perm + 1.5 v_bitop3 per product (rs_kernels.hip), the
+// coefficient tables wave-uniform (kernel argument -> SGPRs).
+struct Tabs {
+  const uint32_t* t;  // device array of 4*10*5 table dwords
+};
+
+static float time_it(void (*launch)(void*), void* arg, int iters);
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+template <int K, int E>
+__device__ __forceinline__ void gf_compute(const Tabs& tb0, const u32x4 (&x)[K], u32x4 (&y)[E]) {
+  u32x4 pend[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) y[r] = u32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    uint32_t ia[4], ib[4], ic[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      ia[d] = x[c][d] & 0x07070707u;
+      ib[d] = (x[c][d] >> 3) & 0x07070707u;
+      ic[d] = (x[c][d] >> 6) & 0x03030303u;
+    }
+    // tables re-read (scalar cache) per input, as rs_kernels.hip does: an opaque
+    // pointer per input keeps the compiler from hoisting 200 dwords into SGPRs
+    const uint32_t* tp = tb0.t;
+    asm volatile("" : "+s"(tp));
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const __attribute__((address_space(4))) uint32_t* q =
+          (const __attribute__((address_space(4))) uint32_t*)(tp) + (r * K + c) * 5;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t prod = x3(__builtin_amdgcn_perm(q[1], q[0], ia[d]), __builtin_amdgcn_perm(q[3], q[2], ib[d]),
+                                 __builtin_amdgcn_perm(0u, q[4], ic[d]));
+        if (c & 1)
+          y[r][d] = x3(y[r][d], pend[r][d], prod);
+        else if (c == K - 1)
+          y[r][d] ^= prod;
+        else
+          pend[r][d] = prod;
+      }
+    }
+  }
+}
+
+template <int K, int M, int E>
+__device__ __forceinline__ void gf_store(const Geo& g, const Tabs& tb, uint32_t s, uint32_t col, uint32_t off,
+                                         const u32x4 (&x)[K]) {
+  u32x4 y[E];
+  gf_compute<K, E>(tb, x, y);
+  uint8_t* ob = g.p + (uint64_t)s * M * g.P;
+#pragma unroll
+  for (int r = 0; r < E; ++r) st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y[r]);
+}
+
+template <int K, int M, int E>
+__global__ __launch_bounds__(256) void cB(Geo g, Tabs tb) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t s = t / bps, b = t - s * bps, col = b * 64 + lane;
+    u32x4 x[K];
+    uint32_t off;
+    task_load<K, M>(g, s, col, x, &off);
+    gf_store<K, M, E>(g, tb, s, col, off, x);
+  }
+}
+
+template <int K, int M, int E>
+__global__ __launch_bounds__(256) void cD(Geo g, Tabs tb) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  u32x4 xa[K], xb[K];
+  uint32_t oa = 0, ob = 0, sa = 0, sb = 0, ca = 0, cb = 0;
+  uint32_t t = wave;
+  if (t < tasks) {
+    sa = t / bps;
+    ca = (t - sa * bps) * 64 + lane;
+    task_load<K, M>(g, sa, ca, xa, &oa);
+  }
+  while (t < tasks) {
+    const uint32_t t1 = t + nw;
+    if (t1 < tasks) {
+      sb = t1 / bps;
+      cb = (t1 - sb * bps) * 64 + lane;
+      task_load<K, M>(g, sb, cb, xb, &ob);
+    }
+    gf_store<K, M, E>(g, tb, sa, ca, oa, xa);
+    if (t1 >= tasks) break;
+    const uint32_t t2 = t1 + nw;
+    if (t2 < tasks) {
+      sa = t2 / bps;
+      ca = (t2 - sa * bps) * 64 + lane;
+      task_load<K, M>(g, sa, ca, xa, &oa);
+    }
+    gf_store<K, M, E>(g, tb, sb, cb, ob, xb);
+    t = t2;
+  }
+}
+
+struct CRun {
+  const void* fn;
+  Geo g[2];
+  Tabs tb;
+  uint32_t grid;
+  int i;
+};
+
+static void launch_crun(void* a) {
+  CRun* r = static_cast<CRun*>(a);
+  Geo g = r->g[r->i++ & 1];
+  void* args[] = {&g, &r->tb};
+  CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, 0, nullptr));
+}
+
+template <int K, int M, int E>
+static void compute_geometry(int cus, uint32_t S, uint32_t N) {
+  const uint32_t P = (S + 255) / 256 * 256;
+  Geo g[2];
+  for (auto& x : g) {
+    uint8_t *d, *p;
+    CHECK(hipMalloc(&d, (size_t)N * K * P));
+    CHECK(hipMalloc(&p, (size_t)N * M * P));
+    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+  }
+  std::vector<uint32_t> ht(200);
+  for (int i = 0; i < 200; ++i) ht[i] = 0x01020304u * (i + 1);
+  uint32_t* dt;
+  CHECK(hipMalloc(&dt, 800));
+  CHECK(hipMemcpy(dt, ht.data(), 800, hipMemcpyHostToDevice));
+  Tabs tb{dt};
+  const double alg = (double)N * S * (K + E);
+  struct V {
+    const char* name;
+    const void* fn;
+  } vs[] = {{"B+gf  1KiB", (const void*)&cB<K, M, E>}, {"D+gf pipelined", (const void*)&cD<K, M, E>}};
+  for (auto& v : vs) {
+    for (int bpc : {1, 2, 3, 4, 6}) {
+      CRun r{v.fn, {g[0], g[1]}, tb, (uint32_t)(cus * bpc), 0};
+      const float ms = time_it(launch_crun, &r, 10);
+      std::printf("RS(%d+%d) E=%d S=%u  %-16s bpc=%d  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", K, M, E, S, v.name, bpc,
+                  alg / ms / 1e6, alg / ms / 1e6 / 80.0);
+    }
+  }
+  for (auto& x : g) {
+    CHECK(hipFree(const_cast<uint8_t*>(x.d)));
+    CHECK(hipFree(x.p));
+  }
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void copyk(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base < n16; base += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * 256 < n16) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * 256 < n16) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+  }
+}
+
+static float time_it(void (*launch)(void*), void* arg, int iters) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int i = 0; i < 2; ++i) launch(arg);
+  CHECK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) launch(arg);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
+  return ms / iters;
+}
+
+struct Run {
+  const void* fn;
+  Geo g[2];
+  uint32_t grid;
+  int i;
+};
+
+static void launch_run(void* a) {
+  Run* r = static_cast<Run*>(a);
+  Geo g = r->g[r->i++ & 1];
+  void* args[] = {&g};
+  CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, 0, nullptr));
+}
+
+template <int K, int M>
+static void geometry(int cus, uint32_t S, uint32_t N) {
+  const uint32_t P = (S + 255) / 256 * 256;
+  Geo g[2];
+  for (auto& x : g) {
+    uint8_t *d, *p;
+    CHECK(hipMalloc(&d, (size_t)N * K * P));
+    CHECK(hipMalloc(&p, (size_t)N * M * P));
+    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+  }
+  const double alg = (double)N * S * (K + M);
+  struct V {
+    const char* name;
+    const void* fn;
+  } vs[] = {{"A plain-if 1KiB", (const void*)&pA<K, M>},
+            {"B bufdrop 1KiB", (const void*)&pB<K, M>},
+            {"C bufdrop 2KiB", (const void*)&pC<K, M>},
+            {"D pipelined 1KiB", (const void*)&pD<K, M>},
+            {"E stripe-per-wave", (const void*)&pE<K, M>}};
+  for (auto& v : vs) {
+    for (int bpc : {2, 4, 8}) {
+      Run r{v.fn, {g[0], g[1]}, (uint32_t)(cus * bpc), 0};
+      const float ms = time_it(launch_run, &r, 10);
+      std::printf("RS(%d+%d) S=%u P=%u  %-18s bpc=%d  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", K, M, S, P, v.name, bpc,
+                  alg / ms / 1e6, alg / ms / 1e6 / 80.0);
+    }
+  }
+  for (auto& x : g) {
+    CHECK(hipFree(const_cast<uint8_t*>(x.d)));
+    CHECK(hipFree(x.p));
+  }
+}
+
+struct CopyRun {
+  const void* fn;
+  const u32x4* s;
+  u32x4* d;
+  uint64_t n16;
+  uint32_t grid;
+};
+static void launch_copy(void* a) {
+  CopyRun* r = static_cast<CopyRun*>(a);
+  void* args[] = {&r->s, &r->d, &r->n16};
+  CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, 0, nullptr));
+}
+
+int main(int argc, char** argv) {
+  hipDeviceProp_t prop;
+  CHECK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+  const bool only_copy = argc > 1 && argv[1][0] == 'c';
+  if (argc > 1 && argv[1][0] == 'g') {
+    compute_geometry<10, 4, 2>(cus, 6554, 16384);
+    compute_geometry<10, 4, 4>(cus, 6554, 16384);
+    compute_geometry<8, 4, 4>(cus, 8192, 16384);
+    compute_geometry<4, 2, 2>(cus, 1024, 65536);
+    return 0;
+  }
+  if (!only_copy) {
+    geometry<10, 4>(cus, 6554, 16384);
+    geometry<10, 4>(cus, 6656, 16384);
+    geometry<8, 4>(cus, 8192, 16384);
+    geometry<4, 2>(cus, 1024, 65536);
+  }
+  const uint64_t bytes = 1ull << 30;
+  u32x4 *a, *b;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipMalloc(&b, bytes));
+  CHECK(hipMemset(a, 1, bytes));
+  struct C {
+    const char* name;
+    const void* fn;
+  } cs[] = {{"U=2", (const void*)&copyk<2>}, {"U=4", (const void*)&copyk<4>}, {"U=8", (const void*)&copyk<8>},
+            {"U=16", (const void*)&copyk<16>}};
+  for (auto& c : cs)
+    for (int g : {1, 2, 4, 8, 16}) {
+      CopyRun r{c.fn, a, b, bytes / 16, (uint32_t)(cus * g)};
+      const float ms = time_it(launch_copy, &r, 10);
+      std::printf("copy %-5s blocks/CU=%-2d %7.1f GB/s (read+write)\n", c.name, g, 2.0 * bytes / ms / 1e6);
+    }
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipMemcpy(b, a, bytes, hipMemcpyDeviceToDevice));
+  CHECK(hipEventRecord(e0));
+  for (int i = 0; i < 10; ++i) CHECK(hipMemcpyAsync(b, a, bytes, hipMemcpyDeviceToDevice, nullptr));
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  std::printf("hipMemcpyAsync D2D          %7.1f GB/s (read+write)\n", 2.0 * bytes / (ms / 10) / 1e6);
+  return 0;
+}
