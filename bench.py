@@ -13,11 +13,20 @@ each with its own stripe batches (objects are independent: weak scaling, no
 data-path collective); the only collectives are the timing barrier / max-reduce.
 
 Roofline: the dominant kernel's algorithmic bytes per launch (encode N.S.(K+M),
-reconstruct N.S.(K+e)) / its average launch time measured with HIP
-events on the launch stream, against 8.0 TB/s (MI355X_MICROARCH.md).
+reconstruct N.S.(K+e)) / its average launch time, measured with one
+HIP event pair on the launch stream around 100 back-to-back launches of that kernel
+over the same rotating batches (so launch gaps count against it), against 8.0 TB/s
+(MI355X_MICROARCH.md).  `frac_rocprof` is the same bytes over the
+rocprofv3 average of the kernel from the committed profiles/ summary of this
+workload (null when none is committed).
 cpu_baseline: oracle/rs_cpu_baseline.c (AVX-512 GFNI / AVX2 split-nibble C
 restatement of klauspost's CPU kernels -- a port, not the Go reference, which is
 absent) on the host cores of this box, same workload, bounded sample.
+
+Every BASELINE config is measured at every world size: the K/M sweep (configs[3])
+weak-scaled (16 384 stripes of 64 KiB per GPU), the healer mix (configs[4]) strong-
+scaled (1 M objects split across the GPUs), each rank timed on its own GPU and the
+slowest rank's time taken.
 """
 from __future__ import annotations
 
@@ -26,6 +35,7 @@ import glob
 import itertools
 import json
 import os
+import platform
 import sys
 import time
 
@@ -36,18 +46,24 @@ sys.path.insert(0, ROOT)
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Compute-free ceilings of the RS access patterns on MI355X (tools/pattern_probe.hip,
+# profiles/r02_pattern_probe.log): the best the split layout's traffic reaches with no
+# arithmetic at all, fraction of 8 TB/s.
+PATTERN_CEILING = {(4, 2, 1024): 0.797, (4, 2, 16384): 0.774, (8, 4, 8192): 0.778, (10, 4, 6554): 0.712}
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--steps", type=int, default=500)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--stripes", type=int, default=65536)
     p.add_argument("--stripe-kib", type=int, default=4)
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--m", type=int, default=2)
     p.add_argument("--rotate-gib", type=float, default=2.0)
+    p.add_argument("--sustained-ms", type=float, default=150.0,
+                   help="also time >= this many ms of steps (extras.sustained); 0 = off")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -73,80 +89,123 @@ def make_batches(torch, n_batches, N, k, m, P, seed):
     return out
 
 
-def measure_rs(torch, eng, k, m, S, N, steps, warmup, rotate_bytes, seed, roofline_reps=20, barrier=lambda: None):
-    """Step = encode the batch + reconstruct 2 erased shards per stripe (seeded
-    per-stripe pattern, device-resident masks).  Returns the step time, and each
-    kernel's average launch duration from `roofline_reps` back-to-back launches
-    bracketed by one HIP event pair on the launch stream (torch's current stream,
-    which the engine launches on)."""
-    from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
+class RSWorkload:
+    """Rotating device batches of one code and one step: encode the batch, then
+    reconstruct 2 erased shards per stripe (seeded per-stripe pattern, device masks)
+    out of place -- the reference's semantics (Reconstruct gives missing entries NEW
+    slices; the healer writes back only those), include/rsgpu.h's
+    rs_reconstruct_batch_out."""
 
-    t = k + m
-    P = shard_pitch_for(S)
-    batch_bytes = N * t * P
-    nb = max(2, int(np.ceil(rotate_bytes / batch_bytes)))
-    bufs = make_batches(torch, nb, N, k, m, P, seed)
-    # reconstruct writes the 2 missing shards of every stripe to a separate output
-    # buffer: the reference's semantics (Reconstruct gives missing entries NEW
-    # slices; the healer writes back only those) and include/rsgpu.h's
-    # rs_reconstruct_batch_out
-    # (device masks: the engine cannot bound #missing on the host, so it requires
-    # room for m outputs per stripe; only the first 2 are written here)
-    outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)]
-    rng = np.random.default_rng(0x5EED0003)
-    masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(nb)]
-    for d, p in bufs:  # make every batch a codeword before timing
-        eng.encode(d, p, S, N)
+    def __init__(self, torch, eng, k, m, S, N, rotate_bytes, seed):
+        from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
 
-    def enc(i):
-        d, p = bufs[i % nb]
-        eng.encode(d, p, S, N)
-
-    def rec(i):
-        d, p = bufs[i % nb]
-        eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
-
-    for i in range(warmup):
-        enc(i)
-        rec(i)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        enc(i)
-        rec(i)
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    eng.sync()
-    kernel_ms = {}
-    kernel_names = {}
-    for name, fn in (("encode", enc), ("reconstruct", rec)):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for i in range(roofline_reps):
-            fn(i)
-        e1.record()
+        self.torch, self.eng, self.k, self.m, self.S, self.N = torch, eng, k, m, S, N
+        t = k + m
+        self.P = shard_pitch_for(S)
+        self.batch_bytes = N * t * self.P
+        self.nb = max(2, int(np.ceil(rotate_bytes / self.batch_bytes)))
+        self.bufs = make_batches(torch, self.nb, N, k, m, self.P, seed)
+        # device masks: the engine cannot bound #missing on the host, so outputs
+        # have room for m per stripe; the first 2 are written here
+        self.outs = [torch.empty((N, m, self.P), dtype=torch.uint8, device="cuda") for _ in range(self.nb)]
+        rng = np.random.default_rng(0x5EED0003)
+        self.masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(self.nb)]
+        for d, p in self.bufs:  # every batch a codeword before timing
+            eng.encode(d, p, S, N)
         torch.cuda.synchronize()
-        kernel_ms[name] = e0.elapsed_time(e1) / roofline_reps
-        kernel_names[name] = eng.last_kernel()
-    eng.sync()
-    # full-size property check on every stripe of two batches: the reconstructed
-    # shards equal the erased originals (encode -> erase 2 -> reconstruct round trip)
-    ok = True
-    for i in range(min(nb, 2)):
-        d, p = bufs[i]
-        full = torch.cat([d[:, :, :S], p[:, :, :S]], dim=1)
-        mk = masks[i].cpu().numpy().view(np.uint32)
-        lost = torch.from_numpy((((mk[:, None] >> np.arange(t)[None, :]) & 1) == 0)).cuda()
-        want = full[lost].view(N, 2, S)  # missing shards in index order
-        ok &= bool(torch.equal(outs[i][:, :2, :S], want))
-    del bufs, masks, outs
-    torch.cuda.empty_cache()
-    return {"dt": dt, "steps": steps, "kernel_ms": kernel_ms, "batch_bytes": batch_bytes, "n_batches": nb, "ok": ok,
-            "kernels": kernel_names}
+
+    def enc(self, i):
+        d, p = self.bufs[i % self.nb]
+        self.eng.encode(d, p, self.S, self.N)
+
+    def rec(self, i):
+        d, p = self.bufs[i % self.nb]
+        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks[i % self.nb])
+
+    def alg_bytes(self):
+        return {"encode": self.N * self.S * (self.k + self.m), "reconstruct": self.N * self.S * (self.k + 2)}
+
+    def run_steps(self, steps, warmup, barrier):
+        """Times exactly `steps` steps between barrier + synchronize brackets."""
+        torch = self.torch
+        for i in range(warmup):
+            self.enc(i)
+            self.rec(i)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            self.enc(i)
+            self.rec(i)
+        torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        self.eng.sync()
+        return dt
+
+    def kernel_ms(self, reps=100):
+        """Each kernel's average launch duration: one HIP event pair around `reps`
+        back-to-back launches on the launch stream (launch gaps included)."""
+        out = {}
+        for name, fn in (("encode", self.enc), ("reconstruct", self.rec)):
+            out[name] = kernel_ms_events(self.torch, fn, reps, per_launch=False)
+        self.eng.sync()
+        return out
+
+    def check(self):
+        """Full-size property check on every stripe of two batches: the
+        reconstructed shards equal the erased originals.  (Bit-exactness against
+        the CPU oracle is the test suite's job -- tests/test_gpu_configs.py runs
+        these exact configs against it; bench.py touches oracle/ only in its
+        cpu_baseline leg.)"""
+        torch, k, m, S, N = self.torch, self.k, self.m, self.S, self.N
+        t = k + m
+        ok = True
+        for i in range(min(self.nb, 2)):
+            self.enc(i)
+            self.rec(i)
+            torch.cuda.synchronize()
+            d, p = self.bufs[i]
+            full = torch.cat([d[:, :, :S], p[:, :, :S]], dim=1)
+            mk = self.masks[i].cpu().numpy().view(np.uint32)
+            lost = torch.from_numpy((((mk[:, None] >> np.arange(t)[None, :]) & 1) == 0)).cuda()
+            ok &= bool(torch.equal(self.outs[i][:, :2, :S], full[lost].view(N, 2, S)))
+        return ok
+
+    def close(self):
+        del self.bufs, self.outs, self.masks
+        self.torch.cuda.empty_cache()
+
+
+def kernel_ms_events(torch, fn, reps, per_launch=False):
+    """Average duration of fn's launches on torch's current stream (the launch
+    stream): one HIP event pair around `reps` back-to-back launches."""
+    fn(0)
+    fn(1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for i in range(reps):
+        fn(i)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, affinity
 
 
 def cpu_baseline(k, m, S, N_sample, seconds):
@@ -155,11 +214,8 @@ def cpu_baseline(k, m, S, N_sample, seconds):
     t = k + m
     P = S  # host layout: contiguous shards
     buf = np.random.default_rng(1).integers(0, 256, N_sample * t * P, dtype=np.uint8)
-    try:
-        threads = len(os.sched_getaffinity(0))
-    except AttributeError:
-        threads = os.cpu_count() or 1
-    threads = max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads))))
+    model, nproc, affinity = cpu_info()
+    threads = max(1, min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity))))
     mat = rs_oracle.build_matrix(k, m)
     surv, miss, rows = rs_oracle.decode_rows(k, m, [0, 0] + [1] * (t - 2))
     level = 0
@@ -178,9 +234,13 @@ def cpu_baseline(k, m, S, N_sample, seconds):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
+        "cpu_model": model,
+        "nproc": nproc,
+        "affinity_cpus": affinity,
         "sample": f"{done} passes x (encode + 2-erasure reconstruct) of {N_sample} x {k * S // 1024} KiB "
-                  f"RS({k}+{m}) stripes, {simd}, one stripe per task, {threads} threads "
-                  f"(C restatement of klauspost's CPU kernels; Go reference absent)",
+                  f"RS({k}+{m}) stripes in {dt:.1f} s, {simd}, one stripe per task, {threads} threads on "
+                  f"'{model}' (nproc {nproc}, {affinity} CPUs in this process's affinity mask; C restatement of "
+                  f"klauspost's CPU kernels, Go reference absent)",
     }
 
 
@@ -188,17 +248,7 @@ def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
     a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     a.fill_(1)
-    for _ in range(3):
-        eng.device_copy(b, a)
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        eng.device_copy(b, a)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
+    ms = kernel_ms_events(torch, lambda i: eng.device_copy(b, a), iters)
     del a, b
     torch.cuda.empty_cache()
     return 2 * nbytes / (ms * 1e-3) / 1e9
@@ -251,21 +301,27 @@ def host_e2e(torch, eng, k, m, S, N):
     return out
 
 
-def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
+def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
     """N objects, each either encoded (parity missing) or
     repaired from one erasure (index uniform in [0, k+m)), 50/50 by a seeded draw,
     in ONE batched call with a present-mask per stripe.  e2e: shards in pinned host
     memory, H2D + kernel + D2H inside the timed region (rs_reconstruct_batch,
-    RS_MEM_HOST).  device: the same masks on HBM-resident shards."""
+    RS_MEM_HOST).  device: the same masks on HBM-resident shards.  The N_total
+    objects are split across the ranks (contiguous ranges); times are the slowest
+    rank's, rates the whole job's."""
+    rank, _, world = rdist.world()
+    b, e = rdist.stripe_range(N_total, rank, world)
+    N = e - b
     t = k + m
     full = (1 << t) - 1
     rng = np.random.default_rng(seed)
-    is_rec = rng.random(N) < 0.5
-    lost = rng.integers(0, t, N)
+    is_rec_all = rng.random(N_total) < 0.5
+    lost_all = rng.integers(0, t, N_total)
+    is_rec, lost = is_rec_all[b:e], lost_all[b:e]
     masks = np.where(is_rec, full & ~(1 << lost), (1 << k) - 1).astype(np.uint32)
     data = torch.empty((N, k, S), dtype=torch.uint8, pin_memory=True)
     parity = torch.empty((N, m, S), dtype=torch.uint8, pin_memory=True)
-    g = torch.Generator(device="cuda").manual_seed(seed)
+    g = torch.Generator(device="cuda").manual_seed(seed + rank)
     step = 1 << 16
     for s0 in range(0, N, step):  # random data + its true parity, made on the GPU
         n = min(step, N - s0)
@@ -278,12 +334,12 @@ def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
     dn, pn = data.numpy(), parity.numpy()
     sample = rng.choice(N, size=min(N, 4096), replace=False)
     ref_d, ref_p = dn[sample].copy(), pn[sample].copy()
-    lost_d = (~masks[:, None] >> np.arange(k)[None, :]) & 1
-    lost_p = (~masks[:, None] >> np.arange(k, t)[None, :]) & 1
+    lost_d = ((~masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
+    lost_p = ((~masks[:, None] >> np.arange(k, t)[None, :]) & 1).astype(bool)
 
     def erase():
-        dn[lost_d.astype(bool)] = 0
-        pn[lost_p.astype(bool)] = 0
+        dn[lost_d] = 0
+        pn[lost_p] = 0
 
     e2e, ok = {}, True
     for zc in (True, False):  # torch's pinned pages are GPU-mapped: zero-copy qualifies
@@ -293,9 +349,10 @@ def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
         times = []
         for _ in range(2):
             erase()
+            rdist.barrier()
             t0 = time.perf_counter()
             eng.reconstruct_host(dn, pn, S, N, masks)
-            times.append(time.perf_counter() - t0)
+            times.append(rdist.max_over_ranks(time.perf_counter() - t0))
         ok = ok and bool(np.array_equal(dn[sample], ref_d) and np.array_equal(pn[sample], ref_p))
         e2e[eng.last_host_path()] = min(times)
     eng.set_host_zero_copy(True)
@@ -303,25 +360,57 @@ def healer_mix(torch, eng, k, m, S, N, seed=0x5EED0005):
     dd = data.cuda()
     pd = parity.cuda()
     md = torch.from_numpy(masks.view(np.int32)).cuda()
-    eng.reconstruct_devmask(dd, pd, S, N, md)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(5):
-        eng.reconstruct_devmask(dd, pd, S, N, md)
-    e1.record()
-    torch.cuda.synchronize()
-    t_dev = e0.elapsed_time(e1) / 5 * 1e-3
+    rdist.barrier()
+    t_dev = rdist.max_over_ranks(kernel_ms_events(torch, lambda i: eng.reconstruct_devmask(dd, pd, S, N, md), 5)
+                                 * 1e-3)
     eng.sync()
     del dd, pd, md, data, parity
     torch.cuda.empty_cache()
-    user = N * k * S
-    return {"objects": N, "shard_len": S, "encode_frac": round(float((~is_rec).mean()), 4),
+    user = N_total * k * S
+    return {"objects": N_total, "objects_per_gpu": N, "shard_len": S,
+            "encode_frac": round(float((~is_rec_all).mean()), 4),
             "e2e_GiBps": {p: round(user / t / GiB, 2) for p, t in e2e.items()},
-            "e2e_objects_per_s": {p: round(N / t) for p, t in e2e.items()},
-            "device_GiBps": round(user / t_dev / GiB, 1), "ok_sample": ok,
+            "e2e_objects_per_s": {p: round(N_total / t) for p, t in e2e.items()},
+            "device_GiBps": round(user / t_dev / GiB, 1), "ok_sample": rdist.all_true(ok),
             "note": "zero-copy: kernel reads survivors / writes missing shards over PCIe in place; "
                     "staged: every k+m slot DMA'd each way"}
+
+
+def kmsweep(torch, rdist, rotate):
+    """configs[3]: RS(4+2), RS(8+4), RS(10+4) at 64 KiB stripes, 16 384 stripes per
+    GPU (weak scaling): each kernel's average launch time (HIP events) on every
+    rank, the slowest rank's time taken, aggregate rate = world x per-GPU bytes."""
+    from replication_erasurecoding_object_store_amd.batch import BatchEngine
+
+    _, _, world = rdist.world()
+    sweep = {}
+    for kk, mm in [(4, 2), (8, 4), (10, 4)]:
+        e2 = BatchEngine(kk, mm, torch.cuda.current_device())
+        SS, NN = -(-65536 // kk), 16384
+        w = RSWorkload(torch, e2, kk, mm, SS, NN, rotate, seed=0x5EED0004)
+        rdist.barrier()
+        enc_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.enc, 10))
+        rdist.barrier()
+        rec_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec, 10))
+        ok = rdist.all_true(w.check())
+        alg = w.alg_bytes()
+        kern = e2.last_kernel()
+        w.close()
+        e2.close()
+        ceiling = PATTERN_CEILING.get((kk, mm, SS))
+        ent = {
+            "shard_len": SS, "stripes_per_gpu": NN,
+            "encode_GiBps": round(world * NN * kk * SS / (enc_ms * 1e-3) / GiB, 1),
+            "reconstruct2_GiBps": round(world * NN * kk * SS / (rec_ms * 1e-3) / GiB, 1),
+            "encode_hbm_frac": round(alg["encode"] / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "reconstruct2_hbm_frac": round(alg["reconstruct"] / (rec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "ok": ok,
+            "reconstruct_kernel": kern,
+        }
+        if ceiling:
+            ent["pattern_ceiling_frac"] = ceiling
+        sweep[f"rs{kk}{mm}_64KiB"] = ent
+    return sweep
 
 
 def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
@@ -337,15 +426,7 @@ def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
     for d, p in bufs:
         eng.encode(d, p, S, N)
     bad = torch.empty(N, dtype=torch.int32, device="cuda")
-    for i in range(2):
-        eng.verify(*bufs[i % nb], bad, S, N)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(reps):
-        eng.verify(*bufs[i % nb], bad, S, N)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    ms = kernel_ms_events(torch, lambda i: eng.verify(*bufs[i % nb], bad, S, N), reps)
     d, p = bufs[0]
     eng.verify(d, p, bad, S, N)
     torch.cuda.synchronize()
@@ -382,38 +463,28 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
     one = ((1 << t) - 1) & ~(1 << rng.integers(0, t, N))
     full = (1 << t) - 1
     dev_one = torch.from_numpy(one.astype(np.uint32).view(np.int32)).cuda()
-
-    def timed(fn):
-        for i in range(2):
-            fn(i)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for i in range(reps):
-            fn(i)
-        e1.record()
-        torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e-3
-
     res = {}
 
-    def put(name, sec, e):
+    def put(name, ms, e):
+        sec = ms * 1e-3
         res[name] = {"user_GiBps": round(N * k * S / sec / GiB, 1),
                      "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4)}
 
-    put("rec1_per_stripe_out", timed(lambda i: eng.reconstruct_out(split[i % nb][0], split[i % nb][1],
-                                                                      split[i % nb][2], S, N, masks_dev=dev_one)), 1)
+    put("rec1_per_stripe_out", kernel_ms_events(torch, lambda i: eng.reconstruct_out(
+        split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one), reps), 1)
     for name, pat in (("rec_0_1_uniform_out", (0, 1)), ("rec_0_4_uniform_out", (0, 4)),
                       ("rec_4_5_uniform_out", (4, 5))):
         mask = full & ~sum(1 << j for j in pat)
-        put(name, timed(lambda i: eng.reconstruct_out(split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N,
-                                                      present_masks=mask)), 2)
+        put(name, kernel_ms_events(torch, lambda i: eng.reconstruct_out(
+            split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, present_masks=mask), reps), 2)
     del split
     torch.cuda.empty_cache()
     # SoA: shard s of every stripe in one plane
     soa = [(torch.randint(0, 256, (k, N, P), dtype=torch.uint8, device="cuda", generator=g),
             torch.empty((m, N, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
-    put("soa_encode", timed(lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N, shard_pitch=N * P,
-                                                 data_stripe_pitch=P, parity_stripe_pitch=P)), m)
+    put("soa_encode", kernel_ms_events(torch, lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N,
+                                                                   shard_pitch=N * P, data_stripe_pitch=P,
+                                                                   parity_stripe_pitch=P), reps), m)
     del soa
     torch.cuda.empty_cache()
     return res
@@ -421,29 +492,21 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
 
 def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
     """Batched SHA-256 of N device-resident objects (the reference's cold_hash,
-    writeservice.go:51-54) vs hashlib (OpenSSL) on the host cores."""
+    writeservice.go:51-54) vs the host cores (SHA-NI C port)."""
     import hashlib
 
     g = torch.Generator(device="cuda").manual_seed(0x5EED0007)
     bufs = [torch.randint(0, 256, (N, length), dtype=torch.uint8, device="cuda", generator=g) for _ in range(2)]
     out = torch.empty((N, 32), dtype=torch.uint8, device="cuda")
+    sec = kernel_ms_events(torch, lambda i: eng.sha256(bufs[i % 2], length, N, digests=out), reps) * 1e-3
     eng.sha256(bufs[0], length, N, digests=out)
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for i in range(reps):
-        eng.sha256(bufs[i % 2], length, N, digests=out)
-    e1.record()
-    torch.cuda.synchronize()
-    sec = e0.elapsed_time(e1) / reps * 1e-3
-    host = bufs[(reps - 1) % 2][:256].cpu().numpy()
+    host = bufs[0][:256].cpu().numpy()
     ok = all(out[i].cpu().numpy().tobytes() == hashlib.sha256(host[i].tobytes()).digest() for i in range(0, 256, 17))
-    # host baseline: SHA-NI (the class of Go crypto/sha256's amd64 code) on all
-    # host threads, over a sample of the same objects, timed to ~cpu_seconds
-    sys.path.insert(0, ROOT)
     from oracle import rs_oracle
 
-    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    _, _, affinity = cpu_info()
+    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     sample = bufs[0][:8192].cpu().numpy()
     ns, t_cpu, ni = 0, 0.0, False
     while t_cpu < cpu_seconds:
@@ -460,9 +523,9 @@ def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
             "cpu_kind": "port (oracle/sha256_cpu_baseline.c, " + ("SHA-NI" if ni else "scalar") + ")"}
 
 
-def pmc_traffic(workload):
-    """Per-launch HBM bytes from the newest committed rocprofv3 PMC summary of this
-    workload (profiles/<tag>_pmc.json written by tools/prof_summary.py), if any."""
+def committed_profile(workload):
+    """The newest committed rocprofv3 summary of this workload
+    (profiles/<tag>_pmc.json written by tools/prof_summary.py), if any."""
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             with open(path) as f:
@@ -470,6 +533,7 @@ def pmc_traffic(workload):
         except Exception:
             continue
         if doc.get("workload") == workload:
+            doc["_path"] = os.path.relpath(path, ROOT)
             return doc
     return None
 
@@ -500,22 +564,39 @@ def main():
     rotate = int(args.rotate_gib * GiB)
 
     # weak scaling: every rank owns its own N-stripe batches (independent objects)
-    res = measure_rs(torch, eng, k, m, S, N, args.steps, args.warmup, rotate, seed=0x5EED0002 + rank,
-                     barrier=rdist.barrier)
-    dt = rdist.max_over_ranks(res["dt"])
-    res["ok"] = rdist.all_true(res["ok"])
+    w = RSWorkload(torch, eng, k, m, S, N, rotate, seed=0x5EED0002 + rank)
+    dt = rdist.max_over_ranks(w.run_steps(args.steps, args.warmup, rdist.barrier))
+    km = w.kernel_ms()
+    kernel_names = {}
+    for name, fn in (("encode", w.enc), ("reconstruct", w.rec)):
+        fn(0)
+        kernel_names[name] = eng.last_kernel()
+    torch.cuda.synchronize()
     user_bytes_per_step = 2 * N * k * S
     value = world * args.steps * user_bytes_per_step / dt / GiB
     ms_step = dt / args.steps * 1e3
+    sustained = None
+    if args.sustained_ms > 0 and ms_step * args.steps < args.sustained_ms:
+        steps2 = int(np.ceil(args.sustained_ms / ms_step))
+        dt2 = rdist.max_over_ranks(w.run_steps(steps2, 2, rdist.barrier))
+        sustained = {"steps": steps2, "timed_s": round(dt2, 4), "ms_per_step": round(dt2 / steps2 * 1e3, 4),
+                     "value_GiBps": round(world * steps2 * user_bytes_per_step / dt2 / GiB, 3)}
+    ok = rdist.all_true(w.check())
+    alg = w.alg_bytes()
+    w.close()
 
-    km = res["kernel_ms"]
-    alg = {"encode": N * S * (k + m), "reconstruct": N * S * (k + 2)}
-    dom = max(km, key=km.get) if km else "reconstruct"
-    achieved = alg[dom] / (km.get(dom, float("nan")) * 1e-3) / 1e9 if km else None
-    traffic = None
-    pmc = pmc_traffic(f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split")
-    if pmc:
-        traffic = pmc.get("hbm_bytes_per_launch", {}).get(dom)
+    dom = max(km, key=km.get)
+    achieved = alg[dom] / (km[dom] * 1e-3) / 1e9
+    workload_key = f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split"
+    prof = committed_profile(workload_key)
+    frac_rocprof, traffic, rocprof_ns = None, None, None
+    if prof:
+        ent = next((v for kname, v in prof.get("kernels", {}).items()
+                    if kname.endswith("true>" if dom == "reconstruct" else "false>") and "apply_kernel" in kname), None)
+        if ent:
+            rocprof_ns = ent["avg_ns"]
+            frac_rocprof = round(alg[dom] / rocprof_ns / HBM_PEAK_GBS, 4)
+        traffic = prof.get("hbm_bytes_per_launch", {}).get(dom)
 
     out = {
         "metric": "GiB/s device-resident RS(4+2) encode + 2-erasure reconstruct, batched stripes",
@@ -533,56 +614,51 @@ def main():
                 "(seed 0x5EED0003)",
         "config": {
             "workload": f"RS({k}+{m}) encode + 2-erasure reconstruct, {N} objects x {args.stripe_kib} KiB stripe "
-                        f"(S={S}) per GPU, device-resident, {res['n_batches']} rotating batches "
-                        f"({res['n_batches'] * res['batch_bytes'] / GiB:.2f} GiB)",
+                        f"(S={S}) per GPU, device-resident, {w.nb} rotating batches "
+                        f"({w.nb * w.batch_bytes / GiB:.2f} GiB)",
             "k": k, "m": m, "shard_len": S, "stripes_per_gpu": N,
             "parallelism": f"dp{world} (independent stripes per GPU, no collective)",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": f"{res['kernels'].get(dom)} ({dom}; rocprof name rs::apply_kernel<{k}, {m}, 2, "
-                      f"{'true' if dom == 'reconstruct' else 'false'}>)",
-            "timing": "HIP events around 20 back-to-back launches on the launch stream",
-            "achieved": round(achieved, 1) if achieved else None,
+            "kernel": f"{kernel_names.get(dom)} ({dom}; rocprof name rs::apply_kernel<{k}, {m}, "
+                      f"{2 if dom == 'reconstruct' else m}, {'true' if dom == 'reconstruct' else 'false'}>)",
+            "timing": "one HIP event pair around 100 back-to-back launches per kernel, on the launch stream",
+            "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "frac_rocprof": frac_rocprof,
+            "rocprof_avg_ns": rocprof_ns,
+            "rocprof_summary": prof["_path"] if prof else None,
+            "pattern_ceiling_frac": PATTERN_CEILING.get((k, m, S)),
             "kernel_ms": {kk: round(v, 5) for kk, v in km.items()},
             "alg_bytes_per_launch": alg,
         },
-        "parity_check_full_size": res["ok"],
+        "parity_check_full_size": ok,
+        "consistency": {"timed_region_s": round(dt, 4), "sum_kernel_ms": round(sum(km.values()), 5)},
     }
+    if sustained:
+        out["sustained"] = sustained
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds)
-    if rank == 0 and world == 1 and not args.no_extras:
-        extras = {"copy_kernel_peak_GBps": round(copy_peak(torch, eng), 1)}
-        sweep = {}
-        for kk, mm in [(4, 2), (8, 4), (10, 4)]:
-            e2 = BatchEngine(kk, mm, 0)
-            SS = -(-65536 // kk)
-            NN = 16384
-            r = measure_rs(torch, e2, kk, mm, SS, NN, 5, 2, rotate, seed=0x5EED0004, roofline_reps=10)
-            kms = r["kernel_ms"]
-            sweep[f"rs{kk}{mm}_64KiB"] = {
-                "shard_len": SS, "stripes": NN,
-                "encode_GiBps": round(NN * kk * SS / (kms["encode"] * 1e-3) / GiB, 1),
-                "reconstruct2_GiBps": round(NN * kk * SS / (kms["reconstruct"] * 1e-3) / GiB, 1),
-                "encode_hbm_frac": round(NN * SS * (kk + mm) / (kms["encode"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "reconstruct2_hbm_frac": round(NN * SS * (kk + 2) / (kms["reconstruct"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                                               4),
-                "ok": r["ok"],
-            }
+    if not args.no_extras:
+        extras = {}
+        cp = rdist.max_over_ranks(-copy_peak(torch, eng))  # slowest rank's copy rate
+        extras["copy_kernel_peak_GBps_per_gpu"] = round(-cp, 1)
+        extras["kmsweep_64KiB_device"] = kmsweep(torch, rdist, rotate)
+        extras["healer_mix_config5"] = healer_mix(torch, eng, rdist, k, m, S, 1 << 20)
+        if world == 1:
+            extras["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
+            extras["scrub_verify_device"] = {"rs42_4KiB": scrub_rate(torch, eng, k, m, S, N, rotate)}
+            e2 = BatchEngine(10, 4, 0)
+            extras["scrub_verify_device"]["rs104_64KiB"] = scrub_rate(torch, e2, 10, 4, 6554, 16384, rotate)
             e2.close()
-        extras["kmsweep_64KiB_device"] = sweep
-        extras["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
-        extras["scrub_verify_device"] = {"rs42_4KiB": scrub_rate(torch, eng, k, m, S, N, rotate)}
-        e2 = BatchEngine(10, 4, 0)
-        extras["scrub_verify_device"]["rs104_64KiB"] = scrub_rate(torch, e2, 10, 4, 6554, 16384, rotate)
-        e2.close()
-        extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 1 << 18)
-        extras["healer_mix_config5"] = healer_mix(torch, eng, k, m, S, 1 << 20)
-        extras["sha256_cold_hash_4KiB"] = sha256_rate(torch, eng)
+            extras["host_e2e_pinned_rs42_4KiB"] = host_e2e(torch, eng, k, m, S, 1 << 18)
+            extras["sha256_cold_hash_4KiB"] = sha256_rate(torch, eng)
+        copy = extras["copy_kernel_peak_GBps_per_gpu"]
+        out["roofline"]["frac_of_measured_copy"] = round(achieved / copy, 4)
         out["extras"] = extras
     if rank == 0:
         line = json.dumps(out)

@@ -1362,8 +1362,10 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   Engine* e = engine_for_stream(c, as_stream(stream));
   if (!e) return RS_ERR_INVALID_ARG;
   DeviceScope ds(e->device);
+  // 16 workgroups per CU, 4 x 16 B in flight per lane: the best of tools/pattern_probe's
+  // copy sweep (U = 2..16 loads per lane x 1..16 workgroups per CU)
   const uint32_t grid = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count) * 2, (bytes / 16 + 1023) / 1024)));
+      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count) * 16, (bytes / 16 + 1023) / 1024)));
   rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
   c->shared.last_kernel.store("copy_kernel");
   RS_HIP(hipGetLastError());

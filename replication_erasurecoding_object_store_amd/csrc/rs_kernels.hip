@@ -164,164 +164,90 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
 // #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
-//
-// Software-pipelined over a wave's tasks (task = one stripe's 64-column block):
-// task t+1's K input loads -- and, per stripe, its plan's tables -- are issued
-// before task t is computed and stored, so every wave keeps a task's loads in
-// flight while it computes (tools/pattern_probe.hip: at RS(10+4) 64 KiB stripes
-// the same arithmetic reaches 73 % of 8 TB/s pipelined at one wave per SIMD,
-// 65-66 % load-compute-store at any occupancy).  Two register sets, the loop
-// unrolled by two.
-//
-// Per-task state comes from the stripe's present mask alone: the inputs are its
-// first K present shards and the outputs every missing shard in `out_mask`, in
-// index order -- exactly how the plans are built (rs_engine.cpp make_decode_plan)
-// -- found with scalar bit scans, so no plan header is read before the loads.
-// Per-stripe plans are picked by a missing-mask -> plan LUT held in LDS, and the
-// plan's table block (<= 1 KiB) is loaded by one vector load next to the task's
-// data, then written to the wave's LDS slot: the products read their tables with
-// broadcast ds_reads straight into VGPRs (no scalar-cache misses on a plan set
-// of up to 1.3 MB, no constant-bus v_movs).
-constexpr uint32_t kPlanLds = 1024;  // bytes of plan a wave stages in LDS
-typedef const __attribute__((address_space(3))) uint8_t* lds_cptr;
-
-template <int K, int M, int E, bool PER_STRIPE>
-struct Stage {
-  u32x4 x[K];
-  u32x4 tab;         // PER_STRIPE: this lane's 16 B of the task's plan
-  uint32_t stripe;   // wave-uniform
-  uint32_t present;  // wave-uniform present mask
-  uint32_t blk;      // wave-uniform column block
-};
-
-// The first K set bits of `present` (inputs) and the first E of `missing`
-// (outputs), lowest first; n = outputs in use.
-template <int K>
-__device__ __forceinline__ void first_bits(uint32_t v, uint32_t (&s)[K]) {
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    s[c] = v ? static_cast<uint32_t>(__builtin_ctz(v)) : 0u;
-    v &= v - 1u;
-  }
-}
-
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
-  constexpr bool kLutLds = PER_STRIPE && K + M <= 14;
-  __shared__ __attribute__((aligned(16))) uint8_t plan_lds[4][kPlanLds];
-  __shared__ uint16_t lut_lds[kLutLds ? (1u << (K + M)) : 1u];
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wslot = threadIdx.x >> 6;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + wslot);
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;   // the partial last column included
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;      // bytes of a partial last column (0: none)
-  const uint32_t pbytes = a.plan_bytes;       // <= kPlanLds for the specialised shapes
-  uint8_t* const my_plan = plan_lds[wslot];
-  // lane l carries bytes [16 l, 16 l + 16) of a plan; lanes past its end re-read its last 16 B
-  const uint32_t plan_lane_off = min(lane * 16u, pbytes - 16u);
-
-  if constexpr (kLutLds) {
-    for (uint32_t i = threadIdx.x; i < (1u << (K + M)); i += blockDim.x)
-      lut_lds[i] = static_cast<uint16_t>(a.lut[i]);
-  }
-  // one plan for the whole launch: its masks from the header, its tables into LDS
-  const uint32_t uniform_present = PER_STRIPE ? 0u : as_const<uint32_t>(a.plans)[1];
-  const uint32_t out_mask = PER_STRIPE ? a.full_mask : as_const<uint32_t>(a.plans)[2];
-  if constexpr (!PER_STRIPE) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(a.plans + plan_lane_off);
-    *reinterpret_cast<u32x4*>(my_plan + lane * 16u) = v;
-  }
-  __syncthreads();
-
   uint32_t bad = 0u;
-  uint32_t mask_next = 0u;  // PER_STRIPE: present mask of the next task to resolve (vector)
-  auto mask_of = [&](uint32_t t) -> uint32_t {
+
+  // mask of task t's stripe; every lane loads the same word (one request)
+  auto load_mask = [&](uint32_t t) -> uint32_t {
     const uint32_t tt = t < ntasks ? t : ntasks - 1u;
-    return a.present_masks[tt / bps];  // every lane loads the same word
+    return a.present_masks[tt / bps];
   };
 
-  // Resolves task t and issues its loads (plan block, then the K inputs).
-  auto fetch = [&](Stage<K, M, E, PER_STRIPE>& st, uint32_t t) {
-    st.stripe = t / bps;
-    st.blk = t - st.stripe * bps;
-    uint32_t present;
-    if constexpr (PER_STRIPE) {
-      present = __builtin_amdgcn_readfirstlane(mask_next) & a.full_mask;
-      mask_next = mask_of(t + nwaves);
-      const uint32_t missing = ~present & a.full_mask;
-      uint32_t pid;
-      if constexpr (kLutLds) {
-        pid = __builtin_amdgcn_readfirstlane(lut_lds[missing]);
-      } else {
-        pid = as_const<uint32_t>(a.lut)[missing];
-      }
-      if (pid == kPlanInvalid) {  // fewer than K present: leave the stripe untouched
-        bad = 1u;
-        pid = 0u;
-        present = a.full_mask;
-      }
-      st.tab = load16(uniform_ptr(a.plans + static_cast<uint64_t>(pid) * pbytes) + plan_lane_off);
-    } else {
-      present = uniform_present;
-      asm volatile("" : "+s"(present));  // per task: keeps K 64-bit slot offsets out of SGPRs
+  uint32_t mask = 0u;
+  if (PER_STRIPE && wave < ntasks) mask = load_mask(wave);
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
+    const uint8_t* plan = a.plans;
+    if (PER_STRIPE) {
+      const uint32_t present = __builtin_amdgcn_readfirstlane(mask);  // waits for this mask only
+      mask = load_mask(t + nwaves);                                  // next task's mask in flight
+      const uint32_t missing = (~present) & a.full_mask;
+      uint32_t pid = as_const<uint32_t>(a.lut)[missing];
+      bad |= (pid == kPlanInvalid) ? 1u : 0u;
+      pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
+      plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     }
-    st.present = present;
-    uint32_t in[K];
-    first_bits<K>(present, in);
-    const uint32_t col = st.blk * 64u + lane;
-    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;  // past the end: re-read the last column
-#pragma unroll
-    for (int c = 0; c < K; ++c) st.x[c] = load16(slot_ptr(a, K, st.stripe, in[c]) + off);
-  };
-
-  // Computes task st and stores its outputs.
-  auto finish = [&](Stage<K, M, E, PER_STRIPE>& st) {
-    if constexpr (PER_STRIPE) *reinterpret_cast<u32x4*>(my_plan + lane * 16u) = st.tab;
-    const uint32_t missing = ~st.present & out_mask;
-    const uint32_t n_out = __builtin_popcount(missing);
-    uint32_t outs[E];
-    first_bits<E>(missing, outs);
-    const uint32_t col = st.blk * 64u + lane;
-    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
+    if constexpr (K * E * 5 > 48) {
+      // Too many table dwords to keep resident in SGPRs across trips: make the plan
+      // pointer opaque per trip so its loads are not hoisted out of the loop (LICM
+      // would otherwise spill them through VGPR lanes: v_writelane/v_readlane).
+      asm volatile("" : "+s"(plan));
+    }
+    const PlanView pv(plan, K, M);
+    const uint32_t col = blk * 64u + lane;
     const bool full = col < a.full_cols;
+    // clamped, never branched: a lane past the end re-reads the last column (lines
+    // the wave's other lanes fetch anyway) and its stores are dropped
+    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
+
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
 
     // input-outer order (as upstream codeSomeShards): one input's chunk indices
-    // live at a time; products of inputs c-1 and c fold into the accumulator with
-    // one 3-input XOR.
+    // and E x 5 table dwords live at a time.  Products of inputs c-1 and c are
+    // folded into the accumulator with one 3-input XOR.  The scheduling barrier
+    // per input stops the compiler from hoisting every input's tables into SGPRs
+    // at once (K*E*5 dwords: 200 for RS(10+4) -> SGPR spills through VGPR lanes).
     u32x4 y[E], pend[E];
 #pragma unroll
     for (int r = 0; r < E; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
     // Per-stripe batches carry mixed patterns: rows [kLo, E) are only computed
-    // when this task fills more than kLo shards (a wave-uniform branch per input),
-    // so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs do half
-    // the lookups.  Skipped rows' stores are dropped.
+    // when this task's plan fills more than kLo shards (a wave-uniform branch per
+    // input), so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs
+    // do half the lookups.  Skipped rows' stores are dropped.
     constexpr int kLo = (PER_STRIPE && E >= 4) ? E / 2 : E;
     constexpr int kLo1 = kLo < E ? 1 : kLo;  // rows [kLo1, kLo) when n_out > kLo1
-    const bool hi_rows = kLo == E || n_out > static_cast<uint32_t>(kLo);
-    const bool mid_rows = kLo1 == kLo || n_out > static_cast<uint32_t>(kLo1);
+    const bool hi_rows = kLo == E || pv.n_out() > static_cast<uint32_t>(kLo);
+    const bool mid_rows = kLo1 == kLo || pv.n_out() > static_cast<uint32_t>(kLo1);
 #pragma unroll
     for (int c = 0; c < K; ++c) {
       Idx3 ix[4];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) ix[d] = split3(st.x[c][d]);
-      // an opaque LDS base per input: this input's table reads are not hoisted
-      // (a uniform plan's K*E*5 dwords would otherwise be pinned in VGPRs)
-      lds_cptr base = (lds_cptr)(my_plan);  // generic -> LDS address space
-      asm volatile("" : "+v"(base));
-      const lds_cptr quad = base + plan_tab_offset(K, M);
-      const lds_cptr c4 = base + plan_c4_offset(K, M);
-      auto rows = [&](auto lo_tag, auto hi_tag) {
+      for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+      // one opaque base per input: the scalar load merger cannot fuse this
+      // input's table loads with later inputs' (which would pin them in SGPRs)
+      const uint8_t* tcol = plan;
+      if constexpr (K * E * 5 > 48) asm volatile("" : "+s"(tcol));
+      const PlanView pc(tcol, K, M);
+      auto rows = [&](auto lo_tag, auto hi_tag, const PlanView& pt) {
         constexpr int R0 = decltype(lo_tag)::value, R1 = decltype(hi_tag)::value;
 #pragma unroll
         for (int r = R0; r < R1; ++r) {
-          const u32x4 q = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(quad + (r * K + c) * 16);
-          const uint32_t q4 = *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(c4 + (r * K + c) * 4);
+          const RS_CONST uint32_t* tb = pt.quad(r, c);
+          const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pt.c4(r, c);
 #pragma unroll
           for (int d = 0; d < 4; ++d) {
-            const uint32_t prod = lookup3(ix[d], q[0], q[1], q[2], q[3], q4);
+            const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
             if (c & 1)
               y[r][d] = xor3(y[r][d], pend[r][d], prod);
             else if (c == K - 1)
@@ -331,45 +257,33 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
           }
         }
       };
-      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo1>{});
+      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo1>{}, pc);
       if constexpr (kLo1 < kLo) {
-        if (mid_rows) rows(std::integral_constant<int, kLo1>{}, std::integral_constant<int, kLo>{});
+        if (mid_rows) {
+          const uint8_t* tmid = plan;
+          asm volatile("" : "+s"(tmid));
+          rows(std::integral_constant<int, kLo1>{}, std::integral_constant<int, kLo>{}, PlanView(tmid, K, M));
+        }
       }
       if constexpr (kLo < E) {
-        if (hi_rows) rows(std::integral_constant<int, kLo>{}, std::integral_constant<int, E>{});
+        if (hi_rows) {
+          const uint8_t* thi = plan;  // the high rows' tables load inside the branch
+          asm volatile("" : "+s"(thi));
+          rows(std::integral_constant<int, kLo>{}, std::integral_constant<int, E>{}, PlanView(thi, K, M));
+        }
       }
-      // one input's index chunks and tables live at a time
       if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
     }
+    const uint32_t n_out = pv.n_out();
 #pragma unroll
     for (int r = 0; r < E; ++r)
-      store16_or_drop(out_ptr(a, K, st.stripe, r, outs[r]), off, full && static_cast<uint32_t>(r) < n_out, y[r]);
-    if (nb != 0u && st.blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
+      store16_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, full && static_cast<uint32_t>(r) < n_out, y[r]);
+    if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
       const bool part = col == a.full_cols;
 #pragma unroll
       for (int r = 0; r < E; ++r)
-        store_part_or_drop(out_ptr(a, K, st.stripe, r, outs[r]), off, part && static_cast<uint32_t>(r) < n_out,
+        store_part_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, part && static_cast<uint32_t>(r) < n_out,
                            y[r], nb);
-    }
-  };
-
-  uint32_t t = wave;
-  if (t < ntasks) {
-    if constexpr (PER_STRIPE) mask_next = mask_of(t);
-    Stage<K, M, E, PER_STRIPE> A, B;
-    fetch(A, t);
-    for (;;) {
-      const uint32_t t1 = t + nwaves;
-      const bool more1 = t1 < ntasks;
-      if (more1) fetch(B, t1);
-      finish(A);
-      if (!more1) break;
-      const uint32_t t2 = t1 + nwaves;
-      const bool more2 = t2 < ntasks;
-      if (more2) fetch(A, t2);
-      finish(B);
-      if (!more2) break;
-      t = t2;
     }
   }
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
@@ -685,8 +599,8 @@ __global__ __launch_bounds__(256) void verify_kernel_generic(const KernelArgs a)
 
 // ---------------------------------------------------------------------------
 // Streaming copy (bench only): the measured HBM ceiling next to the RS kernels.
-// Shape from tools/hbm_probe.hip's best: 4 independent 16-B nt loads per lane in
-// flight, 2 workgroups per CU.
+// 4 independent 16-B nt loads per lane in flight, 16 workgroups per CU (the launch
+// in rs_device_copy): 6.0-6.2 TB/s read+write (tools/pattern_probe.hip copy sweep).
 __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
                                                    uint64_t n16) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u * 4u;

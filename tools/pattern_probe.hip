@@ -169,6 +169,85 @@ __global__ __launch_bounds__(256) void pE(Geo g) {
   }
 }
 
+static float time_it(void (*launch)(void*), void* arg, int iters);
+
+// F: one workgroup per stripe at a time: the stripe's K data shards (one contiguous
+// K*P-byte region in the split layout) stream into LDS with LDS-DMA (1 KiB per
+// wave-instruction, in address order), then the waves compute column blocks from
+// LDS and write the M parity rows (contiguous M*P bytes).  Occupancy: LDS-bound.
+template <int K, int M>
+__global__ __launch_bounds__(256) void pF(Geo g) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t chunks = (uint32_t)(((uint64_t)K * g.P) / 1024);  // P multiple of 256: K*P multiple of 1024 for K%4==2..
+  const uint32_t bps = (g.cols + 63) / 64;
+  for (uint32_t s = blockIdx.x; s < g.N; s += gridDim.x) {
+    const uint8_t* src = g.d + (uint64_t)s * K * g.P;
+    for (uint32_t j = w; j < chunks; j += 4) {
+      __builtin_amdgcn_global_load_lds(src + (uint64_t)j * 1024 + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(stage + j * 1024), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x3F70);  // vmcnt(0)
+    __syncthreads();
+    uint8_t* ob = g.p + (uint64_t)s * M * g.P;
+    for (uint32_t b = w; b < bps; b += 4) {
+      const uint32_t col = b * 64 + lane;
+      const uint32_t off = (col < g.cols ? col : g.cols - 1) * 16;
+      u32x4 x[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) x[c] = *reinterpret_cast<const u32x4*>(stage + (uint64_t)c * g.P + off);
+#pragma unroll
+      for (int r = 0; r < M; ++r) {
+        u32x4 y = x[r];
+#pragma unroll
+        for (int c = 0; c < K; ++c) y ^= x[c] * (r + 1);
+        st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+struct FRun {
+  const void* fn;
+  Geo g[2];
+  uint32_t grid, lds;
+  int i;
+};
+static void launch_frun(void* a) {
+  FRun* r = static_cast<FRun*>(a);
+  Geo g = r->g[r->i++ & 1];
+  void* args[] = {&g};
+  CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, r->lds, nullptr));
+}
+
+template <int K, int M>
+static void lds_geometry(int cus, uint32_t S, uint32_t N) {
+  const uint32_t P = (S + 255) / 256 * 256;
+  Geo g[2];
+  for (auto& x : g) {
+    uint8_t *d, *p;
+    CHECK(hipMalloc(&d, (size_t)N * K * P));
+    CHECK(hipMalloc(&p, (size_t)N * M * P));
+    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+  }
+  const uint32_t lds = K * P;
+  CHECK(hipFuncSetAttribute((const void*)&pF<K, M>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  const double alg = (double)N * S * (K + M);
+  for (int bpc : {1, 2}) {
+    if (bpc * lds > 160 * 1024) continue;
+    FRun r{(const void*)&pF<K, M>, {g[0], g[1]}, (uint32_t)(cus * bpc), lds, 0};
+    const float ms = time_it(launch_frun, &r, 10);
+    std::printf("RS(%d+%d) S=%u P=%u  F lds-stripe      bpc=%d  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", K, M, S, P, bpc,
+                alg / ms / 1e6, alg / ms / 1e6 / 80.0);
+  }
+  for (auto& x : g) {
+    CHECK(hipFree(const_cast<uint8_t*>(x.d)));
+    CHECK(hipFree(x.p));
+  }
+}
+
 // ---- the same patterns with the engine's GF(2^8) lookup arithmetic ----------------
 // E outputs x K inputs, 3 v_perm + 1.5 v_bitop3 per product (rs_kernels.hip), the
 // coefficient tables wave-uniform (kernel argument -> SGPRs).
@@ -368,8 +447,8 @@ static void launch_run(void* a) {
 }
 
 template <int K, int M>
-static void geometry(int cus, uint32_t S, uint32_t N) {
-  const uint32_t P = (S + 255) / 256 * 256;
+static void geometry(int cus, uint32_t S, uint32_t N, uint32_t pitch = 0, bool only_b = false) {
+  const uint32_t P = pitch ? pitch : (S + 255) / 256 * 256;
   Geo g[2];
   for (auto& x : g) {
     uint8_t *d, *p;
@@ -388,6 +467,7 @@ static void geometry(int cus, uint32_t S, uint32_t N) {
             {"D pipelined 1KiB", (const void*)&pD<K, M>},
             {"E stripe-per-wave", (const void*)&pE<K, M>}};
   for (auto& v : vs) {
+    if (only_b && v.fn != (const void*)&pB<K, M>) continue;
     for (int bpc : {2, 4, 8}) {
       Run r{v.fn, {g[0], g[1]}, (uint32_t)(cus * bpc), 0};
       const float ms = time_it(launch_run, &r, 10);
@@ -419,6 +499,20 @@ int main(int argc, char** argv) {
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   const bool only_copy = argc > 1 && argv[1][0] == 'c';
+  if (argc > 1 && argv[1][0] == 'f') {  // LDS-staged whole-stripe streaming
+    lds_geometry<10, 4>(cus, 6554, 16384);
+    lds_geometry<8, 4>(cus, 8192, 16384);
+    lds_geometry<4, 2>(cus, 16384, 16384);
+    lds_geometry<6, 3>(cus, 10923, 16384);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'p') {  // shard pitch sweep, pattern B
+    for (uint32_t P : {6656u, 6912u, 7168u, 7680u, 8192u, 10240u}) geometry<10, 4>(cus, 6554, 16384, P, true);
+    for (uint32_t P : {8192u, 8448u, 9216u, 10240u}) geometry<8, 4>(cus, 8192, 16384, P, true);
+    for (uint32_t P : {1024u, 1280u, 1536u, 2048u}) geometry<4, 2>(cus, 1024, 65536, P, true);
+    for (uint32_t P : {16384u, 16640u, 17408u}) geometry<4, 2>(cus, 16384, 16384, P, true);
+    return 0;
+  }
   if (argc > 1 && argv[1][0] == 'g') {
     compute_geometry<10, 4, 2>(cus, 6554, 16384);
     compute_geometry<10, 4, 4>(cus, 6554, 16384);
