@@ -30,10 +30,14 @@ import (
 // Service implements interfaces.IEcDriver on the GPU engine (ec.go:15-17).
 // Calls go through the engine's batch coalescer: concurrent request goroutines
 // with the same shard length share one device launch (group commit), while each
-// call keeps rs_encode / rs_reconstruct's exact contract.
+// call keeps rs_encode / rs_reconstruct's exact contract.  One Service drives
+// every MI355X of the node (rs_create_multi): the coalescer spreads its batches
+// over the GPUs.  On a host with no usable GPU, cpu is the reference's own codec
+// (klauspost, configured exactly as ec.go:26) and every call goes to it.
 type Service struct {
 	ctx *C.rs_ctx
 	co  *C.rs_coalescer
+	cpu reedsolomon.Encoder
 }
 
 // Keep klauspost's exported sentinels so errors.Is and %v output match ec.go.
@@ -61,10 +65,22 @@ func toErr(rc C.int) error {
 }
 
 // NewService replaces reedsolomon.New(config.K, config.M, ...) at ec.go:26.
+// Construction fails (log.Fatalf, as ec.go:27-29) only on invalid K/M or a GPU
+// runtime error; a GPU-less host gets the CPU codec instead.
 func NewService() interfaces.IEcDriver {
 	log.Println("--- Initializing EC Driver (Reed-Solomon, MI355X) ---")
 	var ctx *C.rs_ctx
-	if rc := C.rs_create(C.int(config.K), C.int(config.M), 0, 0, &ctx); rc != C.RS_OK {
+	rc := C.rs_create_multi(C.int(config.K), C.int(config.M), 0 /* every visible gfx950 GPU */, 0, &ctx)
+	if rc == C.RS_ERR_NO_DEVICE {
+		enc, err := reedsolomon.New(config.K, config.M, reedsolomon.WithAutoGoroutines(runtime.NumCPU()))
+		if err != nil {
+			log.Fatalf("Failed to create Reed-Solomon encoder: %v", err)
+		}
+		log.Printf("EC Driver loaded (k=%d, m=%d): no MI355X visible (%v), using klauspost/reedsolomon on the CPU\n",
+			config.K, config.M, toErr(rc))
+		return &Service{cpu: enc}
+	}
+	if rc != C.RS_OK {
 		log.Fatalf("Failed to create Reed-Solomon encoder: %v", toErr(rc))
 	}
 	var co *C.rs_coalescer
@@ -78,6 +94,9 @@ func NewService() interfaces.IEcDriver {
 // Split keeps klauspost's semantics in Go (no arithmetic): data shards alias
 // `data`, the short last shard and all parity shards are fresh zeroed slices.
 func (s *Service) Split(data []byte) ([][]byte, error) {
+	if s.cpu != nil {
+		return s.cpu.Split(data)
+	}
 	if len(data) == 0 {
 		return nil, reedsolomon.ErrShortData
 	}
@@ -117,6 +136,9 @@ func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, fu
 
 // Encode fills shards[K:] in place (ec.go:54-56).
 func (s *Service) Encode(shards [][]byte) error {
+	if s.cpu != nil {
+		return s.cpu.Encode(shards)
+	}
 	if len(shards) != config.K+config.M {
 		return reedsolomon.ErrTooFewShards
 	}
@@ -130,6 +152,9 @@ func (s *Service) Encode(shards [][]byte) error {
 // Reconstruct fills every empty entry, data and parity (ec.go:59-61;
 // readservice.go:285 and poller.go:282 rely on all nil entries being filled).
 func (s *Service) Reconstruct(shards [][]byte) error {
+	if s.cpu != nil {
+		return s.cpu.Reconstruct(shards)
+	}
 	if len(shards) != config.K+config.M {
 		return reedsolomon.ErrTooFewShards
 	}
@@ -173,6 +198,12 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 	t := config.K + config.M
 	errs = make([]error, len(objects))
+	if s.cpu != nil {
+		for i, shards := range objects {
+			errs[i] = s.cpu.Reconstruct(shards)
+		}
+		return errs
+	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	flat := make([][]byte, 0, len(objects)*t)

@@ -60,3 +60,35 @@ func TestGPUMatchesReferenceCPU(t *testing.T) {
 		}
 	}
 }
+
+// The same contract on a host with no GPU: NewService must not fail and must give
+// klauspost's own bytes (it IS klauspost there).  Run with HIP_VISIBLE_DEVICES=-1
+// (or ROCR_VISIBLE_DEVICES=-1) to hide the GPUs.
+func TestNoGPUFallsBackToKlauspost(t *testing.T) {
+	if testing.Short() {
+		t.Skip()
+	}
+	svc, ok := NewService().(*Service)
+	if !ok {
+		t.Fatal("NewService must return *Service")
+	}
+	if svc.cpu == nil {
+		t.Skip("a GPU is visible; hide it to exercise the fallback")
+	}
+	ref, _ := reedsolomon.New(config.K, config.M)
+	data := bytes.Repeat([]byte("A"), 1500*1024) // go-ycsb's hybridstore payload shape
+	want, _ := ref.Split(append([]byte(nil), data...))
+	_ = ref.Encode(want)
+	got, err := svc.Split(append([]byte(nil), data...))
+	if err != nil {
+		t.Fatal(err)
+	}
+	if err := svc.Encode(got); err != nil {
+		t.Fatal(err)
+	}
+	for i := range want {
+		if !bytes.Equal(got[i], want[i]) {
+			t.Fatalf("shard %d differs", i)
+		}
+	}
+}

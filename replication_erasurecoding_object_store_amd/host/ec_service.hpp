@@ -49,12 +49,14 @@ class IEcDriver {
 
 class Service final : public IEcDriver {
  public:
-  // ec.go:21 NewService(): RS(K, M) on the MI355X engine.  Unlike the reference
-  // (which can only fail on bad K/M and then log.Fatalf, ec.go:27-29), this can also
-  // report a missing GPU; the caller decides.
+  // ec.go:21 NewService(): RS(K, M) on the MI355X engine; device < 0 = one context
+  // over every visible GPU (rs_create_multi).  Unlike the reference (which can only
+  // fail on bad K/M and then log.Fatalf, ec.go:27-29), this can also report a
+  // missing GPU; the caller decides (the Go shim falls back to
+  // klauspost).
   static std::unique_ptr<Service> NewService(int k = K, int m = M, int device = 0, Error* err = nullptr) {
     rs_ctx* ctx = nullptr;
-    const int rc = rs_create(k, m, device, 0, &ctx);
+    const int rc = device < 0 ? rs_create_multi(k, m, 0, 0, &ctx) : rs_create(k, m, device, 0, &ctx);
     if (err) err->code = rc;
     if (rc != RS_OK) return nullptr;
     std::fprintf(stderr, "[EC Driver] Reed-Solomon k=%d m=%d on %s\n", k, m, rs_backend(ctx));
