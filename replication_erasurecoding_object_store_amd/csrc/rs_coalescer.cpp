@@ -12,12 +12,13 @@
 //
 //   caller i:  validate -> reserve slot i of the open batch for its S -> copy its
 //              shards into the batch's pinned staging (callers copy in parallel)
-//   leader  :  the batch's first caller waits until the batch is full or
-//              max_wait_us has passed, closes it, then moves it:
-//              H2D (data [n,K,P] (+ parity [n,M,P] if a reconstruct needs it) +
-//              masks) -> rs_reconstruct_batch_out with per-stripe masks (an encode
-//              is the pattern "all parity missing") or rs_verify_batch -> D2H
-//   caller i:  copies its outputs out of the staging batch and returns.
+//              -> sleep on the batch's completion word
+//   launcher:  (one thread per GPU) closes an open batch once fewer than max_exec
+//              of its GPU's batches are executing (group commit; optional
+//              max_wait_us linger) or it is full, and enqueues it: kernel on the
+//              pinned staging in place (zero-copy) or H2D -> kernel -> D2H
+//   completer: (one thread per GPU) waits for each launched batch and wakes its
+//              callers, who copy their outputs out of the staging and return.
 //
 // Up to `inflight` batches exist at once (each with its own stream, pinned and
 // device slab), so one batch's transfers overlap the next batch's filling.  All
@@ -34,11 +35,14 @@
 #include <unistd.h>
 
 #include <algorithm>
-#include <climits>
 #include <atomic>
+#include <climits>
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -78,15 +82,36 @@ struct Batch {
   std::atomic<uint64_t> key_S{0};     //   before `ticket` (read racily by the fast path)
   std::atomic<uint64_t> ticket{kClosedBit};
   std::atomic<uint32_t> parity_in{0};  // some slot needs its parity shards uploaded
-  size_t n_final = 0;          // slots of the closed batch (published by done_gen)
-  int rc = RS_OK;              // published by done_gen
+  size_t n_final = 0;          // slots of the closed batch (published by the group words)
+  int rc = RS_OK;              // published by the group words
   Clock::time_point deadline;
   // Lock-free completion: callers stage, wait and drain without the mutex, so a
   // finished batch of n callers does not turn into a convoy of n lock handoffs.
   std::atomic<uint32_t> filled{0};    // slots staged
   std::atomic<uint32_t> released{0};  // slots drained
-  std::atomic<uint32_t> done_gen{0};  // bumped (and futex-woken) when a run finishes
+  // Completion words, one per group of kGroup slots, each holding the epoch of the
+  // last batch run that finished for that group.  A caller sleeps on its first
+  // slot's group word until it reaches the caller's epoch (and marks the group as
+  // having a waiter of that epoch).  Groups are woken in order from `wake`
+  // ([epoch:32 | next group:32]): the completer wakes until two groups with
+  // waiters are up, then every woken caller does the same, so waking a batch of n
+  // callers costs the completer two groups' wake-ups instead of n and the rest fan
+  // out over the woken threads.  Groups nobody sleeps on (slots of a multi-object
+  // call) are advanced in passing and never end the chain.
+  //
+  // Everything is epoch-tagged because a waker may still be in the chain when the
+  // batch has drained, been recycled and reopened: a claim on `wake` succeeds only
+  // in the waker's own epoch, and group words only move forward, so a late waker
+  // can neither wake callers of a newer run early nor move a word back.
+  static constexpr uint32_t kGroup = 8;
+  uint32_t epoch = 0;                 // of the current open period (set in prepare, mu)
+  uint32_t n_groups_alloc = 0;        // fixed at creation: ceil(max cap / kGroup)
+  std::unique_ptr<std::atomic<uint32_t>[]> grp;
+  std::unique_ptr<std::atomic<uint32_t>[]> has_waiter;
+  std::atomic<uint64_t> wake{0};
+  std::atomic<uint32_t> wake_groups{0};
   hipStream_t stream = nullptr;
+  hipEvent_t done_ev = nullptr;       // recorded after the batch's last device op
   rs::PinnedBuf host;
   rs::DevBuf dev;
   // region offsets (same in host staging and device slab)
@@ -114,17 +139,60 @@ static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
 void futex_wait(std::atomic<uint32_t>* w, uint32_t expected) {
   syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAIT_PRIVATE, expected, nullptr, nullptr, 0);
 }
-void futex_wake_all(std::atomic<uint32_t>* w) {
-  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+void futex_wake(std::atomic<uint32_t>* w, int n) {
+  syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
 }
-// Waits until *w != v: a brief spin, then sleeps (callers may far outnumber cores,
-// so spinning long would steal the CPU the stragglers need to stage their shards).
-void wait_change(std::atomic<uint32_t>* w, uint32_t v) {
+// Epochs compare modulo 2^32 (prepare() keeps every live word within 2^30).
+bool epoch_reached(uint32_t word, uint32_t epoch) { return static_cast<int32_t>(word - epoch) >= 0; }
+
+// Moves a group word forward to `epoch` (never back).
+void advance_epoch(std::atomic<uint32_t>* w, uint32_t epoch) {
+  uint32_t cur = w->load(std::memory_order_relaxed);
+  while (!epoch_reached(cur, epoch) &&
+         !w->compare_exchange_weak(cur, epoch, std::memory_order_release, std::memory_order_relaxed)) {
+  }
+}
+
+// Waits until *w reaches `epoch`: a brief spin, then sleeps (callers may far
+// outnumber cores, so spinning long would steal the CPU the stragglers need to
+// stage their shards).
+void wait_epoch(std::atomic<uint32_t>* w, uint32_t epoch) {
   for (int i = 0; i < 64; ++i) {
-    if (w->load(std::memory_order_acquire) != v) return;
+    if (epoch_reached(w->load(std::memory_order_acquire), epoch)) return;
     __builtin_ia32_pause();
   }
-  while (w->load(std::memory_order_acquire) == v) futex_wait(w, v);
+  for (;;) {
+    const uint32_t v = w->load(std::memory_order_acquire);
+    if (epoch_reached(v, epoch)) return;
+    futex_wait(w, v);
+  }
+}
+
+// Per-GPU dispatch: a launcher thread closes open batches and launches them (at
+// most max_exec executing), a completer thread waits for each launched batch and
+// wakes its callers.  Callers only reserve, stage and sleep -- no caller thread is
+// on the launch critical path, so a descheduled caller never holds up a batch
+// (round 1's leader-caller design collapsed past ~256 callers on 16 cores:
+// profiles/r01_coalesce_hi.log).
+struct Dispatcher {
+  int engine = 0;
+  std::thread launcher, completer;
+  std::atomic<uint32_t> work{0};      // bumped on every event the launcher may act on
+  std::atomic<bool> launcher_idle{false};
+  std::atomic<int> executing{0};
+  std::mutex run_mu;
+  std::condition_variable run_cv;
+  std::deque<Batch*> running;         // launched, completion pending (launch order)
+  std::vector<Batch*> mine;           // this engine's batches
+};
+
+// Wakes the launcher if it sleeps.  The handshake with launcher_loop's sleep
+// (idle = true, then re-read work) is store -> load on both sides, so both are
+// sequentially consistent: with acquire / release alone x86 may reorder each
+// side's load before its store and both miss (a lost wake-up).
+void poke(Dispatcher* d) {
+  d->work.fetch_add(1, std::memory_order_seq_cst);
+  if (d->launcher_idle.load(std::memory_order_seq_cst)) futex_wake(&d->work, 1);
 }
 
 }  // namespace
@@ -138,22 +206,42 @@ struct rs_coalescer {
 
   int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
+  std::atomic<bool> stop{false};
 
   std::mutex mu;
-  std::condition_variable free_cv;    // a batch became free (or opened)
-  std::condition_variable leader_cv;  // batch full / an execution slot freed
+  std::condition_variable free_cv;    // a batch became free (back-pressure)
+  int free_waiters = 0;               // callers blocked on free_cv (mu)
   std::vector<std::unique_ptr<Batch>> batches;
   std::vector<Batch*> free_list;
   std::vector<int> engine_load;   // batches open or executing per engine (mu)
-  std::vector<int> engine_exec;   // batches executing per engine (mu)
   std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots (mu)
   std::atomic<uint64_t> hot{0};  // last opened batch: hot_word(gen, index); 0 = none
+  std::vector<std::unique_ptr<Dispatcher>> disp;  // one per engine
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
+  // diagnostics (printed at destroy when RS_CO_DEBUG is set)
+  std::atomic<uint64_t> straggle_ns{0}, exec_ns{0}, free_waits{0}, launches_idle{0};
 
   ~rs_coalescer() {
+    if (std::getenv("RS_CO_DEBUG"))
+      std::fprintf(stderr, "[rs_coalescer] batches %llu straggle_ms %.1f exec_ms %.1f free_waits %llu\n",
+                   (unsigned long long)n_batches.load(), straggle_ns.load() / 1e6, exec_ns.load() / 1e6,
+                   (unsigned long long)free_waits.load());
+    stop.store(true, std::memory_order_release);
+    for (auto& d : disp) {
+      poke(d.get());
+      d->launcher_idle.store(true);
+      futex_wake(&d->work, INT_MAX);
+      {
+        std::lock_guard<std::mutex> g(d->run_mu);
+        d->run_cv.notify_all();
+      }
+      if (d->launcher.joinable()) d->launcher.join();
+      if (d->completer.joinable()) d->completer.join();
+    }
     for (auto& b : batches) {
       rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(ctx, b->engine)));
+      if (b->done_ev) (void)hipEventDestroy(b->done_ev);
       if (b->stream) (void)hipStreamDestroy(b->stream);
       b.reset();  // slabs freed on their device
     }
@@ -175,7 +263,8 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
   rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, b->engine)));
   const size_t per = b->P * (k + 2 * m) + 8;
-  const size_t cap = std::max<size_t>(1, std::min(co->max_batch, co->max_bytes / per));
+  const size_t cap = std::max<size_t>(
+      1, std::min({co->max_batch, co->max_bytes / per, size_t(b->n_groups_alloc) * Batch::kGroup}));
   b->cap.store(cap, std::memory_order_relaxed);
   b->o_data = 0;
   b->o_parity = round_up(cap * k * b->P, 256);
@@ -184,7 +273,15 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->o_bad = b->o_masks + round_up(cap * 4, 256);
   b->bytes = b->o_bad + round_up(cap * 4, 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+  if (!b->done_ev) RS_HIP(hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming));
   if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
+  b->epoch += 1;
+  // Words of groups unused for ~2^30 runs would read as "reached" once the epoch
+  // wraps half-way round: pull them along (loads only, almost always).
+  const uint32_t groups = static_cast<uint32_t>((cap + Batch::kGroup - 1) / Batch::kGroup);
+  for (uint32_t g = 0; g < groups; ++g)
+    if (static_cast<uint32_t>(b->epoch - b->grp[g].load(std::memory_order_relaxed)) > (1u << 30))
+      advance_epoch(&b->grp[g], b->epoch - 1);
   b->filled.store(0, std::memory_order_relaxed);
   b->released.store(0, std::memory_order_relaxed);
   b->parity_in.store(0, std::memory_order_relaxed);
@@ -198,15 +295,16 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   return RS_OK;
 }
 
-// Runs a closed batch of n slots on its engine's stream and waits for the outputs.
-int execute(rs_coalescer* co, Batch* b, size_t n) {
+// Enqueues a closed batch of n slots on its engine's stream (H2D / kernel / D2H as
+// the staging mode needs) and records its completion event.  Asynchronous.
+int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
   const size_t k = co->k, m = co->m, P = b->P;
   rs::Engine* eng = rs::ctx_engine(co->ctx, b->engine);
   rs::DeviceScope ds(rs::engine_device(eng));
   hipStream_t st = b->stream;
   // Zero-copy (default): the staging is pinned host memory the GPU can address, so
   // the kernel reads the staged shards and writes its outputs there directly --
-  // one launch + one sync per batch instead of 3-4 DMA round trips.
+  // one launch per batch instead of 3-4 DMA round trips.
   void* hd = nullptr;
   const bool zc = co->zero_copy && hipHostGetDevicePointer(&hd, b->host.p, 0) == hipSuccess && hd;
   if (!zc) (void)hipGetLastError();
@@ -238,18 +336,10 @@ int execute(rs_coalescer* co, Batch* b, size_t n) {
     if (!zc)
       RS_HIP(hipMemcpyAsync(host_at(b, b->o_out), dev_at(b, b->o_out), n * m * P, hipMemcpyDeviceToHost, st));
   }
-  RS_HIP(hipStreamSynchronize(st));
+  RS_HIP(hipEventRecord(b->done_ev, st));
   return RS_OK;  // every mask was checked (>= k present) before it was staged
 }
 
-// One call through the coalescer.  fill(b, slot) stages the inputs, drain(b, slot)
-// copies the outputs back; both run outside the lock, in the caller's thread.
-//
-// Batching is group commit: a batch's leader starts it as soon as an execution slot
-// is free (at most max_exec batches on the device at once) and max_wait has passed
-// since the batch opened (default 0).  Callers that arrive while earlier batches
-// are on the device pile into the open batch, so batches grow with the load and a
-// lone caller pays no timer.
 uint64_t hot_word(uint32_t gen, int index) {
   return (static_cast<uint64_t>(gen) << 16) | static_cast<uint64_t>(index + 1);
 }
@@ -264,6 +354,132 @@ void unpublish(rs_coalescer* co, Batch* b, uint32_t gen) {
   if (h == mine) co->hot.compare_exchange_strong(h, 0, std::memory_order_relaxed);
 }
 
+// Wakes the next groups of run `epoch` of a finished batch until `limit` groups
+// with waiters are up (or none is left).  A no-op once the batch has moved on.
+void wake_more(Batch* b, uint32_t epoch, int limit) {
+  int woken = 0;
+  while (woken < limit) {
+    uint64_t w = b->wake.load(std::memory_order_acquire);
+    if (static_cast<uint32_t>(w >> 32) != epoch) return;
+    const uint32_t g = static_cast<uint32_t>(w);
+    if (g >= b->wake_groups.load(std::memory_order_acquire)) return;
+    if (!b->wake.compare_exchange_weak(w, w + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+    advance_epoch(&b->grp[g], epoch);
+    if (b->has_waiter[g].load(std::memory_order_acquire) == epoch) {
+      futex_wake(&b->grp[g], INT_MAX);
+      ++woken;
+    }
+  }
+}
+
+// Publishes a finished batch to its callers.
+void complete(rs_coalescer* co, Dispatcher* d, Batch* b, int rc) {
+  b->rc = rc;
+  co->n_batches.fetch_add(1, std::memory_order_relaxed);
+  co->stripes.fetch_add(b->n_final, std::memory_order_relaxed);
+  uint64_t seen = co->max_seen.load(std::memory_order_relaxed);
+  while (b->n_final > seen && !co->max_seen.compare_exchange_weak(seen, b->n_final)) {
+  }
+  const uint32_t epoch = b->epoch;
+  b->wake_groups.store(static_cast<uint32_t>((b->n_final + Batch::kGroup - 1) / Batch::kGroup),
+                       std::memory_order_relaxed);
+  b->wake.store(static_cast<uint64_t>(epoch) << 32, std::memory_order_release);
+  d->executing.fetch_sub(1, std::memory_order_acq_rel);
+  poke(d);  // an execution slot is free: the next batch may start before the wake-ups
+  wake_more(b, epoch, 2);
+}
+
+// Launcher: batching is group commit -- an open batch starts as soon as fewer than
+// max_exec batches of this GPU are executing and max_wait has passed since it
+// opened (default 0), or at once when full.  Callers arriving meanwhile pile into
+// it, so batches grow with the load and a lone caller waits for no timer.
+void launcher_loop(rs_coalescer* co, Dispatcher* d) {
+  for (;;) {
+    const uint32_t w = d->work.load(std::memory_order_acquire);
+    if (co->stop.load(std::memory_order_acquire)) return;
+    Batch* pick = nullptr;
+    Clock::time_point wake_at = Clock::time_point::max();
+    const bool slot = d->executing.load(std::memory_order_acquire) < co->max_exec;
+    for (Batch* b : d->mine) {
+      const uint64_t t = b->ticket.load(std::memory_order_acquire);
+      const size_t cnt = static_cast<size_t>(t & kCountMask);
+      if ((t & kClosedBit) || cnt == 0) continue;  // free, closed, or nobody in it yet
+      const bool full = cnt >= b->cap.load(std::memory_order_relaxed);
+      if (full || (slot && Clock::now() >= b->deadline)) {
+        if (!pick || full) pick = b;
+        if (full) break;
+      } else if (slot) {
+        wake_at = std::min(wake_at, b->deadline);
+      }
+    }
+    if (pick && (slot || d->executing.load(std::memory_order_acquire) < co->max_exec)) {
+      const uint64_t t = pick->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
+      const size_t n = static_cast<size_t>(t & kCountMask);
+      {
+        std::lock_guard<std::mutex> g(co->mu);
+        unpublish(co, pick, static_cast<uint32_t>(t >> kGenShift));
+      }
+      const auto ts0 = Clock::now();
+      for (int spin = 0; pick->filled.load(std::memory_order_acquire) < n; ++spin) {  // stragglers staging
+        if (spin < 4096)
+          __builtin_ia32_pause();
+        else
+          std::this_thread::yield();  // a preempted caller holds a slot: let it run
+      }
+      co->straggle_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - ts0).count(),
+                                std::memory_order_relaxed);
+      pick->n_final = n;
+      d->executing.fetch_add(1, std::memory_order_acq_rel);
+      const int rc = launch_batch(co, pick, n);
+      if (rc) {
+        complete(co, d, pick, rc);
+        continue;
+      }
+      std::lock_guard<std::mutex> g(d->run_mu);
+      d->running.push_back(pick);
+      d->run_cv.notify_one();
+      continue;
+    }
+    // nothing to start: sleep until a caller stages, a slot frees or a linger ends
+    d->launcher_idle.store(true, std::memory_order_seq_cst);
+    if (d->work.load(std::memory_order_seq_cst) == w && !co->stop.load(std::memory_order_acquire)) {
+      if (wake_at != Clock::time_point::max()) {
+        const auto ns = std::chrono::duration_cast<std::chrono::nanoseconds>(wake_at - Clock::now()).count();
+        if (ns > 0) {
+          timespec ts{static_cast<time_t>(ns / 1000000000), static_cast<long>(ns % 1000000000)};
+          syscall(SYS_futex, reinterpret_cast<uint32_t*>(&d->work), FUTEX_WAIT_PRIVATE, w, &ts, nullptr, 0);
+        }
+      } else {
+        futex_wait(&d->work, w);
+      }
+    }
+    d->launcher_idle.store(false, std::memory_order_release);
+  }
+}
+
+// Completer: waits for each launched batch in launch order and wakes its callers.
+void completer_loop(rs_coalescer* co, Dispatcher* d) {
+  rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, d->engine)));
+  for (;;) {
+    Batch* b = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(d->run_mu);
+      d->run_cv.wait(lk, [&] { return !d->running.empty() || co->stop.load(std::memory_order_acquire); });
+      if (d->running.empty()) return;  // stopping with nothing in flight
+      b = d->running.front();
+      d->running.pop_front();
+    }
+    const auto t0 = Clock::now();
+    const int rc = hipEventSynchronize(b->done_ev) == hipSuccess ? RS_OK : RS_ERR_DEVICE;
+    co->exec_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
+                          std::memory_order_relaxed);
+    complete(co, d, b, rc);
+  }
+}
+
+// One call through the coalescer.  fill(b, slot, item) stages the inputs,
+// drain(b, slot, item) copies the outputs back; both run in the caller's thread,
+// outside any lock.
 template <class Fill, class Drain>
 int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity_in, Fill&& fill, Drain&& drain) {
   const auto key = std::make_pair(static_cast<int>(kind), S);
@@ -284,9 +500,8 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
         gen = hg;
       }
     }
-    std::unique_lock<std::mutex> lk(co->mu, std::defer_lock);
     if (!b) {
-      lk.lock();
+      std::unique_lock<std::mutex> lk(co->mu);
       for (;;) {
         auto it = co->open.find(key);
         if (it != co->open.end()) {
@@ -311,84 +526,46 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
           if (rc) {
             nb->free = true;
             co->free_list.push_back(nb);
-            co->free_cv.notify_all();
+            if (co->free_waiters) co->free_cv.notify_one();
             return rc;
           }
           ++co->engine_load[nb->engine];
-          take = try_reserve(nb, nb->gen, want, &slot0);  // slot 0: this caller leads
+          take = try_reserve(nb, nb->gen, want, &slot0);
           b = nb;
           gen = nb->gen;
           co->open[key] = nb;
           co->hot.store(hot_word(gen, nb->index), std::memory_order_release);
-          co->free_cv.notify_all();  // waiters for this S may join it
           break;
         }
-        co->free_cv.wait(lk);  // every batch is in flight: back-pressure
+        ++co->free_waiters;  // every batch is in flight: back-pressure
+        co->free_waits.fetch_add(1, std::memory_order_relaxed);
+        co->free_cv.wait(lk);
+        --co->free_waiters;
       }
-      lk.unlock();
     }
-    const bool leader = slot0 == 0;
-    const uint32_t dgen = b->done_gen.load(std::memory_order_relaxed);
+    (void)gen;
+    // the epoch was set before the ticket opened (acquired by the reservation)
+    const uint32_t epoch = b->epoch;
+    const uint32_t grp = static_cast<uint32_t>(slot0 / Batch::kGroup);
+    b->has_waiter[grp].store(epoch, std::memory_order_release);  // before `filled`: seen by the waker
     if (parity_in) b->parity_in.store(1, std::memory_order_relaxed);
-    if (slot0 + take == b->cap.load(std::memory_order_relaxed)) {  // took the last slot: close it
-      b->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
-      lk.lock();
-      unpublish(co, b, gen);
-      co->leader_cv.notify_all();
-      lk.unlock();
-    }
     for (size_t j = 0; j < take; ++j) fill(b, slot0 + j, done_items + j);
     b->filled.fetch_add(static_cast<uint32_t>(take), std::memory_order_release);
-    if (leader) {
-      lk.lock();
-      // gather: until full, or (an execution slot is free and the linger is over)
-      int& exec = co->engine_exec[b->engine];
-      for (;;) {
-        if (b->ticket.load(std::memory_order_acquire) & kClosedBit) break;
-        const bool slot_free = exec < co->max_exec;
-        if (slot_free && Clock::now() >= b->deadline) break;
-        if (slot_free)
-          co->leader_cv.wait_until(lk, b->deadline);
-        else
-          co->leader_cv.wait(lk);
-      }
-      const uint64_t t = b->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
-      const size_t n = static_cast<size_t>(t & kCountMask);
-      unpublish(co, b, gen);
-      while (exec >= co->max_exec) co->leader_cv.wait(lk);
-      ++exec;
-      lk.unlock();
-      while (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();  // stragglers staging
-      b->n_final = n;
-      const int rc = execute(co, b, n);
-      co->n_batches.fetch_add(1, std::memory_order_relaxed);
-      co->stripes.fetch_add(n, std::memory_order_relaxed);
-      uint64_t seen = co->max_seen.load(std::memory_order_relaxed);
-      while (n > seen && !co->max_seen.compare_exchange_weak(seen, n)) {
-      }
-      lk.lock();
-      --exec;
-      co->leader_cv.notify_all();  // an execution slot is free
-      lk.unlock();
-      b->rc = rc;
-      b->done_gen.fetch_add(1, std::memory_order_release);
-      futex_wake_all(&b->done_gen);
-    } else {
-      wait_change(&b->done_gen, dgen);
-    }
+    poke(co->disp[static_cast<size_t>(b->engine)].get());
+    wait_epoch(&b->grp[grp], epoch);
+    wake_more(b, epoch, 2);
     const int rc = b->rc;
-    const size_t n = b->n_final;  // published by done_gen
+    const size_t n = b->n_final;  // published by the group word (release / acquire)
     if (rc == RS_OK)
       for (size_t j = 0; j < take; ++j) drain(b, slot0 + j, done_items + j);
     else if (result == RS_OK)
       result = rc;
     if (b->released.fetch_add(static_cast<uint32_t>(take), std::memory_order_acq_rel) + take == n) {
-      lk.lock();
+      std::lock_guard<std::mutex> g(co->mu);
       b->free = true;
       --co->engine_load[b->engine];
       co->free_list.push_back(b);
-      co->free_cv.notify_all();
-      lk.unlock();
+      if (co->free_waiters) co->free_cv.notify_one();
     }
     done_items += take;
   }
@@ -518,14 +695,34 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
   co->engine_load.assign(static_cast<size_t>(ne), 0);
-  co->engine_exec.assign(static_cast<size_t>(ne), 0);
+  // the most slots a batch can hold: max_batch, bounded by the bytes budget at
+  // the smallest slot (16-B shards) and by 2^20
+  const size_t max_cap = std::max<size_t>(
+      1, std::min({o.max_batch, o.max_batch_bytes / (16 * static_cast<size_t>(co->k + 2 * co->m) + 8),
+                   size_t(1) << 20}));
+  for (int e = 0; e < ne; ++e) {
+    co->disp.push_back(std::make_unique<Dispatcher>());
+    co->disp.back()->engine = e;
+  }
   for (int i = 0; i < o.inflight; ++i) {
     co->batches.push_back(std::make_unique<Batch>());
     Batch* b = co->batches.back().get();
     b->index = i;
     b->engine = i % ne;
+    b->n_groups_alloc = static_cast<uint32_t>((max_cap + Batch::kGroup - 1) / Batch::kGroup);
+    b->grp.reset(new std::atomic<uint32_t>[b->n_groups_alloc]);
+    b->has_waiter.reset(new std::atomic<uint32_t>[b->n_groups_alloc]);
+    for (uint32_t g = 0; g < b->n_groups_alloc; ++g) {
+      b->grp[g].store(0, std::memory_order_relaxed);
+      b->has_waiter[g].store(0, std::memory_order_relaxed);
+    }
     b->host.numa = rs::device_numa_node(rs::engine_device(rs::ctx_engine(ctx, b->engine)));
     co->free_list.push_back(b);
+    co->disp[static_cast<size_t>(b->engine)]->mine.push_back(b);
+  }
+  for (auto& d : co->disp) {
+    d->launcher = std::thread(launcher_loop, co.get(), d.get());
+    d->completer = std::thread(completer_loop, co.get(), d.get());
   }
   *out = co.release();
   return RS_OK;

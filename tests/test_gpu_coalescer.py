@@ -222,3 +222,33 @@ def test_reservation_stress(gpu, max_batch, inflight):
         assert st["max_batch"] <= max_batch
     finally:
         svc.close()
+
+
+def test_many_and_single_callers_share_batches(gpu):
+    """Multi-object calls (one caller holding many slots, so whole wake-up groups
+    with no sleeper) interleaved with single-object callers in the same batches:
+    every caller must be woken and get its own bytes."""
+    svc = CoalescingService(4, 2, max_batch=64, max_wait_us=200, inflight=4)
+    try:
+        def worker(t):
+            for j in range(20):
+                if t % 4 == 0:
+                    objs = [rs_oracle.split(4, 2, xoshiro_bytes(t * 1000 + j * 50 + i, 4096)) for i in range(13)]
+                    mine = [[bytearray(s) for s in o] for o in objs]
+                    assert svc.EncodeMany(mine) == [None] * 13
+                    for o, got in zip(objs, mine):
+                        rs_oracle.encode(4, 2, o)
+                        assert [bytes(s) for s in got] == [bytes(s) for s in o]
+                else:
+                    data = xoshiro_bytes(t * 1000 + j, 4096)
+                    sh = svc.Split(data)
+                    svc.Encode(sh)
+                    ref = rs_oracle.split(4, 2, data)
+                    rs_oracle.encode(4, 2, ref)
+                    assert [bytes(s) for s in sh] == [bytes(s) for s in ref]
+
+        _run_threads(48, worker)
+        st = svc.stats()
+        assert st["stripes"] == 12 * 20 * 13 + 36 * 20
+    finally:
+        svc.close()
