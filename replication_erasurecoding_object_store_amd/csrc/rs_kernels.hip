@@ -162,8 +162,63 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
 }
 
 // ---------------------------------------------------------------------------
+// Rows [R0, R0 + NR) of one task: y[r] = sum_c C[R0 + r][c] (x) x[c].
+// Input-outer order (as upstream codeSomeShards): one input's chunk indices and
+// NR x 5 table dwords live at a time; products of inputs c-1 and c are folded into
+// the accumulator with one 3-input XOR.  The scheduling barrier per input stops the
+// compiler from hoisting every input's tables into SGPRs at once (K*NR*5 dwords,
+// e.g. 100 for RS(10+4) x 2 rows -> SGPR spills through VGPR lanes).
+template <int K, int M, int R0, int NR>
+__device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K], u32x4 (&y)[NR]) {
+  u32x4 pend[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    Idx3 ix[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+    // one opaque base per input: the scalar load merger cannot fuse this input's
+    // table loads with later inputs' (which would pin them in SGPRs)
+    const uint8_t* tcol = plan;
+    if constexpr (K * NR * 5 > 48) asm volatile("" : "+s"(tcol));
+    const PlanView pc(tcol, K, M);
+    auto row = [&](auto r_tag) {
+      constexpr int r = decltype(r_tag)::value;
+      const RS_CONST uint32_t* tb = pc.quad(R0 + r, c);
+      const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(R0 + r, c);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
+        if (c & 1)
+          y[r][d] = xor3(y[r][d], pend[r][d], prod);
+        else if (c == K - 1)
+          y[r][d] ^= prod;
+        else
+          pend[r][d] = prod;
+      }
+    };
+    row(std::integral_constant<int, 0>{});
+    if constexpr (NR > 1) row(std::integral_constant<int, 1>{});
+    if constexpr (NR > 2) row(std::integral_constant<int, 2>{});
+    if constexpr (NR > 3) row(std::integral_constant<int, 3>{});
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
 // #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
+//
+// Per-stripe batches sized for E > 2 outputs compute in two passes over the same
+// K loaded inputs: rows 0-1, then rows 2..E-1 only when the stripe misses more
+// than two shards -- so only two rows' accumulators and one input's chunk indices
+// are ever live (RS(10+4): 160 -> ~70 VGPRs, occupancy 3 -> 7) and a 1- or
+// 2-erasure stripe does no work for rows 2..E-1.  (Skipping row 1 for 1-erasure
+// stripes as well measured slower: the second code version costs occupancy,
+// profiles/r02_ab_row_passes.log.)  Every trip issues the same loads and stores (dropped when
+// not live); the wave-uniform branches hold VALU work only, so the compiler's
+// vmcnt bookkeeping stays exact across them.
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -173,6 +228,8 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;      // bytes of a partial last column (0: none)
+  constexpr int E1 = (PER_STRIPE && E > 2) ? 2 : E;  // rows of the first pass
+  constexpr int E2 = E - E1;                         // rows of the second pass
   uint32_t bad = 0u;
 
   // mask of task t's stripe; every lane loads the same word (one request)
@@ -196,7 +253,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     }
-    if constexpr (K * E * 5 > 48) {
+    if constexpr (K * E1 * 5 > 48) {
       // Too many table dwords to keep resident in SGPRs across trips: make the plan
       // pointer opaque per trip so its loads are not hoisted out of the loop (LICM
       // would otherwise spill them through VGPR lanes: v_writelane/v_readlane).
@@ -213,66 +270,32 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
 #pragma unroll
     for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
 
-    // input-outer order (as upstream codeSomeShards): one input's chunk indices
-    // and E x 5 table dwords live at a time.  Products of inputs c-1 and c are
-    // folded into the accumulator with one 3-input XOR.  The scheduling barrier
-    // per input stops the compiler from hoisting every input's tables into SGPRs
-    // at once (K*E*5 dwords: 200 for RS(10+4) -> SGPR spills through VGPR lanes).
-    u32x4 y[E], pend[E];
+    u32x4 y[E];
+    {
+      u32x4 y1[E1];
+      gf_rows<K, M, 0, E1>(plan, x, y1);
 #pragma unroll
-    for (int r = 0; r < E; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
-    // Per-stripe batches carry mixed patterns: rows [kLo, E) are only computed
-    // when this task's plan fills more than kLo shards (a wave-uniform branch per
-    // input), so e.g. 2-erasure stripes in an RS(10+4) batch sized for 4 outputs
-    // do half the lookups.  Skipped rows' stores are dropped.
-    constexpr int kLo = (PER_STRIPE && E >= 4) ? E / 2 : E;
-    constexpr int kLo1 = kLo < E ? 1 : kLo;  // rows [kLo1, kLo) when n_out > kLo1
-    const bool hi_rows = kLo == E || pv.n_out() > static_cast<uint32_t>(kLo);
-    const bool mid_rows = kLo1 == kLo || pv.n_out() > static_cast<uint32_t>(kLo1);
+      for (int r = 0; r < E1; ++r) y[r] = y1[r];
+    }
+    if constexpr (E2 > 0) {
+      u32x4 z[E2];
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
-      Idx3 ix[4];
+      for (int r = 0; r < E2; ++r) z[r] = y[0];  // dropped unless computed below
+      if (pv.n_out() > static_cast<uint32_t>(E1)) {
+        const uint8_t* p2 = plan;  // the second pass's tables load inside the branch
+        asm volatile("" : "+s"(p2));
+        // opaque inputs: the chunk indices are recomputed here, not kept live from
+        // the first pass (K x 12 VGPRs -> occupancy 3)
+        u32x4 x2[K];
 #pragma unroll
-      for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
-      // one opaque base per input: the scalar load merger cannot fuse this
-      // input's table loads with later inputs' (which would pin them in SGPRs)
-      const uint8_t* tcol = plan;
-      if constexpr (K * E * 5 > 48) asm volatile("" : "+s"(tcol));
-      const PlanView pc(tcol, K, M);
-      auto rows = [&](auto lo_tag, auto hi_tag, const PlanView& pt) {
-        constexpr int R0 = decltype(lo_tag)::value, R1 = decltype(hi_tag)::value;
-#pragma unroll
-        for (int r = R0; r < R1; ++r) {
-          const RS_CONST uint32_t* tb = pt.quad(r, c);
-          const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pt.c4(r, c);
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
-            if (c & 1)
-              y[r][d] = xor3(y[r][d], pend[r][d], prod);
-            else if (c == K - 1)
-              y[r][d] ^= prod;
-            else
-              pend[r][d] = prod;
-          }
+        for (int c = 0; c < K; ++c) {
+          x2[c] = x[c];
+          asm volatile("" : "+v"(x2[c]));
         }
-      };
-      rows(std::integral_constant<int, 0>{}, std::integral_constant<int, kLo1>{}, pc);
-      if constexpr (kLo1 < kLo) {
-        if (mid_rows) {
-          const uint8_t* tmid = plan;
-          asm volatile("" : "+s"(tmid));
-          rows(std::integral_constant<int, kLo1>{}, std::integral_constant<int, kLo>{}, PlanView(tmid, K, M));
-        }
+        gf_rows<K, M, E1, E2>(p2, x2, z);
       }
-      if constexpr (kLo < E) {
-        if (hi_rows) {
-          const uint8_t* thi = plan;  // the high rows' tables load inside the branch
-          asm volatile("" : "+s"(thi));
-          rows(std::integral_constant<int, kLo>{}, std::integral_constant<int, E>{}, PlanView(thi, K, M));
-        }
-      }
-      if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < E2; ++r) y[E1 + r] = z[r];
     }
     const uint32_t n_out = pv.n_out();
 #pragma unroll
@@ -371,6 +394,9 @@ struct BsNet {
 };
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_step(const uint32_t (&x)[8], uint32_t (&y)[8 * M]);
+// Prefix programs (parity rows 0..R-1 only) for the bitsliced reconstruct kernel.
+template <int K, int M, int R, int C>
+__device__ __forceinline__ void bs_pstep(const uint32_t (&x)[8], uint32_t (&y)[8 * R]);
 
 #include "rs_xor_networks.inc"
 

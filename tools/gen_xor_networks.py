@@ -26,6 +26,9 @@ import os
 from collections import Counter
 
 SHAPES = [(4, 2), (8, 4), (10, 4), (6, 3)]
+# shapes that also get prefix programs (parity rows 0..R-1, R = 1..M) for the
+# bitsliced reconstruct kernel
+PREFIX_SHAPES = [(8, 4), (10, 4)]
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "replication_erasurecoding_object_store_amd", "csrc", "rs_xor_networks.inc")
 
@@ -84,7 +87,7 @@ def parity_rows(k: int, m: int):
 # ---- XOR programs ---------------------------------------------------------------
 def input_rows(rows, k, m, c):
     """For input c: output plane p = (r*8 + i) needs XOR of planes {j : bit i of
-    f_rc * 2^j}."""
+    f_rc * 2^j}, for the first m parity rows."""
     out = []
     for r in range(m):
         f = rows[r][c]
@@ -120,11 +123,16 @@ def paar(subsets):
     return temps, rows
 
 
-def emit_step(k, m, c, rows):
-    subsets = input_rows(rows, k, m, c)
+def emit_step(k, m, c, rows, r_rows=None):
+    """Step of input c.  r_rows=None: the full encode program bs_step<k, m, c>
+    (all m rows); r_rows=R: the prefix program bs_pstep<k, m, R, c> over parity
+    rows 0..R-1 only (the reconstruct kernel's syndrome / re-encode rows)."""
+    nr = m if r_rows is None else r_rows
+    subsets = input_rows(rows, k, nr, c)
     temps, red = paar(subsets)
-    lines = [f"template <> __device__ __forceinline__ void bs_step<{k}, {m}, {c}>(const uint32_t (&x)[8], "
-             f"uint32_t (&y)[{8 * m}]) {{"]
+    head = (f"bs_step<{k}, {m}, {c}>" if r_rows is None else f"bs_pstep<{k}, {m}, {r_rows}, {c}>")
+    lines = [f"template <> __device__ __forceinline__ void {head}(const uint32_t (&x)[8], "
+             f"uint32_t (&y)[{8 * nr}]) {{"]
     nx = 0
     for name, a, b in temps:
         lines.append(f"  const uint32_t {name} = {a.replace('x', 'x[') + ']' if a[0] == 'x' else a} ^ "
@@ -167,6 +175,17 @@ def main():
             total += nx
         out.append("")
         summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column")
+        if (k, m) in PREFIX_SHAPES:
+            pre = []
+            for r_rows in range(1, m + 1):
+                n_r = 0
+                for c in range(k):
+                    lines, nx = emit_step(k, m, c, rows, r_rows)
+                    out += lines
+                    n_r += nx
+                pre.append(f"{r_rows} rows {n_r}")
+            out.append("")
+            summary.append(f"RS({k}+{m}) prefix programs: " + ", ".join(pre))
     out.insert(3, "// " + "; ".join(summary))
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
