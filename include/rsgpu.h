@@ -244,6 +244,10 @@ int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *
 /* Tuning knob: workgroups (256 threads) per CU for the batched kernels
  * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
+/* Tuning knob: kernel family for the batched encode / reconstruct (0 = by shape,
+ * 1 = grid-stride kernels, 2 / 3 = pipelined kernel with 2 / 3 task slots per wave;
+ * shapes without a specialisation always run the generic kernel). */
+int rs_set_kernel_variant(rs_ctx *ctx, int variant);
 /* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or
  * rs_host_register) and 16-B aligned run zero-copy by default: the kernel reads
  * the survivors and writes the missing shards across PCIe in place.  0 forces

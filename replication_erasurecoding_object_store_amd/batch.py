@@ -217,3 +217,7 @@ class BatchEngine(Service):
 
     def set_blocks_per_cu(self, n: int) -> None:
         _check(_lib.lib().rs_set_blocks_per_cu(self.ctx, n))
+
+    def set_kernel_variant(self, v: int) -> None:
+        """0 = by shape, 1 = grid-stride kernels, 2/3 = pipelined (2/3 task slots)."""
+        _check(_lib.lib().rs_set_kernel_variant(self.ctx, v))

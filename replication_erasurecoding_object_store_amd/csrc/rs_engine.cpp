@@ -116,6 +116,22 @@ using rs::round_up;
 // until the per-byte VALU work (K*E lookups) needs more waves to hide latency.
 int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
 
+// Default kernel family per shape (rs_set_kernel_variant): 1 = grid-stride
+// apply / bitsliced encode, 2 / 3 = pipelined with 2 / 3 task slots per wave.
+// RS_KERNEL_VARIANT=<1..3> in the environment overrides it (tests run the whole
+// suite on each family).
+int default_variant(int k, int e, bool per_stripe) {
+  static const int forced = [] {
+    const char* v = std::getenv("RS_KERNEL_VARIANT");
+    return v ? std::atoi(v) : 0;
+  }();
+  if (forced >= 1 && forced <= 3) return forced;
+  (void)k;
+  (void)e;
+  (void)per_stripe;
+  return 1;
+}
+
 // ---- plan construction -----------------------------------------------------
 // 3-chunk v_perm tables for coefficient f (see rs_kernels.hip):
 //   A[v] = f*v (v<8), B[v] = f*(v<<3) (v<8), C[v] = f*(v<<6) (v<4).
@@ -145,15 +161,9 @@ std::vector<uint8_t> make_plan(int k, int m, uint32_t present, uint32_t out_mask
   uint32_t* ii = reinterpret_cast<uint32_t*>(p.data() + 16);
   for (int c = 0; c < k; ++c) ii[c] = static_cast<uint32_t>(in_idx[c]);
   for (size_t r = 0; r < out_idx.size(); ++r) ii[k + r] = static_cast<uint32_t>(out_idx[r]);
-  uint32_t* quad = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
-  uint32_t* c4 = reinterpret_cast<uint32_t*>(p.data() + rs::plan_c4_offset(k, m));
+  uint32_t* tab = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
   for (size_t r = 0; r < out_idx.size(); ++r)
-    for (int c = 0; c < k; ++c) {
-      uint32_t t[5];
-      perm_tables(rows[r * k + c], t);
-      std::memcpy(quad + (r * k + c) * 4, t, 16);
-      c4[r * k + c] = t[4];
-    }
+    for (int c = 0; c < k; ++c) perm_tables(rows[r * k + c], tab + (c * m + r) * 5);
   return p;
 }
 
@@ -264,6 +274,7 @@ struct Engine {
   const std::vector<uint32_t>* h_lut = nullptr;
   Shared* shared = nullptr;
   int blocks_per_cu = 0;                  // 0 = by shape
+  int variant = 0;                        // kernel family (rs_set_kernel_variant): 0 = by shape
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   std::string name;
@@ -460,9 +471,10 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   // the encode plan with a verified generated XOR program -> bitsliced kernel
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.status = per_stripe ? status_word(e, s) : nullptr;
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
-  const char* name =
-      rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s, false);
+  const int variant = e->variant > 0 ? e->variant : default_variant(e->k, e_out, per_stripe);
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : (variant >= 2 ? 1 : default_blocks_per_cu(e->k, e_out));
+  const char* name = rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc),
+                                      static_cast<uint32_t>(e->cu_count), s, false, variant);
   if (!name) return RS_ERR_DEVICE;
   e->shared->last_kernel.store(name);
   RS_HIP(hipGetLastError());
@@ -1411,6 +1423,12 @@ int rs_set_host_zero_copy(rs_ctx* c, int enable) {
 }
 
 const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_path.load() : "none"; }
+
+int rs_set_kernel_variant(rs_ctx* c, int variant) {
+  if (!c || variant < 0 || variant > 3) return RS_ERR_INVALID_ARG;
+  for (auto& e : c->engines) e->variant = variant;  // 0 = by shape
+  return RS_OK;
+}
 
 int rs_set_blocks_per_cu(rs_ctx* c, int bpc) {
   if (!c || bpc < 0) return RS_ERR_INVALID_ARG;

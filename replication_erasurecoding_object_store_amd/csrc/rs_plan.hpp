@@ -11,9 +11,9 @@
 //   u32 n_out; u32 present; u32 out_mask; u32 reserved; u32 in_idx[K]; u32 out_idx[M];
 //   pad to 16;   (present: the shards the plan reads from; out_mask: the shards it
 //                 may fill -- all, or the data shards for ReconstructData)
-//   u32x4 quad[M][K]  -- per coefficient f: 3-chunk v_perm tables {A_lo, A_hi, B_lo,
-//                        B_hi} (see rs_kernels.hip), 16-B aligned for ds_read_b128
-//   u32   c4[M][K]    -- per coefficient f: C_lo
+//   u32 tab[K][M][5]  -- per coefficient f = C[r][c]: the 3-chunk v_perm tables
+//                        {A_lo, A_hi, B_lo, B_hi, C_lo} (see rs_kernels.hip), input-major
+//                        so one input's E rows are one contiguous scalar load
 // The kernels derive the input / output slots from the present mask itself (first
 // K present in index order / every missing one), which is exactly how these plans
 // are built; in_idx / out_idx are kept for the generic kernel and for checks.
@@ -35,11 +35,8 @@ constexpr uint32_t kColumnWindow = 1u << 30;
 __host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
   return (16u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
 }
-__host__ __device__ constexpr uint32_t plan_c4_offset(int k, int m) {
-  return plan_tab_offset(k, m) + 16u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m);
-}
 __host__ __device__ constexpr uint32_t plan_stride(int k, int m) {
-  return (plan_c4_offset(k, m) + 4u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) & ~15u;
+  return (plan_tab_offset(k, m) + 20u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) & ~15u;
 }
 
 // Plans, masks and LUT are written by the host before a launch and never by a
@@ -66,9 +63,9 @@ struct PlanView {
   __host__ __device__ uint32_t out_idx(int r) const { return as_const<uint32_t>(p + 16 + 4 * k)[r]; }
   // the five table dwords of coefficient (r, c): quad(r, c)[0..3] and c4(r, c)
   __host__ __device__ const RS_CONST uint32_t* quad(int r, int c) const {
-    return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (r * k + c) * 4;
+    return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (c * m + r) * 5;
   }
-  __host__ __device__ uint32_t c4(int r, int c) const { return as_const<uint32_t>(p + plan_c4_offset(k, m))[r * k + c]; }
+  __host__ __device__ uint32_t c4(int r, int c) const { return quad(r, c)[4]; }
 };
 
 // Shard slot s of stripe i lives at
@@ -107,8 +104,10 @@ const uint8_t* bitsliced_encode_rows(int k, int m);
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
 // e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or
 // nullptr if the launch failed.  Any shard_len up to 0xFFFFFFF0 (column windows).
+// variant: 0/1 grid-stride kernels (apply / bitsliced encode), 2/3 pipelined kernel
+// with 2/3 task slots per wave (specialised shapes only).
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
-                         uint32_t cu_count, hipStream_t s, bool force_generic);
+                         uint32_t cu_count, hipStream_t s, bool force_generic, int variant);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.

@@ -82,6 +82,7 @@ def main():
     bpcs = [int(b) for b in args.bpc.split(",")]
     results = {}
     engines = {}
+    knames, digests = {}, {}
     pads = [int(x) for x in args.pads.split(",")]
     if pads != [0]:
         workloads = {(f"{n}+{pad}" if pad else n): (*w, pad) for n, w in workloads.items() for pad in pads}
@@ -151,6 +152,7 @@ def main():
         for rnd in range(args.rounds):
             for v in variants:
                 for bpc in bpcs:
+                    eng.set_kernel_variant(v)
                     eng.set_blocks_per_cu(bpc)
                     for i in range(2):
                         run(i)
@@ -163,12 +165,19 @@ def main():
                     torch.cuda.synchronize()
                     ms = e0.elapsed_time(e1) / args.iters
                     results.setdefault((name, v, bpc), []).append(alg / (ms * 1e-3) / 1e9)
-                    kname = eng.last_kernel()
+                    knames[(v, bpc)] = eng.last_kernel()
+                    # outputs of buffer 0 under this variant (must agree across variants)
+                    run(0)
+                    torch.cuda.synchronize()
+                    o = outs[0] if outs else (bufs[0][1] if mode == "enc" else
+                                              (bad if mode == "ver" else torch.cat([bufs[0][0], bufs[0][1]], 1)))
+                    digests.setdefault(name, set()).add(hash(o.cpu().numpy().tobytes()))
         eng.sync()
         # correctness spot check after all variants: stripes reconstruct to the encoded bytes
         d, p = bufs[0]
         chk = torch.empty_like(p[:256])
         eng.set_blocks_per_cu(0)
+        eng.set_kernel_variant(0)
         eng.encode(d[:256], chk, S, 256)
         torch.cuda.synchronize()
         ok = bool(torch.equal(chk[:, :, :S], p[:256, :, :S]))
@@ -176,8 +185,9 @@ def main():
             for bpc in bpcs:
                 r = results[(name, v, bpc)]
                 print(f"{name:18s} v{v} bpc={bpc:2d}: median {np.median(r):7.1f} GB/s  max {np.max(r):7.1f}  "
-                      f"({np.median(r) / 8000 * 100:4.1f}% of 8 TB/s)  {kname if v == variants[-1] else ''}", flush=True)
-        print(f"{name:18s} parity-consistent after all runs: {ok}", flush=True)
+                      f"({np.median(r) / 8000 * 100:4.1f}% of 8 TB/s)  {knames[(v, bpc)]}", flush=True)
+        print(f"{name:18s} parity-consistent after all runs: {ok}; variants agree on outputs: "
+              f"{len(digests[name]) == 1}", flush=True)
         del bufs, masks
         torch.cuda.empty_cache()
 

@@ -171,6 +171,28 @@ __global__ __launch_bounds__(256) void pE(Geo g) {
 
 static float time_it(void (*launch)(void*), void* arg, int iters);
 
+// Input fill: constant 0x01 bytes (the round-1/2 default) or, with "rand" as the
+// second argument, splitmix64 pseudo-random bytes -- DVFS and the DRAM bus both
+// see the data, so ceilings are quoted on random data too.
+static bool g_random = false;
+__global__ void fill_rand(uint64_t* p, uint64_t n8, uint64_t seed) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256) {
+    uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = z ^ (z >> 31);
+  }
+}
+static void fill(void* p, size_t bytes) {
+  if (!g_random) {
+    CHECK(hipMemset(p, 1, bytes));
+    return;
+  }
+  hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, nullptr, static_cast<uint64_t*>(p), bytes / 8,
+                     reinterpret_cast<uint64_t>(p));
+  CHECK(hipDeviceSynchronize());
+}
+
 // F: one workgroup per stripe at a time: the stripe's K data shards (one contiguous
 // K*P-byte region in the split layout) stream into LDS with LDS-DMA (1 KiB per
 // wave-instruction, in address order), then the waves compute column blocks from
@@ -229,7 +251,7 @@ static void lds_geometry(int cus, uint32_t S, uint32_t N) {
     uint8_t *d, *p;
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
-    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    fill(d, (size_t)N * K * P);
     x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
   }
   const uint32_t lds = K * P;
@@ -374,7 +396,7 @@ static void compute_geometry(int cus, uint32_t S, uint32_t N) {
     uint8_t *d, *p;
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
-    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    fill(d, (size_t)N * K * P);
     x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
   }
   std::vector<uint32_t> ht(200);
@@ -454,7 +476,7 @@ static void geometry(int cus, uint32_t S, uint32_t N, uint32_t pitch = 0, bool o
     uint8_t *d, *p;
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
-    CHECK(hipMemset(d, 1, (size_t)N * K * P));
+    fill(d, (size_t)N * K * P);
     x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
   }
   const double alg = (double)N * S * (K + M);
@@ -499,6 +521,8 @@ int main(int argc, char** argv) {
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   const bool only_copy = argc > 1 && argv[1][0] == 'c';
+  g_random = argc > 2 && argv[2][0] == 'r';
+  std::printf("input data: %s\n", g_random ? "random (splitmix64)" : "constant 0x01");
   if (argc > 1 && argv[1][0] == 'f') {  // LDS-staged whole-stripe streaming
     lds_geometry<10, 4>(cus, 6554, 16384);
     lds_geometry<8, 4>(cus, 8192, 16384);
@@ -530,7 +554,7 @@ int main(int argc, char** argv) {
   u32x4 *a, *b;
   CHECK(hipMalloc(&a, bytes));
   CHECK(hipMalloc(&b, bytes));
-  CHECK(hipMemset(a, 1, bytes));
+  fill(a, bytes);
   struct C {
     const char* name;
     const void* fn;
