@@ -208,7 +208,10 @@ def cpu_info():
     return model, os.cpu_count() or 1, affinity
 
 
-def cpu_baseline(k, m, S, N_sample, seconds):
+def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
+    """CPU codec on a bounded sample of the workload.  With `eng`, the same sample's
+    data shards are also encoded on the GPU and compared with the CPU's parity
+    (an oracle cross-check of the measured kernels outside the timed region)."""
     from oracle import rs_oracle
 
     t = k + m
@@ -228,12 +231,24 @@ def cpu_baseline(k, m, S, N_sample, seconds):
         done += 1
     dt = time.perf_counter() - t0
     gibs = done * 2 * N_sample * k * S / dt / GiB
+    agree = None
+    if eng is not None and done:
+        # buf now holds valid codewords (CPU encode, then CPU reconstruct of shards
+        # 0-1 from 2..t-1): the GPU's parity of the same data must be identical
+        n = min(N_sample, 4096)
+        cw = buf[:n * t * P].reshape(n, t, P)
+        d = torch.from_numpy(np.ascontiguousarray(cw[:, :k])).cuda()
+        p = torch.empty((n, m, P), dtype=torch.uint8, device="cuda")
+        eng.encode(d, p, S, n)
+        torch.cuda.synchronize()
+        agree = bool(np.array_equal(p.cpu().numpy(), cw[:, k:]))
     simd = {0: "scalar", 2: "avx2-vpshufb", 3: "avx512-gfni"}.get(level, str(level))
     return {
         "value": round(gibs, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
+        "gpu_matches_cpu_sample": agree,
         "cpu_model": model,
         "nproc": nproc,
         "affinity_cpus": affinity,
@@ -245,9 +260,9 @@ def cpu_baseline(k, m, S, N_sample, seconds):
 
 
 def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
-    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    # random bytes, as the RS kernels stream (constant fills measured ~5 % slower)
+    a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
     b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    a.fill_(1)
     ms = kernel_ms_events(torch, lambda i: eng.device_copy(b, a), iters)
     del a, b
     torch.cuda.empty_cache()
@@ -642,7 +657,7 @@ def main():
     if sustained:
         out["sustained"] = sustained
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds, torch, eng)
     if not args.no_extras:
         extras = {}
         cp = rdist.max_over_ranks(-copy_peak(torch, eng))  # slowest rank's copy rate

@@ -47,6 +47,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -69,6 +70,23 @@ enum class Kind : int { kApply = 0, kVerify = 1 };
 constexpr uint64_t kClosedBit = 1ull << 39;
 constexpr uint64_t kCountMask = kClosedBit - 1;
 constexpr int kGenShift = 40;
+
+struct Batch;
+
+// How one reservation is staged, published in its slots right after the slots are
+// reserved: if the caller is descheduled before it has staged them, the launcher
+// stages them itself (the caller's buffers stay valid -- it is blocked in the call
+// until its batch completes) instead of holding the whole batch for it.  Both may
+// copy the same bytes into the same slot; the per-slot state decides who counts it.
+struct FillReq {
+  void (*fn)(const void* ctx, Batch* b, size_t slot, size_t item);
+  const void* ctx;
+  size_t slot0, item0;  // the reservation's first slot and item index
+};
+constexpr uint32_t kSlotReserved = 0;   // reserved, FillReq not yet published
+constexpr uint32_t kSlotPublished = 1;  // FillReq published, not yet staged
+constexpr uint32_t kSlotStaged = 2;     // staged by its caller
+constexpr uint32_t kSlotTaken = 3;      // staged by the launcher
 
 struct Batch {
   int index = 0;               // position in rs_coalescer::batches (the hot-slot id)
@@ -108,6 +126,9 @@ struct Batch {
   uint32_t n_groups_alloc = 0;        // fixed at creation: ceil(max cap / kGroup)
   std::unique_ptr<std::atomic<uint32_t>[]> grp;
   std::unique_ptr<std::atomic<uint32_t>[]> has_waiter;
+  // per slot (reset to kSlotReserved by the launcher once the batch is staged)
+  std::unique_ptr<std::atomic<uint32_t>[]> slot_state;
+  std::unique_ptr<std::atomic<const FillReq*>[]> slot_req;
   std::atomic<uint64_t> wake{0};
   std::atomic<uint32_t> wake_groups{0};
   hipStream_t stream = nullptr;
@@ -389,6 +410,27 @@ void complete(rs_coalescer* co, Dispatcher* d, Batch* b, int rc) {
   wake_more(b, epoch, 2);
 }
 
+// Waits until all n reserved slots of a closed batch are staged.  After a short
+// spin, slots whose callers published their FillReq but have not staged yet (a
+// descheduled caller, common with callers far outnumbering cores) are staged here;
+// only a caller preempted between its reservation and publishing (a few
+// instructions) is waited for.  Then the slot states are reset for the next run.
+void stage_stragglers(Batch* b, size_t n) {
+  for (int spin = 0; spin < 2048 && b->filled.load(std::memory_order_acquire) < n; ++spin) __builtin_ia32_pause();
+  while (b->filled.load(std::memory_order_acquire) < n) {
+    for (size_t s = 0; s < n; ++s) {
+      uint32_t st = b->slot_state[s].load(std::memory_order_acquire);
+      if (st != kSlotPublished) continue;
+      const FillReq* r = b->slot_req[s].load(std::memory_order_relaxed);
+      if (!b->slot_state[s].compare_exchange_strong(st, kSlotTaken, std::memory_order_acq_rel)) continue;
+      r->fn(r->ctx, b, s, r->item0 + (s - r->slot0));
+      b->filled.fetch_add(1, std::memory_order_release);
+    }
+    if (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();
+  }
+  for (size_t s = 0; s < n; ++s) b->slot_state[s].store(kSlotReserved, std::memory_order_relaxed);
+}
+
 // Launcher: batching is group commit -- an open batch starts as soon as fewer than
 // max_exec batches of this GPU are executing and max_wait has passed since it
 // opened (default 0), or at once when full.  Callers arriving meanwhile pile into
@@ -420,12 +462,7 @@ void launcher_loop(rs_coalescer* co, Dispatcher* d) {
         unpublish(co, pick, static_cast<uint32_t>(t >> kGenShift));
       }
       const auto ts0 = Clock::now();
-      for (int spin = 0; pick->filled.load(std::memory_order_acquire) < n; ++spin) {  // stragglers staging
-        if (spin < 4096)
-          __builtin_ia32_pause();
-        else
-          std::this_thread::yield();  // a preempted caller holds a slot: let it run
-      }
+      stage_stragglers(pick, n);
       co->straggle_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - ts0).count(),
                                 std::memory_order_relaxed);
       pick->n_final = n;
@@ -549,8 +586,23 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     const uint32_t grp = static_cast<uint32_t>(slot0 / Batch::kGroup);
     b->has_waiter[grp].store(epoch, std::memory_order_release);  // before `filled`: seen by the waker
     if (parity_in) b->parity_in.store(1, std::memory_order_relaxed);
-    for (size_t j = 0; j < take; ++j) fill(b, slot0 + j, done_items + j);
-    b->filled.fetch_add(static_cast<uint32_t>(take), std::memory_order_release);
+    // publish how to stage these slots (the launcher may do it if we are descheduled)
+    const FillReq fr{[](const void* c, Batch* bb, size_t slot, size_t item) {
+                       (*static_cast<const std::remove_reference_t<Fill>*>(c))(bb, slot, item);
+                     },
+                     &fill, slot0, done_items};
+    for (size_t j = 0; j < take; ++j) {
+      b->slot_req[slot0 + j].store(&fr, std::memory_order_relaxed);
+      b->slot_state[slot0 + j].store(kSlotPublished, std::memory_order_release);
+    }
+    uint32_t staged = 0;
+    for (size_t j = 0; j < take; ++j) {
+      uint32_t st = kSlotPublished;
+      if (b->slot_state[slot0 + j].load(std::memory_order_acquire) != st) continue;  // the launcher took it
+      fill(b, slot0 + j, done_items + j);
+      if (b->slot_state[slot0 + j].compare_exchange_strong(st, kSlotStaged, std::memory_order_acq_rel)) ++staged;
+    }
+    if (staged) b->filled.fetch_add(staged, std::memory_order_release);
     poke(co->disp[static_cast<size_t>(b->engine)].get());
     wait_epoch(&b->grp[grp], epoch);
     wake_more(b, epoch, 2);
@@ -715,6 +767,13 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
     for (uint32_t g = 0; g < b->n_groups_alloc; ++g) {
       b->grp[g].store(0, std::memory_order_relaxed);
       b->has_waiter[g].store(0, std::memory_order_relaxed);
+    }
+    const size_t slots = static_cast<size_t>(b->n_groups_alloc) * Batch::kGroup;
+    b->slot_state.reset(new std::atomic<uint32_t>[slots]);
+    b->slot_req.reset(new std::atomic<const FillReq*>[slots]);
+    for (size_t i = 0; i < slots; ++i) {
+      b->slot_state[i].store(kSlotReserved, std::memory_order_relaxed);
+      b->slot_req[i].store(nullptr, std::memory_order_relaxed);
     }
     b->host.numa = rs::device_numa_node(rs::engine_device(rs::ctx_engine(ctx, b->engine)));
     co->free_list.push_back(b);

@@ -9,7 +9,7 @@
 //          -Ireplication_erasurecoding_object_store_amd -Lreplication_erasurecoding_object_store_amd \
 //          -lrsgpu -Wl,-rpath,$PWD/replication_erasurecoding_object_store_amd \
 //          -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
-// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma]
+// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight]
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
   const size_t obj = argc > 7 ? std::strtoull(argv[7], nullptr, 10) : 4096;
   if (argc > 8) opts.max_exec = std::atoi(argv[8]);
   if (argc > 9) opts.staged_dma = std::atoi(argv[9]);
+  if (argc > 10) opts.inflight = std::atoi(argv[10]);
   const int k = 4, m = 2;
   rs_ctx* ctx = nullptr;
   if (int rc = rs_create(k, m, 0, 0, &ctx)) {
@@ -103,11 +104,11 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
-      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d}\n",
+      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d}\n",
       co ? "coalesced" : "direct", mix ? "mix" : "enc", T, obj, dt, n_ops / dt,
       n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
-      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma);
+      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight);
   if (co) rs_coalescer_destroy(co);
   rs_destroy(ctx);
   return bad.load() ? 1 : 0;
