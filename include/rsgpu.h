@@ -245,7 +245,8 @@ int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *
  * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
 /* Tuning knob: kernel family for the batched encode / reconstruct (0 = by shape,
- * 1 = grid-stride kernels, 2 / 3 = pipelined kernel with 2 / 3 task slots per wave;
+ * 1 = grid-stride kernels, 2 / 3 = pipelined kernel with 2 / 3 task slots per wave,
+ * 4 = grid-stride lookup kernels only (no bitsliced encode);
  * shapes without a specialisation always run the generic kernel). */
 int rs_set_kernel_variant(rs_ctx *ctx, int variant);
 /* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or

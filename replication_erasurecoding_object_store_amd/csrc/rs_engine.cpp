@@ -117,7 +117,8 @@ using rs::round_up;
 int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
 
 // Default kernel family per shape (rs_set_kernel_variant): 1 = grid-stride
-// apply / bitsliced encode, 2 / 3 = pipelined with 2 / 3 task slots per wave.
+// apply / bitsliced encode, 2 / 3 = pipelined with 2 / 3 task slots per wave,
+// 4 = grid-stride lookup kernels only.
 // RS_KERNEL_VARIANT=<1..3> in the environment overrides it (tests run the whole
 // suite on each family).
 int default_variant(int k, int e, bool per_stripe) {
@@ -125,7 +126,7 @@ int default_variant(int k, int e, bool per_stripe) {
     const char* v = std::getenv("RS_KERNEL_VARIANT");
     return v ? std::atoi(v) : 0;
   }();
-  if (forced >= 1 && forced <= 3) return forced;
+  if (forced >= 1 && forced <= 4) return forced;
   (void)k;
   (void)e;
   (void)per_stripe;
@@ -470,9 +471,10 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   rs::KernelArgs a = args;
   // the encode plan with a verified generated XOR program -> bitsliced kernel
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
+  a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.status = per_stripe ? status_word(e, s) : nullptr;
   const int variant = e->variant > 0 ? e->variant : default_variant(e->k, e_out, per_stripe);
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : (variant >= 2 ? 1 : default_blocks_per_cu(e->k, e_out));
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : ((variant == 2 || variant == 3) ? 1 : default_blocks_per_cu(e->k, e_out));
   const char* name = rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc),
                                       static_cast<uint32_t>(e->cu_count), s, false, variant);
   if (!name) return RS_ERR_DEVICE;
@@ -1425,7 +1427,7 @@ int rs_set_host_zero_copy(rs_ctx* c, int enable) {
 const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_path.load() : "none"; }
 
 int rs_set_kernel_variant(rs_ctx* c, int variant) {
-  if (!c || variant < 0 || variant > 3) return RS_ERR_INVALID_ARG;
+  if (!c || variant < 0 || variant > 4) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->variant = variant;  // 0 = by shape
   return RS_OK;
 }

@@ -283,8 +283,16 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
 
     u32x4 x[K];
+    if (!PER_STRIPE && a.data_inputs) {
+      // the plan reads data shards 0..K-1 (encode): addresses need no plan load,
+      // so the K loads issue at the top of the task
+      const uint8_t* db = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
+      for (int c = 0; c < K; ++c) x[c] = load16(db + static_cast<uint64_t>(c) * a.shard_pitch + off);
+    } else {
+#pragma unroll
+      for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
+    }
 
     u32x4 y[E];
     {
@@ -984,7 +992,7 @@ static const void* pipe_fn(bool per_stripe, int variant) {
 static const void* pick_spec(int k, int m, int e, bool per_stripe, int variant, const char** name) {
 #define RS_SPEC(KK, MM, EE)                                 \
   if (k == KK && m == MM && e == EE) {                      \
-    if (variant >= 2) {                                     \
+    if (variant == 2 || variant == 3) {                     \
       *name = variant == 3 ? "pipe_kernel<" #KK "," #MM "," #EE ",3>" : "pipe_kernel<" #KK "," #MM "," #EE ",2>"; \
       return pipe_fn<KK, MM, EE>(per_stripe, variant);      \
     }                                                       \
@@ -1043,8 +1051,9 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
   const char* name = nullptr;
   // pipe_kernel addresses slots with 32-bit offsets: (k+m) * pitch < 2 GiB
-  if (variant >= 2 && static_cast<uint64_t>(a.k + a.m) * a.shard_pitch >= (1ull << 31)) variant = 1;
-  if (a.encode_net && !per_stripe && !force_generic && e == a.m && variant < 2) {
+  if ((variant == 2 || variant == 3) && static_cast<uint64_t>(a.k + a.m) * a.shard_pitch >= (1ull << 31))
+    variant = 4;
+  if (a.encode_net && !per_stripe && !force_generic && e == a.m && variant < 2) {  // 4: lookup only
     if (const void* fn = pick_bitsliced(a.k, a.m, &name)) {
       const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * ((cols + 127u) / 128u);
       if (waves == 0) return name;

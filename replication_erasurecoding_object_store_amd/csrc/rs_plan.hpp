@@ -94,6 +94,7 @@ struct KernelArgs {
   uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
   uint32_t encode_net;             // 1: uniform plan is the encode matrix and the generated
                                    //    bitsliced XOR program for (k, m) matches it
+  uint32_t data_inputs;            // 1: uniform plan reads data shards 0..k-1 (encode)
 };
 
 // Parity rows the generated bitsliced encode program of (k, m) was derived from
@@ -105,7 +106,8 @@ const uint8_t* bitsliced_encode_rows(int k, int m);
 // e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or
 // nullptr if the launch failed.  Any shard_len up to 0xFFFFFFF0 (column windows).
 // variant: 0/1 grid-stride kernels (apply / bitsliced encode), 2/3 pipelined kernel
-// with 2/3 task slots per wave (specialised shapes only).
+// with 2/3 task slots per wave (specialised shapes only), 4 grid-stride lookup
+// kernels only (no bitsliced encode).
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s, bool force_generic, int variant);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);

@@ -175,6 +175,7 @@ static float time_it(void (*launch)(void*), void* arg, int iters);
 // second argument, splitmix64 pseudo-random bytes -- DVFS and the DRAM bus both
 // see the data, so ceilings are quoted on random data too.
 static bool g_random = false;
+static bool g_real_tables = false;  // compute_geometry: real GF product tables (third arg "real")
 __global__ void fill_rand(uint64_t* p, uint64_t n8, uint64_t seed) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256) {
     uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
@@ -401,6 +402,29 @@ static void compute_geometry(int cus, uint32_t S, uint32_t N) {
   }
   std::vector<uint32_t> ht(200);
   for (int i = 0; i < 200; ++i) ht[i] = 0x01020304u * (i + 1);
+  if (g_real_tables) {  // real 3-chunk product tables of pseudo-random nonzero coefficients
+    auto mul = [](uint32_t a, uint32_t b) {
+      uint32_t r = 0;
+      for (; b; b >>= 1, a = (a << 1) ^ ((a & 0x80) ? 0x11d : 0))
+        if (b & 1) r ^= a;
+      return r & 0xFF;
+    };
+    uint32_t x = 12345;
+    for (int q = 0; q < 40; ++q) {
+      x = x * 1103515245u + 12345u;
+      const uint32_t f = 1 + (x >> 16) % 255;
+      auto pack4 = [&](int base, int shift) {
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) w |= mul(f, ((base + j) << shift) & 0xFF) << (8 * j);
+        return w;
+      };
+      ht[q * 5 + 0] = pack4(0, 0);
+      ht[q * 5 + 1] = pack4(4, 0);
+      ht[q * 5 + 2] = pack4(0, 3);
+      ht[q * 5 + 3] = pack4(4, 3);
+      ht[q * 5 + 4] = pack4(0, 6);
+    }
+  }
   uint32_t* dt;
   CHECK(hipMalloc(&dt, 800));
   CHECK(hipMemcpy(dt, ht.data(), 800, hipMemcpyHostToDevice));
@@ -522,6 +546,7 @@ int main(int argc, char** argv) {
   const int cus = prop.multiProcessorCount;
   const bool only_copy = argc > 1 && argv[1][0] == 'c';
   g_random = argc > 2 && argv[2][0] == 'r';
+  g_real_tables = argc > 3 && argv[3][0] == 'r';
   std::printf("input data: %s\n", g_random ? "random (splitmix64)" : "constant 0x01");
   if (argc > 1 && argv[1][0] == 'f') {  // LDS-staged whole-stripe streaming
     lds_geometry<10, 4>(cus, 6554, 16384);
