@@ -181,8 +181,10 @@ int rs_sync(rs_ctx *ctx, void *stream);
  * buffers and nothing of the caller's is retained.  Concurrent calls with the
  * same shard length are staged into one batch and run as one device launch (a
  * batch closes when max_batch slots are taken or max_wait_us after its first
- * call).  With k+m > 16 only encode and verify coalesce (reconstruct runs the
- * per-object path).  Thread-safe; the context must outlive the coalescer.
+ * call).  Every call kind coalesces: with k+m <= 16 a staged object carries its
+ * present mask (resolved by the kernel through the all-pattern LUT), with k+m > 16
+ * the address of its plan from the engine's plan cache.  Thread-safe; the context
+ * must outlive the coalescer.
  * Batching is group commit: a batch starts as soon as fewer than max_exec batches
  * are on the device (after an optional max_wait_us linger); calls arriving
  * meanwhile join the open batch, so batch size follows the load and a lone caller

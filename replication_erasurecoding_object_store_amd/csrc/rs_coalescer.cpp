@@ -100,6 +100,7 @@ struct Batch {
   std::atomic<uint64_t> key_S{0};     //   before `ticket` (read racily by the fast path)
   std::atomic<uint64_t> ticket{kClosedBit};
   std::atomic<uint32_t> parity_in{0};  // some slot needs its parity shards uploaded
+  std::atomic<uint32_t> fill_err{0};   // a slot's plan could not be resolved (plan mode)
   size_t n_final = 0;          // slots of the closed batch (published by the group words)
   int rc = RS_OK;              // published by the group words
   Clock::time_point deadline;
@@ -136,7 +137,7 @@ struct Batch {
   rs::PinnedBuf host;
   rs::DevBuf dev;
   // region offsets (same in host staging and device slab)
-  size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_bad = 0, bytes = 0;
+  size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_plans = 0, o_bad = 0, bytes = 0;
 };
 
 // Reserves up to `want` consecutive slots of batch b in generation gen.
@@ -221,7 +222,9 @@ void poke(Dispatcher* d) {
 struct rs_coalescer {
   rs_ctx* ctx = nullptr;
   int k = 0, m = 0;
-  bool per_stripe = false;  // k+m <= 16: per-stripe masks (reconstruct coalesces)
+  // k+m <= 16: a mask per slot, resolved by the kernel through the all-pattern LUT;
+  // else a plan address per slot (resolved at staging from the engine's plan cache)
+  bool per_stripe = false;
   size_t max_batch = 0, max_bytes = 0;
   std::chrono::microseconds max_wait{0};
 
@@ -283,7 +286,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->S = S;
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
   rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, b->engine)));
-  const size_t per = b->P * (k + 2 * m) + 8;
+  const size_t per = b->P * (k + 2 * m) + 16;  // shards + out + mask + plan + bad
   const size_t cap = std::max<size_t>(
       1, std::min({co->max_batch, co->max_bytes / per, size_t(b->n_groups_alloc) * Batch::kGroup}));
   b->cap.store(cap, std::memory_order_relaxed);
@@ -291,7 +294,8 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->o_parity = round_up(cap * k * b->P, 256);
   b->o_out = b->o_parity + round_up(cap * m * b->P, 256);
   b->o_masks = b->o_out + round_up(cap * m * b->P, 256);
-  b->o_bad = b->o_masks + round_up(cap * 4, 256);
+  b->o_plans = b->o_masks + round_up(cap * 4, 256);
+  b->o_bad = b->o_plans + round_up(cap * 8, 256);
   b->bytes = b->o_bad + round_up(cap * 4, 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   if (!b->done_ev) RS_HIP(hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming));
@@ -306,6 +310,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->filled.store(0, std::memory_order_relaxed);
   b->released.store(0, std::memory_order_relaxed);
   b->parity_in.store(0, std::memory_order_relaxed);
+  b->fill_err.store(0, std::memory_order_relaxed);
   b->rc = RS_OK;
   b->free = false;
   b->deadline = Clock::now() + co->max_wait;
@@ -337,6 +342,8 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_parity), host_at(b, b->o_parity), n * m * P, hipMemcpyHostToDevice, st));
     if (b->kind == Kind::kApply && co->per_stripe)
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
+    if (b->kind == Kind::kApply && !co->per_stripe)
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_plans), host_at(b, b->o_plans), n * 8, hipMemcpyHostToDevice, st));
   }
   int rc;
   if (b->kind == Kind::kVerify) {
@@ -346,12 +353,15 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(host_at(b, b->o_bad), dev_at(b, b->o_bad), n * 4, hipMemcpyDeviceToHost, st));
   } else {
+    if (b->fill_err.load(std::memory_order_acquire)) return RS_ERR_DEVICE;
     if (co->per_stripe) {
       rc = rs::engine_reconstruct_batch_out(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
                                             reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, at(b->o_out),
                                             m * P, st);
-    } else {  // encode-only batches (k+m > 16): parity straight into the out region
-      rc = rs::engine_encode_batch(eng, at(b->o_data), k * P, at(b->o_out), m * P, P, b->S, n, st);
+    } else {  // k+m > 16: every slot names its plan (encode, reconstruct or ReconstructData)
+      rc = rs::engine_apply_batch_plans(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
+                                        reinterpret_cast<const uint64_t*>(at(b->o_plans)), at(b->o_out), m * P,
+                                        st);
     }
     if (rc) return rc;
     if (!zc)
@@ -680,7 +690,19 @@ int rec_check(const rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool
   return RS_OK;
 }
 
-void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it) {
+// Plan mode (k+m > 16): slot's plan address on the batch's engine.
+void set_plan(const rs_coalescer* co, Batch* b, size_t slot, uint64_t present, bool data_only, bool encode) {
+  rs::Engine* eng = rs::ctx_engine(co->ctx, b->engine);
+  const uint8_t* plan = nullptr;
+  if (encode)
+    plan = rs::engine_encode_plan(eng);
+  else if (rs::engine_plan_for(eng, present, data_only, &plan) != RS_OK)
+    plan = nullptr;
+  if (!plan) b->fill_err.store(1, std::memory_order_release);
+  reinterpret_cast<uint64_t*>(host_at(b, b->o_plans))[slot] = reinterpret_cast<uint64_t>(plan);
+}
+
+void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
   const int k = co->k, m = co->m, t = k + m;
   const size_t P = b->P;
   for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
@@ -689,7 +711,10 @@ void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it) 
     uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P) : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
     std::memcpy(dst, it.shards[i], it.S);
   }
-  reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
+  if (co->per_stripe)
+    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
+  else
+    set_plan(co, b, slot, it.present, data_only, false);
 }
 
 void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
@@ -707,14 +732,12 @@ void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it,
 
 int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool data_only) {
   if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
-  if (!co->per_stripe)
-    return data_only ? rs_reconstruct_data(co->ctx, shards, lens) : rs_reconstruct(co->ctx, shards, lens);
   RecItem it;
   bool need = false;
   const int rc = rec_check(co, shards, lens, data_only, &it, &need);
   if (rc || !need) return rc;
   return submit(
-      co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it); },
+      co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it, data_only); },
       [&](Batch* b, size_t slot) { rec_drain(co, b, slot, it, data_only); });
 }
 
@@ -802,7 +825,10 @@ int rs_co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens) {
   const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
   auto fill = [&](Batch* b, size_t slot) {
     for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+    if (co->per_stripe)
+      reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+    else
+      set_plan(co, b, slot, data_mask, false, true);
   };
   auto drain = [&](Batch* b, size_t slot) {
     for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
@@ -845,10 +871,6 @@ int rs_co_reconstruct_many(rs_coalescer* co, size_t n_objects, uint8_t* const* s
   if (!co || (n_objects && (!shards || !lens || !rcs))) return RS_ERR_INVALID_ARG;
   const size_t t = static_cast<size_t>(co->k + co->m);
   co->calls.fetch_add(n_objects, std::memory_order_relaxed);
-  if (!co->per_stripe) {
-    for (size_t i = 0; i < n_objects; ++i) rcs[i] = rs_reconstruct(co->ctx, shards + i * t, lens + i * t);
-    return RS_OK;
-  }
   std::vector<RecItem> items(n_objects);
   std::map<size_t, std::vector<size_t>> by_len;
   for (size_t i = 0; i < n_objects; ++i) {
@@ -862,7 +884,7 @@ int rs_co_reconstruct_many(rs_coalescer* co, size_t n_objects, uint8_t* const* s
     for (size_t i : idx) parity_in |= items[i].parity_used;
     const int rc = submit_many(
         co, Kind::kApply, g.first, idx.size(), parity_in,
-        [&](Batch* b, size_t slot, size_t j) { rec_fill(co, b, slot, items[idx[j]]); },
+        [&](Batch* b, size_t slot, size_t j) { rec_fill(co, b, slot, items[idx[j]], false); },
         [&](Batch* b, size_t slot, size_t j) { rec_drain(co, b, slot, items[idx[j]], false); });
     if (rc) {
       for (size_t i : idx)
@@ -901,7 +923,10 @@ int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards
         [&](Batch* b, size_t slot, size_t j) {
           uint8_t* const* sh = shards + idx[j] * t;
           for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
-          reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+          if (co->per_stripe)
+            reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+          else
+            set_plan(co, b, slot, data_mask, false, true);
         },
         [&](Batch* b, size_t slot, size_t j) {
           uint8_t* const* sh = shards + idx[j] * t;

@@ -1001,6 +1001,32 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
   return launch(e, a, max_missing, true, s);
 }
 
+int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan) {
+  DeviceScope ds(e->device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
+  return uniform_plan(e, present, data_only, plan);
+}
+
+const uint8_t* engine_encode_plan(Engine* e) { return static_cast<const uint8_t*>(e->d_enc_plan.p); }
+
+int engine_apply_batch_plans(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                             size_t parity_sp, size_t pitch, size_t S, size_t N, const uint64_t* plans_dev,
+                             uint8_t* out, size_t out_sp, hipStream_t s) {
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!batch_sizes_ok(S, N, pitch)) return RS_ERR_INVALID_ARG;
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, pitch};
+  if (!device_layout_ok(L, e->m, S) || reinterpret_cast<uintptr_t>(out) % 16 || out_sp % 16 ||
+      !out_layout_ok(out_sp, pitch, S, N, e->m))
+    return RS_ERR_INVALID_ARG;
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.out = out;
+  a.out_sp = out_sp;
+  a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);  // unused: every stripe has its own
+  a.stripe_plans = plans_dev;
+  return launch(e, a, e->m, true, s);
+}
+
 int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
                         size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s) {
   if (N == 0) return RS_OK;

@@ -58,5 +58,15 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
                                  size_t n_masks, int masks_on_device, uint8_t* out, size_t out_sp, hipStream_t s);
 int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
                         size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s);
+// Device address of the plan for one pattern on this engine (cached; thread-safe):
+// reconstruct (data_only: ReconstructData) of `present`, or the encode plan.
+int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan);
+const uint8_t* engine_encode_plan(Engine* e);
+// Out-of-place batch with a plan per stripe (any k+m; the coalescer's k+m > 16
+// batches): the r-th output of stripe i at out + i*out_sp + r*pitch, the plan's
+// inputs read from the split layout.  plans_dev: n device-visible plan addresses.
+int engine_apply_batch_plans(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                             size_t parity_sp, size_t pitch, size_t S, size_t N, const uint64_t* plans_dev,
+                             uint8_t* out, size_t out_sp, hipStream_t s);
 
 }  // namespace rs

@@ -657,7 +657,13 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
     const uint32_t stripe = t / bps;
     const uint32_t blk = t - stripe * bps;
     const uint8_t* plan = a.plans;
-    if (PER_STRIPE) {
+    if (PER_STRIPE && a.stripe_plans) {  // a plan per stripe (any k+m)
+      plan = reinterpret_cast<const uint8_t*>(as_const<uint64_t>(a.stripe_plans)[stripe]);
+      if (!plan) {
+        if (lane == 0 && blk == 0) atomicOr(a.status, 1u);
+        continue;
+      }
+    } else if (PER_STRIPE) {
       const uint32_t present = as_const<uint32_t>(a.present_masks)[stripe];
       const uint32_t missing = (~present) & a.full_mask;
       const uint32_t pid = as_const<uint32_t>(a.lut)[missing];
@@ -1050,6 +1056,7 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   void* args[] = {const_cast<KernelArgs*>(&a)};
   const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
   const char* name = nullptr;
+  if (a.stripe_plans) force_generic = true;  // only the generic kernel reads per-stripe plan addresses
   // pipe_kernel addresses slots with 32-bit offsets: (k+m) * pitch < 2 GiB
   if ((variant == 2 || variant == 3) && static_cast<uint64_t>(a.k + a.m) * a.shard_pitch >= (1ull << 31))
     variant = 4;

@@ -92,6 +92,8 @@ struct KernelArgs {
   uint8_t* out;                    // null: outputs in place (slot addresses); else the
   uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
   uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
+  const uint64_t* stripe_plans;    // PER_STRIPE, generic kernel: plan address per stripe (0 =
+                                   //   invalid) instead of mask -> LUT; k+m > 16 batches
   uint32_t encode_net;             // 1: uniform plan is the encode matrix and the generated
                                    //    bitsliced XOR program for (k, m) matches it
   uint32_t data_inputs;            // 1: uniform plan reads data shards 0..k-1 (encode)

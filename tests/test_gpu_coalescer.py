@@ -103,6 +103,60 @@ def test_batch_fills_then_closes(gpu):
         svc.close()
 
 
+@pytest.mark.parametrize("data_only", [False, True])
+def test_plan_mode_coalesces_reconstruct(gpu, data_only):
+    """k+m > 16 (no all-pattern LUT): 16 concurrent Reconstruct / ReconstructData
+    calls with 16 different erasure patterns still ride one launch, each object with
+    its own plan, and match the oracle."""
+    k, m = 17, 3
+    svc = CoalescingService(k, m, max_batch=16, max_wait_us=2_000_000, inflight=2)
+    try:
+        barrier = threading.Barrier(16)
+        refs, outs, losts = [None] * 16, [None] * 16, [None] * 16
+
+        def worker(t):
+            ref = rs_oracle.split(k, m, xoshiro_bytes(0x5EED0017 + t, 5000 + 7 * t))
+            rs_oracle.encode(k, m, ref)
+            rng = np.random.default_rng(t)
+            lost = set(rng.choice(k + m, size=1 + t % m, replace=False).tolist())
+            got = [None if i in lost else bytearray(s) for i, s in enumerate(ref)]
+            barrier.wait()
+            (svc.ReconstructData if data_only else svc.Reconstruct)(got)
+            refs[t], outs[t], losts[t] = ref, got, lost
+
+        _run_threads(16, worker)
+        # objects of 16 different lengths: one batch per shard length
+        for ref, got, lost in zip(refs, outs, losts):
+            for i in range(k + m):
+                if data_only and i >= k and i in lost:
+                    assert got[i] is None
+                else:
+                    assert bytes(got[i]) == bytes(ref[i])
+        # same length, different patterns: one launch
+        svc2 = CoalescingService(k, m, max_batch=16, max_wait_us=2_000_000, inflight=2)
+        try:
+            barrier2 = threading.Barrier(16)
+            ok = [False] * 16
+
+            def worker2(t):
+                ref = rs_oracle.split(k, m, xoshiro_bytes(0x5EED0117 + t, 17 * 300))
+                rs_oracle.encode(k, m, ref)
+                lost = {t % (k + m), (t + 5) % (k + m)}
+                got = [None if i in lost else bytearray(s) for i, s in enumerate(ref)]
+                barrier2.wait()
+                (svc2.ReconstructData if data_only else svc2.Reconstruct)(got)
+                ok[t] = all((data_only and i >= k and i in lost and got[i] is None) or bytes(got[i]) == bytes(ref[i])
+                            for i in range(k + m))
+
+            _run_threads(16, worker2)
+            assert all(ok)
+            assert svc2.stats() == {"calls": 16, "batches": 1, "stripes": 16, "max_batch": 16}
+        finally:
+            svc2.close()
+    finally:
+        svc.close()
+
+
 def test_errors_identical_to_per_object(gpu):
     svc = CoalescingService(4, 2, max_wait_us=0)
     try:
@@ -125,7 +179,7 @@ def test_errors_identical_to_per_object(gpu):
         svc.close()
 
 
-@pytest.mark.parametrize("k,m", [(4, 2), (10, 4)])
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3)])
 def test_reconstruct_many_matches_oracle(gpu, k, m):
     """rs_co_reconstruct_many: per object exactly Reconstruct's result / error."""
     svc = CoalescingService(k, m, max_batch=50)
