@@ -221,7 +221,7 @@ struct Lane {
 
 // Staging for per-stripe masks passed in host memory to an asynchronous device
 // call.  A slot is reused only after the kernel that READ it has finished: `done`
-// is recorded on the launch stream after that kernel (upload_release), and `busy`
+// is recorded on the launch stream after that kernel (~UploadGuard), and `busy`
 // keeps a second caller off the slot between its upload and its launch.
 struct UploadSlot {
   PinnedBuf host;
