@@ -50,6 +50,7 @@ WORKLOADS = {
     "rs104_64K_rec2ph_out": (10, 4, 6554, 16384, "rec2ph_out"),    # per-stripe host masks -> E=2 kernel
     "rs104_64K_encu_out": (10, 4, 6554, 16384, "encu_out"),        # lookup encode (uniform data-only mask)
     "rs84_64K_encu_out": (8, 4, 8192, 16384, "encu_out"),
+    "rs84_64K_rec2ph_out": (8, 4, 8192, 16384, "rec2ph_out"),      # per-stripe host masks -> E=2 kernel
 }
 
 
