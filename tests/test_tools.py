@@ -1,0 +1,35 @@
+"""Build-time generators (CPU): the committed bitsliced XOR programs are exactly what
+tools/gen_xor_networks.py produces, and the parity rows they were derived from are
+the oracle's encode matrix ([upstream klauspost matrix.go buildMatrix])."""
+import importlib.util
+import os
+
+import numpy as np
+
+from oracle import rs_oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GEN = os.path.join(ROOT, "tools", "gen_xor_networks.py")
+INC = os.path.join(ROOT, "replication_erasurecoding_object_store_amd", "csrc", "rs_xor_networks.inc")
+
+
+def _gen():
+    spec = importlib.util.spec_from_file_location("gen_xor_networks", GEN)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_xor_networks_regenerate_identically(tmp_path):
+    mod = _gen()
+    mod.OUT = str(tmp_path / "rs_xor_networks.inc")
+    mod.main()
+    with open(mod.OUT) as a, open(INC) as b:
+        assert a.read() == b.read(), "rs_xor_networks.inc is stale: rerun tools/gen_xor_networks.py"
+
+
+def test_xor_network_rows_are_the_oracle_encode_matrix():
+    mod = _gen()
+    for k, m in mod.SHAPES:
+        rows = np.array(mod.parity_rows(k, m), dtype=np.uint8)
+        assert np.array_equal(rows, np.asarray(rs_oracle.build_matrix(k, m), dtype=np.uint8)[k:]), (k, m)
