@@ -405,6 +405,14 @@ def kmsweep(torch, rdist, rotate):
         w = RSWorkload(torch, e2, kk, mm, SS, NN, rotate, seed=0x5EED0004)
         rdist.barrier()
         enc_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.enc, 10))
+        pad_ms = None
+        if SS % 128:
+            # rs_set_parity_pad_writes: parity shards end on whole 128-B lines (the
+            # bench's own layout, pitch 256-B aligned); bytes counted stay N*S*(K+M)
+            e2.set_parity_pad_writes(True)
+            rdist.barrier()
+            pad_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.enc, 10))
+            e2.set_parity_pad_writes(False)
         rdist.barrier()
         rec_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec, 10))
         ok = rdist.all_true(w.check())
@@ -422,6 +430,9 @@ def kmsweep(torch, rdist, rotate):
             "ok": ok,
             "reconstruct_kernel": kern,
         }
+        if pad_ms:
+            ent["encode_parity_pad_GiBps"] = round(world * NN * kk * SS / (pad_ms * 1e-3) / GiB, 1)
+            ent["encode_parity_pad_hbm_frac"] = round(alg["encode"] / (pad_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         if ceiling:
             ent["pattern_ceiling_frac"] = ceiling
         sweep[f"rs{kk}{mm}_64KiB"] = ent

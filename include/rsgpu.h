@@ -251,6 +251,16 @@ int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
  * 4 = grid-stride lookup kernels only (no bitsliced encode);
  * shapes without a specialisation always run the generic kernel). */
 int rs_set_kernel_variant(rs_ctx *ctx, int variant);
+/* Batched encode may write each parity slot's padding up to the next 128-B line
+ * (bytes [S, min(pitch, round_up(S, 128))) of every parity slot; never past the
+ * pitch) and reads the data slots' padding over the same range: every parity shard
+ * write then ends on a whole 128-B line.  A partial last line costs HBM a
+ * read-modify-write, and with the line-aligned shard length the flat-task
+ * bitsliced encode covers the batch without partial columns (RS(10+4) at 64 KiB
+ * objects: S = 6554 -> 6656, profiles/r02c_flat_encode.log).  The parity bytes
+ * [0, S) are unchanged; the padding then holds the code of the data padding.
+ * 0 (the default): no byte past S of any slot is ever written. */
+int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
 /* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or
  * rs_host_register) and 16-B aligned run zero-copy by default: the kernel reads
  * the survivors and writes the missing shards across PCIe in place.  0 forces

@@ -218,6 +218,10 @@ class BatchEngine(Service):
     def set_blocks_per_cu(self, n: int) -> None:
         _check(_lib.lib().rs_set_blocks_per_cu(self.ctx, n))
 
+    def set_parity_pad_writes(self, enable: bool) -> None:
+        """Encode may write parity slot padding up to the next 128-B line (rsgpu.h)."""
+        _check(_lib.lib().rs_set_parity_pad_writes(self.ctx, 1 if enable else 0))
+
     def set_kernel_variant(self, v: int) -> None:
         """0 = by shape, 1 = grid-stride kernels, 2/3 = pipelined (2/3 task slots)."""
         _check(_lib.lib().rs_set_kernel_variant(self.ctx, v))

@@ -278,6 +278,7 @@ struct Engine {
   int variant = 0;                        // kernel family (rs_set_kernel_variant): 0 = by shape
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
+  bool parity_pad = false;                // encode may write parity padding to the next 128-B line
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -473,6 +474,15 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.status = per_stripe ? status_word(e, s) : nullptr;
+  if (e->parity_pad && a.data_inputs && !a.out) {
+    // rs_set_parity_pad_writes: run encode over whole 128-B lines of the slot
+    const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
+    if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
+      a.shard_len = static_cast<uint32_t>(s_eff);
+      a.blocks_per_stripe = static_cast<uint32_t>((round_up(s_eff, 16) / 16 + 63) / 64);
+      a.full_cols = static_cast<uint32_t>(s_eff / 16);
+    }
+  }
   const int variant = e->variant > 0 ? e->variant : default_variant(e->k, e_out, per_stripe);
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : ((variant == 2 || variant == 3) ? 1 : default_blocks_per_cu(e->k, e_out));
   const char* name = rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc),
@@ -1451,6 +1461,12 @@ int rs_set_host_zero_copy(rs_ctx* c, int enable) {
 }
 
 const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_path.load() : "none"; }
+
+int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
+  if (!c) return RS_ERR_INVALID_ARG;
+  for (auto& e : c->engines) e->parity_pad = enable != 0;
+  return RS_OK;
+}
 
 int rs_set_kernel_variant(rs_ctx* c, int variant) {
   if (!c || variant < 0 || variant > 4) return RS_ERR_INVALID_ARG;

@@ -147,6 +147,31 @@ __device__ __forceinline__ void store_part_or_drop(uint8_t* base, uint32_t off, 
     __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
 }
 
+// The first nb (1..15, wave-uniform) bytes of v at voff (+ soff) of descriptor r in at
+// most four naturally aligned buffer stores, landing only for `live` lanes (the
+// range check applies to voff: a dropped lane's offset is kDropOffset).
+__device__ __forceinline__ void store_part_rsrc(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, bool live,
+                                                u32x4 v, uint32_t nb) {
+  const uint32_t o = live ? voff : kDropOffset;
+  uint32_t q = 0;  // bytes stored so far
+  if (nb & 8u) {
+    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, r, o, soff, 2);
+    q = 8;
+  }
+  uint32_t w = q ? v[2] : v[0];  // dword holding byte q
+  if (nb & 4u) {
+    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), r, live ? voff + q : kDropOffset, soff, 2);
+    q += 4;
+    w = q == 12u ? v[3] : v[1];
+  }
+  if (nb & 2u) {
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), r, live ? voff + q : kDropOffset, soff, 2);
+    q += 2;
+    w >>= 16;
+  }
+  if (nb & 1u) __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), r, live ? voff + q : kDropOffset, soff, 2);
+}
+
 // Shard slot s of stripe i (s < k: data region, else parity region).
 __device__ __forceinline__ uint8_t* slot_ptr(const KernelArgs& a, int k, uint32_t stripe, uint32_t s) {
   return s < static_cast<uint32_t>(k)
@@ -737,11 +762,14 @@ __device__ __forceinline__ void bs_pstep(const uint32_t (&x)[8], uint32_t (&y)[8
 
 // 8x8 bit transpose in every byte lane across 8 dwords: afterwards dword r, byte
 // b, bit q = bit r of byte b of the original dword q.  An involution.
+// Each delta swap is two shifts and two bit selects (v_bitop3_b32 0xCA = m ? x : y):
+// 4 VALU instructions instead of the XOR form's 5 (tools/valu_probe.hip: shifts and
+// bitop3 issue at the same half rate, so this saves issue cycles too).
 __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
   auto swap = [&](int a, int b, int sh, uint32_t mask) {
-    const uint32_t t = ((d[a] >> sh) ^ d[b]) & mask;
-    d[b] ^= t;
-    d[a] ^= t << sh;
+    const uint32_t oa = d[a], ob = d[b];
+    d[b] = __builtin_amdgcn_bitop3_b32(mask, oa >> sh, ob, 0xCA);
+    d[a] = __builtin_amdgcn_bitop3_b32(mask << sh, ob << sh, oa, 0xCA);
   };
   swap(0, 4, 4, 0x0F0F0F0Fu);
   swap(1, 5, 4, 0x0F0F0F0Fu);
@@ -762,28 +790,65 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 // (registers for more waves) while W 2 KiB loads per wave stay in flight.
 constexpr int kBsWindow = 5;  // profiles/r01_ab_bs_window_occupancy.log
 
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2 /* nt */));
+}
+
 template <int K, int M, int C>
-__device__ __forceinline__ void bs_fold(const uint8_t* dbase, uint64_t pitch, uint32_t off_a, uint32_t off_b,
+__device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off_a, uint32_t off_b,
                                         u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&y)[8 * M]) {
   if constexpr (C < K) {
     constexpr int slot = C % kBsWindow;
     uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
                      xb[slot][0], xb[slot][1], xb[slot][2], xb[slot][3]};
     if constexpr (C + kBsWindow < K) {
-      xa[slot] = load16(dbase + static_cast<uint64_t>(C + kBsWindow) * pitch + off_a);
-      xb[slot] = load16(dbase + static_cast<uint64_t>(C + kBsWindow) * pitch + off_b);
+      xa[slot] = bload16(din, off_a, (C + kBsWindow) * pitch);
+      xb[slot] = bload16(din, off_b, (C + kBsWindow) * pitch);
     }
     transpose8(d);
     bs_step<K, M, C>(d, y);
-    bs_fold<K, M, C + 1>(dbase, pitch, off_a, off_b, xa, xb, y);
+    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, y);
   }
 }
 
-// Task = one stripe's 2 KiB column block: lane l owns the 16 B at l*16 and at
-// 1024 + l*16 of the block in every shard (two coalesced 1 KiB wave accesses per
-// shard).  Same memory discipline as apply_kernel: halves past the end re-read the
-// last column and their stores are dropped; the partial column is stored
-// byte-exact in the last block's wave-uniform branch.
+// One lane-column of a flat task: global column g = (stripe s0, column c0 + i) of the
+// batch's N x cols columns, i < 128 <= cols, so the column lies in stripe s0 or s0+1.
+struct FlatCol {
+  uint32_t col;   // column within its stripe
+  uint32_t doff;  // byte offset from the task's data stripe base (next stripe: + data_sp)
+  uint32_t poff;  // same for parity
+  bool live;      // the stripe exists (the batch's last task may run past the end)
+};
+
+__device__ __forceinline__ FlatCol flat_col(const KernelArgs& a, uint32_t s0, uint32_t c, uint32_t cstride,
+                                            uint32_t cols) {
+  const bool next = c >= cstride;
+  FlatCol f;
+  f.col = next ? c - cstride : c;
+  f.live = s0 + (next ? 1u : 0u) < a.n_stripes;
+  // a dead lane re-reads the task's first column (in the batch) and stores nothing;
+  // a lane in the line-alignment gap (col >= cols) re-reads its stripe's last column
+  const uint32_t col = f.live ? min(f.col, cols - 1u) : 0u;
+  const bool nx = f.live && next;
+  f.doff = (nx ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
+  f.poff = (nx ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
+  return f;
+}
+
+// Task = 128 consecutive columns of the batch's flat column space (stripe-major,
+// ceil(S/16) columns per stripe rounded up to whole 128-B lines): lane l owns
+// columns l and l+64 of the task, 16 B of every shard each.  A task may straddle two stripes (one encode plan for all),
+// so no lane idles at a stripe's ragged end: RS(10+4) at 64 KiB objects (410
+// columns) runs 3.2 tasks per stripe instead of 4 (20 % of the VALU work and of
+// the memory instructions); the line rounding keeps a straddling access split at a
+// line boundary (measured: S = 6656 flat 72.5-73.5 % vs stripe-aligned 67-70.5 %,
+// while unaligned splits at S = 6554 cost 1-2 points, profiles/r02c_flat_encode.log).
+// Addresses: one buffer descriptor per region off the
+// task's first stripe, a per-lane 32-bit offset (next stripe: + its pitch) and the
+// slot as the scalar offset (c * pitch).  Host preconditions (launch_window):
+// cols >= 128, data_sp / parity_sp + 16 * cols < 2^31, (k+m) * pitch < 2^32.
+// Full columns store 16 B; the lane holding a stripe's partial last column stores
+// it byte-exact in a wave-uniform branch taken by tasks that contain one.
 template <int K, int M>
 __global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -791,26 +856,37 @@ __global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelAr
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
-  const uint32_t bps = (cols + 127u) / 128u;
-  const uint32_t ntasks = a.n_stripes * bps;
-  for (uint32_t t = wave; t < ntasks; t += nwaves) {
-    const uint32_t stripe = t / bps;
-    const uint32_t blk = t - stripe * bps;
-    const uint32_t col_a = blk * 128u + lane, col_b = col_a + 64u;
-    const bool va = col_a < a.full_cols, vb = col_b < a.full_cols;
-    const uint32_t off_a = (col_a < cols ? col_a : cols - 1u) * 16u;
-    const uint32_t off_b = (col_b < cols ? col_b : cols - 1u) * 16u;
-    const uint8_t* dbase = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
+  // flat column space: each stripe rounded up to whole 128-B lines, so a task's
+  // stripe boundary -- where its 1 KiB wave accesses split in two -- is line-aligned
+  const uint32_t cstride = (cols + 7u) & ~7u;
+  const uint64_t total = static_cast<uint64_t>(a.n_stripes) * cstride;
+  if (static_cast<uint64_t>(wave) * 128u >= total) return;
+  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
+  // cursor (s0, c0) = divmod(t * 128, cols), advanced by divmod(nwaves * 128, cols)
+  const uint64_t g0 = static_cast<uint64_t>(wave) * 128u;
+  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
+  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
+  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 128u;
+  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
+  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  while (s0 < a.n_stripes) {
+    const FlatCol fa = flat_col(a, s0, c0 + lane, cstride, cols);
+    const FlatCol fb = flat_col(a, s0, c0 + 64u + lane, cstride, cols);
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pout = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                        0x7FFFFFFF, 0x00020000);
     u32x4 xa[kBsWindow], xb[kBsWindow];
 #pragma unroll
     for (int c = 0; c < kBsWindow && c < K; ++c) {
-      xa[c] = load16(dbase + static_cast<uint64_t>(c) * a.shard_pitch + off_a);
-      xb[c] = load16(dbase + static_cast<uint64_t>(c) * a.shard_pitch + off_b);
+      xa[c] = bload16(din, fa.doff, c * pitch);
+      xb[c] = bload16(din, fb.doff, c * pitch);
     }
     uint32_t y[8 * M];
-    bs_fold<K, M, 0>(dbase, a.shard_pitch, off_a, off_b, xa, xb, y);
-    // the half holding a partial last column (if any), per output row
-    const bool in_b = col_b == a.full_cols;
+    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
+    const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
+    const bool pa = nb != 0u && fa.live && fa.col == a.full_cols;  // this lane holds a partial column
+    const bool pb = nb != 0u && fb.live && fb.col == a.full_cols;
     u32x4 part[M];
 #pragma unroll
     for (int r = 0; r < M; ++r) {
@@ -818,20 +894,21 @@ __global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelAr
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
       transpose8(d);
-      uint8_t* pbase = a.parity + static_cast<uint64_t>(stripe) * a.parity_sp + static_cast<uint64_t>(r) * a.shard_pitch;
       const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
-      store16_or_drop(pbase, off_a, va, lo);
-      store16_or_drop(pbase, off_b, vb, hi);
-      part[r] = in_b ? hi : lo;
+      __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
+      part[r] = pb ? hi : lo;
     }
-    if (nb != 0u && blk + 1u == bps) {  // wave-uniform: the stripe's partial column is in this task
-      const bool live = in_b || col_a == a.full_cols;
-      const uint32_t off = in_b ? off_b : off_a;
+    if (nb != 0u && __builtin_amdgcn_ballot_w64(pa || pb) != 0u) {  // wave-uniform
+      const uint32_t off = pb ? fb.poff : fa.poff;
 #pragma unroll
-      for (int r = 0; r < M; ++r)
-        store_part_or_drop(a.parity + static_cast<uint64_t>(stripe) * a.parity_sp +
-                               static_cast<uint64_t>(r) * a.shard_pitch,
-                           off, live, part[r], nb);
+      for (int r = 0; r < M; ++r) store_part_rsrc(pout, off, r * pitch, pa || pb, part[r], nb);
+    }
+    c0 += step_c;
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
     }
   }
 }
@@ -1061,8 +1138,13 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   if ((variant == 2 || variant == 3) && static_cast<uint64_t>(a.k + a.m) * a.shard_pitch >= (1ull << 31))
     variant = 4;
   if (a.encode_net && !per_stripe && !force_generic && e == a.m && variant < 2) {  // 4: lookup only
-    if (const void* fn = pick_bitsliced(a.k, a.m, &name)) {
-      const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * ((cols + 127u) / 128u);
+    // flat 128-column tasks straddle at most two stripes (cols >= 128) and address
+    // with 32-bit offsets off one stripe base per region
+    const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
+    const bool flat_ok = cols >= 128u && a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31);
+    const void* fn = flat_ok ? pick_bitsliced(a.k, a.m, &name) : nullptr;
+    if (fn) {
+      const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 127u) / 128u;
       if (waves == 0) return name;
       if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
         return nullptr;

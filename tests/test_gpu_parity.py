@@ -608,3 +608,75 @@ def test_soa_layout_device(engines, k, m, S):
         missing = [j for j in range(t) if not (masks[i] >> j) & 1]
         for r, j in enumerate(missing):
             assert np.array_equal(got[r, i, :S], full[j, i, :S]), (i, r, j)
+
+
+# ---- bitsliced encode over flat 128-column tasks (tasks straddle stripes) -----------
+@pytest.mark.parametrize("k,m", [(8, 4), (10, 4)])
+@pytest.mark.parametrize("S,N", [(2048, 1), (2048, 3), (2049, 2), (6554, 1), (6554, 5), (6554, 37),
+                                 (4000, 7), (3000, 129), (16383, 3), (2047, 4), (2032, 4)])
+def test_bitsliced_flat_tasks(engines, k, m, S, N):
+    """Every stripe boundary position inside a task, batches whose column count is not
+    a multiple of 128, partial last columns at every offset, one-stripe batches, and a
+    shard length just below the flat kernel's 128-column minimum (2032: lookup kernel)."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 7 + N + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((N, m, P), 0xEE, dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    torch.cuda.synchronize()
+    kname = eng.last_kernel()
+    assert ("bitsliced" in kname) == (S >= 2033), kname  # 128 columns = S > 2032
+    uni = np.zeros((N, k + m, P), np.uint8)
+    uni[:, :k] = data.cpu().numpy()
+    rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
+    par = parity.cpu().numpy()
+    assert np.array_equal(par[:, :, :S], uni[:, k:, :S]), kname
+    assert (par[:, :, S:] == 0xEE).all(), "slot padding must never be written"
+    # unified K+M-slot layout: the next stripe's parity is data_sp (not parity_sp) away
+    buf = torch.from_numpy(uni.copy()).cuda()
+    buf[:, k:, :] = 0xEE
+    eng.encode_unified(buf, S, P, N)
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    assert np.array_equal(out[:, k:, :S], uni[:, k:, :S])
+    assert (out[:, k:, S:] == 0xEE).all()
+
+
+@pytest.mark.parametrize("k,m,S,P", [(10, 4, 6554, 6656), (10, 4, 6554, 6912), (8, 4, 2049, 2304),
+                                     (4, 2, 1000, 1280), (4, 2, 1000, 1008), (10, 4, 6656, 6656)])
+def test_parity_pad_writes(engines, k, m, S, P):
+    """rs_set_parity_pad_writes: encode writes parity bytes [S, min(P, round_up(S, 128)))
+    -- the code of the data padding -- and nothing past that; reconstruct is unaffected."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    N = 23
+    s_eff = min(P, (S + 127) // 128 * 128)
+    g = torch.Generator(device="cuda").manual_seed(S + P + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((N, m, P), 0xEE, dtype=torch.uint8, device="cuda")
+    eng.set_parity_pad_writes(True)
+    try:
+        eng.encode(data, parity, S, N, shard_pitch=P)
+        torch.cuda.synchronize()
+        uni = np.zeros((N, k + m, P), np.uint8)
+        uni[:, :k] = data.cpu().numpy()
+        rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, s_eff, N)
+        par = parity.cpu().numpy()
+        assert np.array_equal(par[:, :, :s_eff], uni[:, k:, :s_eff])
+        assert (par[:, :, s_eff:] == 0xEE).all(), "written past the 128-B line / pitch"
+        # per-stripe reconstruct with the option on still writes exactly S bytes
+        d2, p2 = data.clone(), parity.clone()
+        d2[:, 1, :] = 0x55
+        p2[:, 0, :] = 0x55
+        t = k + m
+        eng.reconstruct(d2, p2, S, N, np.full(N, ((1 << t) - 1) & ~((1 << 1) | (1 << k)), np.uint32),
+                        shard_pitch=P)
+        torch.cuda.synchronize()
+        assert torch.equal(d2[:, :, :S], data[:, :, :S]) and torch.equal(p2[:, :, :S], parity[:, :, :S])
+        assert (d2[:, 1, S:] == 0x55).all() and (p2[:, 0, S:] == 0x55).all()
+    finally:
+        eng.set_parity_pad_writes(False)

@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--workloads", default="all")
     ap.add_argument("--pads", default="0", help="comma-separated extra bytes added to the shard pitch "
                                                 "(multiples of 16), each its own workload line")
+    ap.add_argument("--parity-pad", action="store_true",
+                    help="rs_set_parity_pad_writes(1): encode writes parity padding to the next 128-B line")
     args = ap.parse_args()
     import torch
 
@@ -92,6 +94,8 @@ def main():
     for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
+            if args.parity_pad:
+                engines[(k, m)].set_parity_pad_writes(True)
         eng = engines[(k, m)]
         t = k + m
         P = shard_pitch_for(S) + pad

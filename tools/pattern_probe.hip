@@ -36,6 +36,7 @@ struct Geo {
   const uint8_t* d;
   uint8_t* p;
   uint32_t N, S, P, cols, full;  // cols = ceil(S/16), full = S/16
+  uint32_t sfull;                 // columns whose stores land (full, or whole 128-B lines)
 };
 
 __device__ __forceinline__ u32x4 ld(const uint8_t* p) { return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p)); }
@@ -90,7 +91,7 @@ __device__ __forceinline__ void task_store(const Geo& g, uint32_t s, uint32_t co
     u32x4 y = x[r];
 #pragma unroll
     for (int c = 0; c < K; ++c) y ^= x[c] * (r + 1);
-    st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y);
+    st_drop(ob + (uint64_t)r * g.P, col * 16, col < g.sfull, y);
   }
 }
 
@@ -175,7 +176,8 @@ static float time_it(void (*launch)(void*), void* arg, int iters);
 // second argument, splitmix64 pseudo-random bytes -- DVFS and the DRAM bus both
 // see the data, so ceilings are quoted on random data too.
 static bool g_random = false;
-static bool g_real_tables = false;  // compute_geometry: real GF product tables (third arg "real")
+static bool g_real_tables = false;
+static bool g_line_stores = false;  // mode 'w': stores cover whole 128-B lines (pad written)  // compute_geometry: real GF product tables (third arg "real")
 __global__ void fill_rand(uint64_t* p, uint64_t n8, uint64_t seed) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * 256) {
     uint64_t z = (i + seed) * 0x9E3779B97F4A7C15ull;
@@ -253,7 +255,7 @@ static void lds_geometry(int cus, uint32_t S, uint32_t N) {
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
     fill(d, (size_t)N * K * P);
-    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16, g_line_stores ? (S + 127) / 128 * 8 : S / 16};
   }
   const uint32_t lds = K * P;
   CHECK(hipFuncSetAttribute((const void*)&pF<K, M>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -326,7 +328,7 @@ __device__ __forceinline__ void gf_store(const Geo& g, const Tabs& tb, uint32_t 
   gf_compute<K, E>(tb, x, y);
   uint8_t* ob = g.p + (uint64_t)s * M * g.P;
 #pragma unroll
-  for (int r = 0; r < E; ++r) st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y[r]);
+  for (int r = 0; r < E; ++r) st_drop(ob + (uint64_t)r * g.P, col * 16, col < g.sfull, y[r]);
 }
 
 template <int K, int M, int E>
@@ -398,7 +400,7 @@ static void compute_geometry(int cus, uint32_t S, uint32_t N) {
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
     fill(d, (size_t)N * K * P);
-    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16, g_line_stores ? (S + 127) / 128 * 8 : S / 16};
   }
   std::vector<uint32_t> ht(200);
   for (int i = 0; i < 200; ++i) ht[i] = 0x01020304u * (i + 1);
@@ -501,7 +503,7 @@ static void geometry(int cus, uint32_t S, uint32_t N, uint32_t pitch = 0, bool o
     CHECK(hipMalloc(&d, (size_t)N * K * P));
     CHECK(hipMalloc(&p, (size_t)N * M * P));
     fill(d, (size_t)N * K * P);
-    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16};
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16, g_line_stores ? (S + 127) / 128 * 8 : S / 16};
   }
   const double alg = (double)N * S * (K + M);
   struct V {
@@ -560,6 +562,18 @@ int main(int argc, char** argv) {
     for (uint32_t P : {8192u, 8448u, 9216u, 10240u}) geometry<8, 4>(cus, 8192, 16384, P, true);
     for (uint32_t P : {1024u, 1280u, 1536u, 2048u}) geometry<4, 2>(cus, 1024, 65536, P, true);
     for (uint32_t P : {16384u, 16640u, 17408u}) geometry<4, 2>(cus, 16384, 16384, P, true);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'w') {  // partial-line stores vs whole-line stores
+    for (int ls = 0; ls < 2; ++ls) {
+      g_line_stores = ls;
+      std::printf("--- stores: %s\n", ls ? "whole 128-B lines (pitch padding written)" : "exact S/16 columns");
+      geometry<10, 4>(cus, 6554, 16384, 0, true);
+      geometry<6, 3>(cus, 10923, 16384, 0, true);
+      compute_geometry<10, 4, 2>(cus, 6554, 16384);
+      compute_geometry<10, 4, 4>(cus, 6554, 16384);
+    }
+    geometry<10, 4>(cus, 6656, 16384, 0, true);
     return 0;
   }
   if (argc > 1 && argv[1][0] == 'g') {

@@ -9,7 +9,7 @@ for r in $(seq 1 $ROUNDS); do
   for v in $VARS; do
     cp abx/$v.so $LIB
     echo "== round $r variant $v"
-    timeout -k 10 240 python3 tools/ab_bench.py --rounds 1 --iters ${ITERS:-20} --bpc $BPC --workloads $WL 2>&1 | grep -v amdgpu.ids
+    timeout -k 10 240 python3 tools/ab_bench.py --rounds 1 --iters ${ITERS:-20} --bpc $BPC --workloads $WL ${AB_EXTRA:-} 2>&1 | grep -v amdgpu.ids
   done
 done
 cp /tmp/_librsgpu_keep.so $LIB

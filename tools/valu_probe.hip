@@ -22,6 +22,9 @@ __global__ __launch_bounds__(256) void probe(uint32_t* out, uint32_t seed) {
       if constexpr (OP == 1) v[i] = __builtin_amdgcn_bitop3_b32(v[i], v[(i + 3) & 7], t0, 0x96);
       if constexpr (OP == 2) asm volatile("v_xor_b32 %0, %1, %0" : "+v"(v[i]) : "v"(v[(i + 5) & 7]));
       if constexpr (OP == 3) v[i] = __builtin_amdgcn_perm(t1, t0, v[i]);  // perm only (sel = data)
+      if constexpr (OP == 4) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(v[i]));
+      if constexpr (OP == 5) asm volatile("v_and_b32 %0, %1, %0" : "+v"(v[i]) : "v"(v[(i + 5) & 7]));
+      if constexpr (OP == 6) asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(v[i]) : "v"(v[(i + 5) & 7]), "v"(v[(i + 3) & 7]));
     }
   }
   uint32_t acc = 0;
@@ -39,9 +42,9 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  const char* names[] = {"v_perm+v_and (2 instr)", "v_bitop3", "v_xor_b32", "v_perm"};
-  const int per_iter[] = {16, 8, 8, 8};
-  for (int op = 0; op < 4; ++op) {
+  const char* names[] = {"v_perm+v_and (2 instr)", "v_bitop3", "v_xor_b32", "v_perm", "v_lshlrev_b32", "v_and_b32", "v_bfi_b32"};
+  const int per_iter[] = {16, 8, 8, 8, 8, 8, 8};
+  for (int op = 0; op < 7; ++op) {
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD: wps*4 waves per CU = wps blocks of 256
       const int grid = cus * wps;
       auto launch = [&] {
@@ -49,6 +52,9 @@ int main() {
         if (op == 1) hipLaunchKernelGGL(probe<1>, dim3(grid), dim3(256), 0, 0, out, 3u);
         if (op == 2) hipLaunchKernelGGL(probe<2>, dim3(grid), dim3(256), 0, 0, out, 3u);
         if (op == 3) hipLaunchKernelGGL(probe<3>, dim3(grid), dim3(256), 0, 0, out, 3u);
+        if (op == 4) hipLaunchKernelGGL(probe<4>, dim3(grid), dim3(256), 0, 0, out, 3u);
+        if (op == 5) hipLaunchKernelGGL(probe<5>, dim3(grid), dim3(256), 0, 0, out, 3u);
+        if (op == 6) hipLaunchKernelGGL(probe<6>, dim3(grid), dim3(256), 0, 0, out, 3u);
       };
       launch();
       (void)hipEventRecord(e0);
