@@ -247,19 +247,42 @@ __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K]
   }
 }
 
+// One row r of a task from the inputs' precomputed chunk indices ix[c][d].
+template <int K, int M>
+__device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)[K][4], int r) {
+  u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const uint8_t* tcol = plan;
+    asm volatile("" : "+s"(tcol));  // one opaque base per input: tables never all in SGPRs
+    const PlanView pc(tcol, K, M);
+    const RS_CONST uint32_t* tb = pc.quad(r, c);
+    const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(r, c);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t prod = lookup3(ix[c][d], q0, q1, q2, q3, q4);
+      if (c & 1)
+        y[d] = xor3(y[d], pend[d], prod);
+      else if (c == K - 1)
+        y[d] ^= prod;
+      else
+        pend[d] = prod;
+    }
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+  }
+  return y;
+}
+
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
 // #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
 //
-// Per-stripe batches sized for E > 2 outputs compute in two passes over the same
-// K loaded inputs: rows 0-1, then rows 2..E-1 only when the stripe misses more
-// than two shards -- so only two rows' accumulators and one input's chunk indices
-// are ever live (RS(10+4): 160 -> ~70 VGPRs, occupancy 3 -> 7) and a 1- or
-// 2-erasure stripe does no work for rows 2..E-1.  (Skipping row 1 for 1-erasure
-// stripes as well measured slower: the second code version costs occupancy,
-// profiles/r02_ab_row_passes.log.)  Every trip issues the same loads and stores (dropped when
-// not live); the wave-uniform branches hold VALU work only, so the compiler's
-// vmcnt bookkeeping stays exact across them.
+// Per-stripe batches sized for E > 2 outputs (device masks: E = M) split every
+// input's bytes into chunk indices once (K x 12 VGPRs) and then compute only the
+// rows the stripe misses, one row at a time (gf_row_ix), in wave-uniform branches.
+// Every trip issues the same loads and stores (dropped when not live); the
+// wave-uniform branches hold VALU work only, so the compiler's vmcnt bookkeeping
+// stays exact across them.
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -269,8 +292,6 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;      // bytes of a partial last column (0: none)
-  constexpr int E1 = (PER_STRIPE && E > 2) ? 2 : E;  // rows of the first pass
-  constexpr int E2 = E - E1;                         // rows of the second pass
   uint32_t bad = 0u;
 
   // mask of task t's stripe; every lane loads the same word (one request)
@@ -294,7 +315,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     }
-    if constexpr (K * E1 * 5 > 48) {
+    if constexpr (K * ((PER_STRIPE && E > 2) ? 2 : E) * 5 > 48) {
       // Too many table dwords to keep resident in SGPRs across trips: make the plan
       // pointer opaque per trip so its loads are not hoisted out of the loop (LICM
       // would otherwise spill them through VGPR lanes: v_writelane/v_readlane).
@@ -320,31 +341,27 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     }
 
     u32x4 y[E];
-    {
-      u32x4 y1[E1];
-      gf_rows<K, M, 0, E1>(plan, x, y1);
+    if constexpr (PER_STRIPE && E > 2) {
+      // every input's chunk indices once, then only the rows this stripe misses
+      // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
+      // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
+      // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
+      // (profiles/r02c_ab_ix_rows.log; the former two-pass form recomputed the
+      // indices and computed two rows for every stripe).
+      Idx3 ix[K][4];
 #pragma unroll
-      for (int r = 0; r < E1; ++r) y[r] = y1[r];
-    }
-    if constexpr (E2 > 0) {
-      u32x4 z[E2];
+      for (int c = 0; c < K; ++c)
 #pragma unroll
-      for (int r = 0; r < E2; ++r) z[r] = y[0];  // dropped unless computed below
-      if (pv.n_out() > static_cast<uint32_t>(E1)) {
-        const uint8_t* p2 = plan;  // the second pass's tables load inside the branch
-        asm volatile("" : "+s"(p2));
-        // opaque inputs: the chunk indices are recomputed here, not kept live from
-        // the first pass (K x 12 VGPRs -> occupancy 3)
-        u32x4 x2[K];
+        for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+      const uint32_t nrow = pv.n_out();
+      y[0] = gf_row_ix<K, M>(plan, ix, 0);
 #pragma unroll
-        for (int c = 0; c < K; ++c) {
-          x2[c] = x[c];
-          asm volatile("" : "+v"(x2[c]));
-        }
-        gf_rows<K, M, E1, E2>(p2, x2, z);
+      for (int r = 1; r < E; ++r) {
+        y[r] = y[0];  // dropped unless computed
+        if (static_cast<uint32_t>(r) < nrow) y[r] = gf_row_ix<K, M>(plan, ix, r);
       }
-#pragma unroll
-      for (int r = 0; r < E2; ++r) y[E1 + r] = z[r];
+    } else {
+      gf_rows<K, M, 0, E>(plan, x, y);
     }
     const uint32_t n_out = pv.n_out();
 #pragma unroll
