@@ -231,6 +231,14 @@ def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
         done += 1
     dt = time.perf_counter() - t0
     gibs = done * 2 * N_sample * k * S / dt / GiB
+    # one core ("plus 1 core"): the same sample, a shorter time
+    n1 = N_sample
+    done1, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < max(1.0, seconds / 5):
+        rs_oracle.baseline_apply_batch(k, mat[k:], list(range(k)), list(range(k, t)), buf, t * P, P, S, n1, 1)
+        rs_oracle.baseline_apply_batch(k, rows, surv, miss, buf, t * P, P, S, n1, 1)
+        done1 += 1
+    gibs1 = done1 * 2 * n1 * k * S / (time.perf_counter() - t1) / GiB
     agree = None
     if eng is not None and done:
         # buf now holds valid codewords (CPU encode, then CPU reconstruct of shards
@@ -247,6 +255,7 @@ def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
         "value": round(gibs, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "value_1core": round(gibs1, 3),
         "kind": "port",
         "gpu_matches_cpu_sample": agree,
         "cpu_model": model,
