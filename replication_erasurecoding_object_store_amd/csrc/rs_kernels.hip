@@ -1016,6 +1016,95 @@ __global__ __launch_bounds__(256) void verify_kernel(const KernelArgs a) {
   }
 }
 
+// The same check over flat 64-column tasks (each stripe rounded up to whole 128-B
+// lines, a task may straddle two stripes; see encode_bitsliced_kernel): RS(10+4)
+// at 64 KiB objects runs 6.5 tasks per stripe instead of 7 stripe-aligned ones.
+// Host preconditions as for the flat encode (cols >= 64 here).
+template <int K, int M>
+__global__ __launch_bounds__(256) void verify_flat_kernel(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t cstride = (cols + 7u) & ~7u;
+  const uint64_t total = static_cast<uint64_t>(a.n_stripes) * cstride;
+  if (static_cast<uint64_t>(wave) * 64u >= total) return;
+  const uint32_t pitch0 = static_cast<uint32_t>(a.shard_pitch);
+  const uint64_t g0 = static_cast<uint64_t>(wave) * 64u;
+  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
+  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
+  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 64u;
+  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
+  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  const uint8_t* const plan0 = uniform_ptr(a.plans);
+  while (s0 < a.n_stripes) {
+    const uint8_t* plan = plan0;
+    uint32_t pitch = pitch0;
+    if constexpr (K * M * 5 > 48) {
+      // opaque per trip, as in verify_kernel
+      asm volatile("" : "+s"(plan));
+      asm volatile("" : "+s"(pitch));
+    }
+    const FlatCol f = flat_col(a, s0, c0 + lane, cstride, cols);
+    const uint32_t start = f.col * 16u;
+    const uint32_t nbytes = f.live && start < a.shard_len ? min(16u, a.shard_len - start) : 0u;
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    u32x4 x[K], st[M];
+#pragma unroll
+    for (int c = 0; c < K; ++c) x[c] = bload16(din, f.doff, c * pitch);
+#pragma unroll
+    for (int r = 0; r < M; ++r) st[r] = bload16(pin, f.poff, r * pitch);
+    u32x4 y[M], pend[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) y[r] = st[r];  // y = stored ^ recomputed: zero when intact
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      Idx3 ix[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+      // one opaque base per input: the scalar load merger cannot fuse this
+      // input's table loads with later inputs' (which would pin them in SGPRs)
+      const uint8_t* tcol = plan;
+      if constexpr (K * M * 5 > 48) asm volatile("" : "+s"(tcol));
+      const PlanView pc(tcol, K, M);
+#pragma unroll
+      for (int r = 0; r < M; ++r) {
+        const RS_CONST uint32_t* tb = pc.quad(r, c);
+        const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(r, c);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t prod = lookup3(ix[d], q0, q1, q2, q3, q4);
+          if (c & 1)
+            y[r][d] = xor3(y[r][d], pend[r][d], prod);
+          else if (c == K - 1)
+            y[r][d] ^= prod;
+          else
+            pend[r][d] = prod;
+        }
+      }
+      if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t bits = 0u;
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      uint32_t diff = 0u;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) diff |= y[r][d] & byte_mask(nbytes, d);
+      bits |= diff ? (1u << r) : 0u;
+    }
+    if (bits) atomicOr(a.bad + s0 + (c0 + lane >= cstride ? 1u : 0u), bits);
+    c0 += step_c;
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
+    }
+  }
+}
+
 // Runtime K/M variant (shapes without a specialisation).
 __global__ __launch_bounds__(256) void verify_kernel_generic(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -1219,7 +1308,22 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
 #undef RS_VSPEC
   if (!fn) fn = reinterpret_cast<const void*>(&verify_kernel_generic);
   if (hipMemsetAsync(a.bad, 0, static_cast<size_t>(a.n_stripes) * 4u, s) != hipSuccess) return nullptr;
-  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  // flat 64-column tasks when a stripe's columns do not fill whole 64-column blocks
+  const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
+  const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
+  if (!force_generic && cols >= 64u && cols % 64u != 0u && a.data_sp + span < (1ull << 31) &&
+      a.parity_sp + span < (1ull << 31)) {
+    const void* ff = nullptr;
+#define RS_VFLAT(KK, MM) \
+    if (!ff && a.k == KK && a.m == MM) { ff = reinterpret_cast<const void*>(&verify_flat_kernel<KK, MM>); name = "verify_flat_kernel<" #KK "," #MM ">"; }
+    RS_VFLAT(4, 2) RS_VFLAT(8, 4) RS_VFLAT(10, 4) RS_VFLAT(6, 3)
+#undef RS_VFLAT
+    if (ff) {
+      fn = ff;
+      waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
+    }
+  }
   if (waves == 0) return name;
   const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
   const uint64_t need = (waves + 3) / 4;
