@@ -122,8 +122,19 @@ class RSWorkload:
         d, p = self.bufs[i % self.nb]
         self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks[i % self.nb])
 
+    def rec1(self, i):
+        """1 erased shard per stripe (seeded uniform index, device masks)."""
+        if not hasattr(self, "masks1"):
+            rng = np.random.default_rng(0x5EED0003 + 1)
+            full = (1 << (self.k + self.m)) - 1
+            self.masks1 = [self.torch.from_numpy((full & ~(1 << rng.integers(0, self.k + self.m, self.N)))
+                                                 .astype(np.uint32).view(np.int32)).cuda() for _ in range(self.nb)]
+        d, p = self.bufs[i % self.nb]
+        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks1[i % self.nb])
+
     def alg_bytes(self):
-        return {"encode": self.N * self.S * (self.k + self.m), "reconstruct": self.N * self.S * (self.k + 2)}
+        return {"encode": self.N * self.S * (self.k + self.m), "reconstruct": self.N * self.S * (self.k + 2),
+                "reconstruct1": self.N * self.S * (self.k + 1)}
 
     def run_steps(self, steps, warmup, barrier):
         """Times exactly `steps` steps between barrier + synchronize brackets."""
@@ -424,6 +435,8 @@ def kmsweep(torch, rdist, rotate):
             e2.set_parity_pad_writes(False)
         rdist.barrier()
         rec_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec, 10))
+        rdist.barrier()
+        rec1_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec1, 10))
         ok = rdist.all_true(w.check())
         alg = w.alg_bytes()
         kern = e2.last_kernel()
@@ -436,6 +449,8 @@ def kmsweep(torch, rdist, rotate):
             "reconstruct2_GiBps": round(world * NN * kk * SS / (rec_ms * 1e-3) / GiB, 1),
             "encode_hbm_frac": round(alg["encode"] / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "reconstruct2_hbm_frac": round(alg["reconstruct"] / (rec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "reconstruct1_GiBps": round(world * NN * kk * SS / (rec1_ms * 1e-3) / GiB, 1),
+            "reconstruct1_hbm_frac": round(alg["reconstruct1"] / (rec1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ok": ok,
             "reconstruct_kernel": kern,
         }
