@@ -684,3 +684,39 @@ def test_parity_pad_writes(engines, k, m, S, P):
         assert (d2[:, 1, S:] == 0x55).all() and (p2[:, 0, S:] == 0x55).all()
     finally:
         eng.set_parity_pad_writes(False)
+
+
+@pytest.mark.parametrize("zero_copy", [True, False])
+@pytest.mark.parametrize("S", [6560, 6554])
+def test_flat_kernels_host(engines, S, zero_copy):
+    """The flat-task encode and scrub kernels on host-resident batches with no slot
+    padding (P = S): zero-copy (the kernels address pinned host memory through
+    their buffer descriptors) and staged."""
+    k, m = 10, 4
+    eng = eng_for(engines, k, m)
+    N = 203
+    P = S
+    rng = np.random.default_rng(S + zero_copy)
+    data = rng.integers(0, 256, (N, k, P), dtype=np.uint8)
+    parity = np.zeros((N, m, P), np.uint8)
+    eng.host_register(data)
+    eng.host_register(parity)
+    eng.set_host_zero_copy(zero_copy)
+    path = "zero-copy" if zero_copy and S % 16 == 0 else "staged"
+    try:
+        eng.encode_host(data, parity, S, N)
+        assert eng.last_host_path() == path
+        assert "bitsliced" in eng.last_kernel(), eng.last_kernel()
+        uni = np.concatenate([data, np.zeros_like(parity)], axis=1).copy()
+        rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * P, P, S, N)
+        assert np.array_equal(parity, uni[:, k:])
+        assert not eng.verify_host(data, parity, S, N).any()
+        assert eng.last_kernel().startswith("verify_flat_kernel"), eng.last_kernel()
+        for i, b in [(0, 0), (1, S - 1), (100, S // 2), (N - 1, S - 1)]:
+            parity[i, 3, b] ^= 0x40
+        bad = eng.verify_host(data, parity, S, N)
+        assert np.array_equal(np.nonzero(bad)[0], [0, 1, 100, N - 1]) and (bad[bad != 0] == 8).all()
+    finally:
+        eng.set_host_zero_copy(True)
+        eng.host_unregister(data)
+        eng.host_unregister(parity)
