@@ -931,6 +931,171 @@ __global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelAr
 }
 
 // ---------------------------------------------------------------------------
+// Per-stripe reconstruct over flat 64-column tasks (out of place, LUT plans).
+//
+// The same flat column space as the flat encode / scrub (each stripe's columns
+// rounded up to whole 128-B lines), so RS(10+4) at 64 KiB objects runs 6.5 tasks
+// per stripe instead of 7 stripe-aligned ones, with every wave access split at a
+// line boundary.  A task that straddles stripes s0 / s0+1 whose erasure patterns
+// differ selects per lane: input slots (the first K present of each mask), table
+// dwords (v_cndmask between the two plans' SGPR tables) and the rows to store.
+// Input loads of such a task come from both regions with one buffer load each;
+// a lane whose slot lies in the other region gets an out-of-range offset, which
+// fetches nothing and returns zeros, so OR-ing the two loads gives its bytes.
+
+// One row r from chunk indices, table dwords chosen per lane between two plans.
+template <int K, int M>
+__device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t* planB, bool inB,
+                                            const Idx3 (&ix)[K][4], int r) {
+  u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const uint8_t* pa = planA;
+    const uint8_t* pb = planB;
+    asm volatile("" : "+s"(pa));
+    asm volatile("" : "+s"(pb));
+    const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(r, c);
+    const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(r, c);
+    uint32_t q[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) q[i] = inB ? tb[i] : ta[i];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t prod = lookup3(ix[c][d], q[0], q[1], q[2], q[3], q[4]);
+      if (c & 1)
+        y[d] = xor3(y[d], pend[d], prod);
+      else if (c == K - 1)
+        y[d] ^= prod;
+      else
+        pend[d] = prod;
+    }
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+  }
+  return y;
+}
+
+template <int K, int M, int E>
+__global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t N = a.n_stripes;
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
+  const uint32_t cstride = (cols + 7u) & ~7u;
+  if (static_cast<uint64_t>(wave) * 64u >= static_cast<uint64_t>(N) * cstride) return;
+  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
+  const uint32_t full = a.full_mask;
+  const uint64_t g0 = static_cast<uint64_t>(wave) * 64u;
+  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
+  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
+  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 64u;
+  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
+  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  uint32_t bad = 0u;
+
+  // stripe s's present mask (an invalid one reads slots 0..K-1) and plan
+  auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
+    const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
+    uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
+    bad |= (pid == kPlanInvalid) ? 1u : 0u;
+    m = (pid == kPlanInvalid) ? full : present;
+    pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
+    const uint8_t* p = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+    nout = PlanView(p, K, M).n_out();
+    return p;
+  };
+
+  while (s0 < N) {
+    const uint32_t cl = c0 + lane;
+    const bool inB = cl >= cstride;
+    const uint32_t colr = inB ? cl - cstride : cl;
+    const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
+    const bool live = !inB || straddle;                         // past the batch end: dead
+    const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
+    uint32_t mA, nA, mB, nB;
+    const uint8_t* planA = plan_of(s0, mA, nA);
+    const uint8_t* planB = planA;
+    mB = mA;
+    nB = nA;
+    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
+    const bool diff = planA != planB;  // wave-uniform: the two stripes' patterns differ
+    const bool lb = live && inB;
+    const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
+    const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    u32x4 x[K];
+    uint32_t bitsA = mA, bitsB = mB;
+    if (!diff) {
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const uint32_t s = pop_low(bitsA);
+        x[c] = s < static_cast<uint32_t>(K) ? bload16(din, offD, s * pitch)
+                                            : bload16(pin, offP, (s - static_cast<uint32_t>(K)) * pitch);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const uint32_t sa = pop_low(bitsA), sb = pop_low(bitsB);
+        const uint32_t s = inB ? sb : sa;
+        const bool par = s >= static_cast<uint32_t>(K);
+        const uint32_t so = (par ? s - static_cast<uint32_t>(K) : s) * pitch;
+        const u32x4 xd = bload16(din, par ? kDropOffset : offD + so, 0);
+        const u32x4 xp = bload16(pin, par ? offP + so : kDropOffset, 0);
+        x[c] = xd | xp;
+      }
+    }
+    Idx3 ix[K][4];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+    const uint32_t nmax = nA > nB ? nA : nB;
+    u32x4 y[E];
+    if (!diff) {
+      y[0] = gf_row_ix<K, M>(planA, ix, 0);
+#pragma unroll
+      for (int r = 1; r < E; ++r) {
+        y[r] = y[0];
+        if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix<K, M>(planA, ix, r);
+      }
+    } else {
+      y[0] = gf_row_ix2<K, M>(planA, planB, inB, ix, 0);
+#pragma unroll
+      for (int r = 1; r < E; ++r) {
+        y[r] = y[0];
+        if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix2<K, M>(planA, planB, inB, ix, r);
+      }
+    }
+    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
+    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
+                                                        0x7FFFFFFF, 0x00020000);
+    const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
+    const uint32_t nl = inB ? nB : nA;
+    const bool fullc = live && colr < a.full_cols;
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+      __builtin_amdgcn_raw_buffer_store_b128(y[r], oout, fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
+                                             r * pitch, 2 /* nt */);
+    const bool part = nb != 0u && live && colr == a.full_cols;
+    if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < E; ++r) store_part_rsrc(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, y[r], nb);
+    }
+    c0 += step_c;
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
+    }
+  }
+  if (bad && lane == 0u) atomicOr(a.status, 1u);
+}
+
+// ---------------------------------------------------------------------------
 // Verify / scrub ([upstream reedsolomon.go Verify]: re-encode and compare; the
 // reference lists bit-rot detection as missing, docs/ARCHITECTURE.md:175-178).
 // Same lookup arithmetic as apply_kernel, but the M stored parity columns are
@@ -1255,6 +1420,31 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
         return nullptr;
       return name;
+    }
+  }
+#ifndef RS_FLAT_PS
+#define RS_FLAT_PS 1
+#endif
+  if (RS_FLAT_PS && per_stripe && !force_generic && a.out && variant < 2 && e == a.m && cols >= 64u &&
+      cols % 64u != 0u) {
+    // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
+    const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
+    if (a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
+      const void* ff = nullptr;
+#define RS_PSFLAT(KK, MM)                                                        \
+      if (!ff && a.k == KK && a.m == MM) {                                       \
+        ff = reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, MM>);   \
+        name = "apply_flat_ps_kernel<" #KK "," #MM "," #MM ">";                  \
+      }
+      RS_PSFLAT(4, 2) RS_PSFLAT(8, 4) RS_PSFLAT(10, 4) RS_PSFLAT(6, 3)
+#undef RS_PSFLAT
+      if (ff) {
+        const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
+        if (waves == 0) return name;
+        if (hipLaunchKernel(ff, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+          return nullptr;
+        return name;
+      }
     }
   }
   const void* fn = force_generic ? nullptr : pick_spec(a.k, a.m, e, per_stripe, variant, &name);

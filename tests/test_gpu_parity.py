@@ -720,3 +720,52 @@ def test_flat_kernels_host(engines, S, zero_copy):
         eng.set_host_zero_copy(True)
         eng.host_unregister(data)
         eng.host_unregister(parity)
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (8, 4), (4, 2), (6, 3)])
+@pytest.mark.parametrize("S,N", [(1040, 37), (2049, 3), (6554, 1), (6554, 29), (10923, 5)])
+def test_flat_reconstruct_tasks(engines, k, m, S, N):
+    """Per-stripe out-of-place reconstruct on ragged shard lengths (flat 64-column
+    tasks that straddle stripes): neighbours with equal and with different erasure
+    patterns, complete stripes, and invalid stripes (> m missing) next to valid ones
+    -- the invalid ones write nothing and the call reports "too few shards given"."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    t = k + m
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 3 + N + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    ref = torch.cat([data, parity], dim=1).cpu().numpy()
+    rng = np.random.default_rng(S + N + t)
+    masks = _masks_upto(rng, N, t, m)
+    for i in range(0, N - 1, 4):
+        masks[i + 1] = masks[i]  # equal patterns across some boundaries
+    invalid = []
+    if N >= 3:
+        invalid = [N // 2]
+        masks[N // 2] = (1 << k) - 1 - 1  # k-1 present: too few
+    out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+    eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
+    if invalid:
+        with pytest.raises(ECError, match="too few shards given"):
+            eng.sync()
+    else:
+        eng.sync()
+    torch.cuda.synchronize()
+    kname = eng.last_kernel()
+    cols = -(-S // 16)
+    assert ("flat_ps" in kname) == (cols >= 64 and cols % 64 != 0), kname
+    got = out.cpu().numpy()
+    for i in range(N):
+        if i in invalid:
+            assert (got[i] == 0xC3).all(), "an invalid stripe writes nothing"
+            continue
+        missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+        for r, j in enumerate(missing):
+            assert np.array_equal(got[i, r, :S], ref[i, j, :S]), (kname, i, r, j)
+        for r in range(len(missing), m):
+            assert (got[i, r] == 0xC3).all(), "unused output slots untouched"
+    assert (got[:, :, S:] == 0xC3).all(), "output padding untouched"
