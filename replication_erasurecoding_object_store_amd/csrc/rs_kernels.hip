@@ -948,6 +948,7 @@ template <int K, int M>
 __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t* planB, bool inB,
                                             const Idx3 (&ix)[K][4], int r) {
   u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+  const uint32_t selB = inB ? 0xFFFFFFFFu : 0u;
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     const uint8_t* pa = planA;
@@ -958,7 +959,10 @@ __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t*
     const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(r, c);
     uint32_t q[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) q[i] = inB ? tb[i] : ta[i];
+    for (int i = 0; i < 5; ++i) {
+      q[i] = __builtin_amdgcn_bitop3_b32(selB, tb[i], ta[i], 0xCA);  // selB ? tb : ta, bitwise
+      asm volatile("" : "+v"(q[i]));                                // one input's tables at a time
+    }
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const uint32_t prod = lookup3(ix[c][d], q[0], q[1], q[2], q[3], q[4]);
