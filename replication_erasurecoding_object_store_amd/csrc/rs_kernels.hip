@@ -31,6 +31,12 @@
 // (its 16-B column lies inside the slot) and stored byte-exact by the lane that
 // holds it, in a wave-uniform branch taken only by a stripe's last block.  Every
 // store is a buffer store: in order in vmcnt, unlike flat stores.
+//
+// Ragged shard lengths (columns not a multiple of the task width, e.g. RS(10+4) at
+// 64 KiB objects: 410 columns) waste the idle lanes of each stripe's last task.
+// The flat-task kernels (bitsliced encode, scrub, per-stripe out-of-place
+// reconstruct) instead cut the batch's columns -- each stripe rounded up to whole
+// 128-B lines -- into tasks that may straddle two stripes (round 2).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
