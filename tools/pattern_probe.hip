@@ -450,6 +450,21 @@ static void compute_geometry(int cus, uint32_t S, uint32_t N) {
   }
 }
 
+// default cache policy (plain loads / stores) for comparison with the nt copy
+template <int U>
+__global__ __launch_bounds__(256) void copyd(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+  for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base < n16; base += stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * 256 < n16) v[u] = src[base + u * 256];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * 256 < n16) dst[base + u * 256] = v[u];
+  }
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void copyk(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16) {
   const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
@@ -546,7 +561,7 @@ int main(int argc, char** argv) {
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
-  const bool only_copy = argc > 1 && argv[1][0] == 'c';
+  const bool only_copy = argc > 1 && (argv[1][0] == 'c' || argv[1][0] == 'C');
   g_random = argc > 2 && argv[2][0] == 'r';
   g_real_tables = argc > 3 && argv[3][0] == 'r';
   std::printf("input data: %s\n", g_random ? "random (splitmix64)" : "constant 0x01");
@@ -589,7 +604,7 @@ int main(int argc, char** argv) {
     geometry<8, 4>(cus, 8192, 16384);
     geometry<4, 2>(cus, 1024, 65536);
   }
-  const uint64_t bytes = 1ull << 30;
+  const uint64_t bytes = (argc > 1 && argv[1][0] == 'C') ? (4ull << 30) : (1ull << 30);
   u32x4 *a, *b;
   CHECK(hipMalloc(&a, bytes));
   CHECK(hipMalloc(&b, bytes));
@@ -598,9 +613,11 @@ int main(int argc, char** argv) {
     const char* name;
     const void* fn;
   } cs[] = {{"U=2", (const void*)&copyk<2>}, {"U=4", (const void*)&copyk<4>}, {"U=8", (const void*)&copyk<8>},
-            {"U=16", (const void*)&copyk<16>}};
+            {"U=16", (const void*)&copyk<16>}, {"dflt U=4", (const void*)&copyd<4>},
+            {"dflt U=8", (const void*)&copyd<8>}};
+  std::printf("copy buffer: %llu MiB each way\n", (unsigned long long)(bytes >> 20));
   for (auto& c : cs)
-    for (int g : {1, 2, 4, 8, 16}) {
+    for (int g : {1, 2, 4, 8, 16, 32}) {
       CopyRun r{c.fn, a, b, bytes / 16, (uint32_t)(cus * g)};
       const float ms = time_it(launch_copy, &r, 10);
       std::printf("copy %-5s blocks/CU=%-2d %7.1f GB/s (read+write)\n", c.name, g, 2.0 * bytes / ms / 1e6);
