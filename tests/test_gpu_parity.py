@@ -769,3 +769,46 @@ def test_flat_reconstruct_tasks(engines, k, m, S, N):
         for r in range(len(missing), m):
             assert (got[i, r] == 0xC3).all(), "unused output slots untouched"
     assert (got[:, :, S:] == 0xC3).all(), "output padding untouched"
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (8, 4), (4, 2), (6, 3)])
+@pytest.mark.parametrize("S,N", [(1040, 37), (6554, 29), (10923, 5)])
+def test_flat_reconstruct_inplace(engines, k, m, S, N):
+    """In-place per-stripe reconstruct (device masks) on ragged shard lengths: every
+    missing slot refilled with its original bytes, in the data and the parity region,
+    nothing past S written, invalid stripes left alone.  (In place runs the
+    stripe-aligned kernel: an in-place flat-task form measured 5 points slower,
+    profiles/r02c_ab_flat_ps_inplace_rejected.log.)"""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    t = k + m
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 5 + N + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    rng = np.random.default_rng(S * 7 + N + t)
+    masks = _masks_upto(rng, N, t, m)
+    for i in range(0, N - 1, 5):
+        masks[i + 1] = masks[i]
+    inv = N // 3
+    masks[inv] = (1 << t) - 1 - sum(1 << j for j in range(m + 1))  # m+1 missing: too few
+    lost = ((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0
+    d2, p2 = data.clone(), parity.clone()
+    d2[torch.from_numpy(lost[:, :k]).cuda()] = 0x33
+    p2[torch.from_numpy(lost[:, k:]).cuda()] = 0x33
+    eng.reconstruct_devmask(d2, p2, S, N, torch.from_numpy(masks.view(np.int32)).cuda())
+    with pytest.raises(ECError, match="too few shards given"):
+        eng.sync()
+    torch.cuda.synchronize()
+    ok = np.ones(N, bool)
+    ok[inv] = False
+    okt = torch.from_numpy(ok).cuda()
+    assert torch.equal(d2[okt][:, :, :S], data[okt][:, :, :S])
+    assert torch.equal(p2[okt][:, :, :S], parity[okt][:, :, :S])
+    # padding past S of refilled slots keeps the 0x33 fill; the invalid stripe is untouched
+    assert (d2[okt][:, :, S:][torch.from_numpy(lost[ok, :k]).cuda()] == 0x33).all()
+    assert (p2[okt][:, :, S:][torch.from_numpy(lost[ok, k:]).cuda()] == 0x33).all()
+    li = torch.from_numpy(lost[inv]).cuda()
+    assert (torch.cat([d2[inv], p2[inv]])[li] == 0x33).all()
