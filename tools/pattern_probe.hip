@@ -170,6 +170,46 @@ __global__ __launch_bounds__(256) void pE(Geo g) {
   }
 }
 
+// R: per-stripe reconstruct read pattern, compute-free: K reads per task of which
+// the first NP come from the parity region (slots 0..NP-1) and the rest from data
+// slots NP..K-1 (as a stripe missing NP data shards reads NP parity survivors), and
+// E writes out of place (out + i*E*P + r*P).  NP = 0 is the all-data read mix.
+template <int K, int NP, int E>
+__global__ __launch_bounds__(256) void pR(Geo g, uint8_t* out) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, tasks = g.N * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t s = t / bps, b = t - s * bps, col = b * 64 + lane;
+    const uint32_t off = (col < g.cols ? col : g.cols - 1) * 16;
+    const uint8_t* db = uni(g.d + (uint64_t)s * K * g.P);
+    const uint8_t* pb = uni(g.p + (uint64_t)s * 4 * g.P);
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+      x[c] = c < NP ? ld(pb + (uint64_t)c * g.P + off) : ld(db + (uint64_t)c * g.P + off);
+    uint8_t* ob = out + (uint64_t)s * 4 * g.P;
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      u32x4 y = x[r];
+#pragma unroll
+      for (int c = 0; c < K; ++c) y ^= x[c] * (r + 1);
+      st_drop(ob + (uint64_t)r * g.P, off, col < g.full, y);
+    }
+  }
+}
+
+struct RRun {
+  const void* fn;
+  Geo g;
+  uint8_t* out;
+  uint32_t grid;
+};
+static void launch_rrun(void* a) {
+  RRun* r = static_cast<RRun*>(a);
+  void* args[] = {&r->g, &r->out};
+  CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, 0, nullptr));
+}
+
 static float time_it(void (*launch)(void*), void* arg, int iters);
 
 // Input fill: constant 0x01 bytes (the round-1/2 default) or, with "rand" as the
@@ -195,6 +235,32 @@ static void fill(void* p, size_t bytes) {
                      reinterpret_cast<uint64_t>(p));
   CHECK(hipDeviceSynchronize());
 }
+
+static void read_mix(int cus, uint32_t S, uint32_t N) {
+  const uint32_t P = (S + 255) / 256 * 256;
+  uint8_t *d, *p, *o;
+  CHECK(hipMalloc(&d, (size_t)N * 10 * P));
+  CHECK(hipMalloc(&p, (size_t)N * 4 * P));
+  CHECK(hipMalloc(&o, (size_t)N * 4 * P));
+  fill(d, (size_t)N * 10 * P);
+  fill(p, (size_t)N * 4 * P);
+  Geo g{d, p, N, S, P, (S + 15) / 16, S / 16, S / 16};
+  struct V { const char* name; const void* fn; int e; } vs[] = {
+      {"10 data, 1 out", (const void*)&pR<10, 0, 1>, 1}, {"9 data + 1 parity, 1 out", (const void*)&pR<10, 1, 1>, 1},
+      {"10 data, 2 out", (const void*)&pR<10, 0, 2>, 2}, {"8 data + 2 parity, 2 out", (const void*)&pR<10, 2, 2>, 2}};
+  for (auto& v : vs)
+    for (int bpc : {2, 6}) {
+      RRun r{v.fn, g, o, (uint32_t)(cus * bpc)};
+      const float ms = time_it(launch_rrun, &r, 10);
+      const double alg = (double)N * S * (10 + v.e);
+      std::printf("RS(10+4) S=%u read mix %-26s bpc=%d  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", S, v.name, bpc,
+                  alg / ms / 1e6, alg / ms / 1e6 / 80.0);
+    }
+  CHECK(hipFree(d));
+  CHECK(hipFree(p));
+  CHECK(hipFree(o));
+}
+
 
 // F: one workgroup per stripe at a time: the stripe's K data shards (one contiguous
 // K*P-byte region in the split layout) stream into LDS with LDS-DMA (1 KiB per
@@ -577,6 +643,10 @@ int main(int argc, char** argv) {
     for (uint32_t P : {8192u, 8448u, 9216u, 10240u}) geometry<8, 4>(cus, 8192, 16384, P, true);
     for (uint32_t P : {1024u, 1280u, 1536u, 2048u}) geometry<4, 2>(cus, 1024, 65536, P, true);
     for (uint32_t P : {16384u, 16640u, 17408u}) geometry<4, 2>(cus, 16384, 16384, P, true);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'R') {  // per-stripe reconstruct read mixes
+    read_mix(cus, 6554, 16384);
     return 0;
   }
   if (argc > 1 && argv[1][0] == 'w') {  // partial-line stores vs whole-line stores
