@@ -1435,18 +1435,21 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
 #ifndef RS_FLAT_PS
 #define RS_FLAT_PS 1
 #endif
-  if (RS_FLAT_PS && per_stripe && !force_generic && a.out && variant < 2 && e == a.m && cols >= 64u &&
-      cols % 64u != 0u) {
+  if (RS_FLAT_PS && per_stripe && !force_generic && a.out && variant < 2 && (e == a.m || e == 2) &&
+      cols >= 64u && cols % 64u != 0u) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
     const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
     if (a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
       const void* ff = nullptr;
-#define RS_PSFLAT(KK, MM)                                                        \
-      if (!ff && a.k == KK && a.m == MM) {                                       \
-        ff = reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, MM>);   \
-        name = "apply_flat_ps_kernel<" #KK "," #MM "," #MM ">";                  \
+#define RS_PSFLAT(KK, MM, EE)                                                    \
+      if (!ff && a.k == KK && a.m == MM && e == EE) {                            \
+        ff = reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>);   \
+        name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                  \
       }
-      RS_PSFLAT(4, 2) RS_PSFLAT(8, 4) RS_PSFLAT(10, 4) RS_PSFLAT(6, 3)
+      // E = M (device masks, mixed encode + reconstruct) and E = 2 (host masks of
+      // 1-2 erasures, e.g. healer batches: +2 points, profiles/r02c_ab_flat_ps_e2.log)
+      RS_PSFLAT(4, 2, 2) RS_PSFLAT(8, 4, 4) RS_PSFLAT(10, 4, 4) RS_PSFLAT(6, 3, 3)
+      RS_PSFLAT(8, 4, 2) RS_PSFLAT(10, 4, 2) RS_PSFLAT(6, 3, 2)
 #undef RS_PSFLAT
       if (ff) {
         const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;

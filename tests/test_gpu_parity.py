@@ -812,3 +812,39 @@ def test_flat_reconstruct_inplace(engines, k, m, S, N):
     assert (p2[okt][:, :, S:][torch.from_numpy(lost[ok, k:]).cuda()] == 0x33).all()
     li = torch.from_numpy(lost[inv]).cuda()
     assert (torch.cat([d2[inv], p2[inv]])[li] == 0x33).all()
+
+
+@pytest.mark.parametrize("k,m", [(10, 4), (8, 4), (6, 3)])
+@pytest.mark.parametrize("S,N", [(6554, 29), (1040, 9), (10923, 4)])
+def test_flat_reconstruct_host_masks_e2(engines, k, m, S, N):
+    """Host masks of at most 2 erasures on ragged shard lengths: the batch is sized
+    for 2 outputs (the flat-task kernel's E = 2 form); straddling stripes with equal
+    and different patterns."""
+    import torch
+
+    eng = eng_for(engines, k, m)
+    t = k + m
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 11 + N + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    ref = torch.cat([data, parity], dim=1).cpu().numpy()
+    rng = np.random.default_rng(S + N * 3 + t)
+    masks = _masks_upto(rng, N, t, 2)
+    masks[0] = ((1 << t) - 1) & ~0b11  # at least one 2-erasure stripe
+    for i in range(1, N - 1, 3):
+        masks[i + 1] = masks[i]
+    out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+    eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
+    torch.cuda.synchronize()
+    cols = -(-S // 16)
+    assert ("flat_ps" in eng.last_kernel()) == (cols % 64 != 0), eng.last_kernel()
+    got = out.cpu().numpy()
+    for i in range(N):
+        missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+        for r, j in enumerate(missing):
+            assert np.array_equal(got[i, r, :S], ref[i, j, :S]), (i, r, j)
+        for r in range(len(missing), m):
+            assert (got[i, r] == 0xC3).all()
+    assert (got[:, :, S:] == 0xC3).all()
