@@ -103,6 +103,15 @@ __device__ __forceinline__ void store_tail(uint8_t* p, u32x4 v, uint32_t nbytes)
 
 __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Global wave index of a grid-stride kernel (256-thread blocks).  Blocks are dealt
+// round-robin over the 8 XCDs, so consecutive tasks run on different XCDs; that
+// placement is kept on purpose: giving each XCD a contiguous eighth of every pass
+// measured level for RS(4+2) and 3-4 points slower for RS(10+4)
+// (profiles/r02c_ab_xcd_remap_rejected.log).
+__device__ __forceinline__ uint32_t wave_index() {
+  return wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+
 // Offset past every descriptor's range: a buffer store there is dropped.
 constexpr uint32_t kDropOffset = 0x80000000u;
 
@@ -292,7 +301,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;   // the partial last column included
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(256, 1) void pipe_kernel(const KernelArgs a) {
   // uniform plans with few table dwords keep them in VGPRs for the whole launch
   constexpr bool kVTab = !PER_STRIPE && E * K * 5 <= 100;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;  // the partial last column included
   const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
@@ -695,7 +704,7 @@ __global__ __launch_bounds__(256, 1) void pipe_kernel(const KernelArgs a) {
 template <bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;
   const uint32_t ntasks = a.n_stripes * bps;
@@ -875,7 +884,7 @@ __device__ __forceinline__ FlatCol flat_col(const KernelArgs& a, uint32_t s0, ui
 template <int K, int M>
 __global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
@@ -987,7 +996,7 @@ __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t*
 template <int K, int M, int E>
 __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t N = a.n_stripes;
   const uint32_t cols = (a.shard_len + 15u) >> 4;
@@ -1121,7 +1130,7 @@ __device__ __forceinline__ uint32_t byte_mask(uint32_t nbytes, int d) {
 template <int K, int M>
 __global__ __launch_bounds__(256) void verify_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;
   const uint32_t ntasks = a.n_stripes * bps;
@@ -1198,7 +1207,7 @@ __global__ __launch_bounds__(256) void verify_kernel(const KernelArgs a) {
 template <int K, int M>
 __global__ __launch_bounds__(256) void verify_flat_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t cstride = (cols + 7u) & ~7u;
@@ -1283,7 +1292,7 @@ __global__ __launch_bounds__(256) void verify_flat_kernel(const KernelArgs a) {
 // Runtime K/M variant (shapes without a specialisation).
 __global__ __launch_bounds__(256) void verify_kernel_generic(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_uniform(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;
   const uint32_t ntasks = a.n_stripes * bps;
