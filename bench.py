@@ -14,11 +14,12 @@ data-path collective); the only collectives are the timing barrier / max-reduce.
 
 Roofline: the dominant kernel's algorithmic bytes per launch (encode N.S.(K+M),
 reconstruct N.S.(K+e)) / its average launch time, measured with one
-HIP event pair on the launch stream around 100 back-to-back launches of that kernel
-over the same rotating batches (so launch gaps count against it), against 8.0 TB/s
-(MI355X_MICROARCH.md).  `frac_rocprof` is the same bytes over the
-rocprofv3 average of the kernel from the committed profiles/ summary of this
-workload (null when none is committed).
+HIP event pair on the launch stream around >= 100 ms of back-to-back launches of
+that kernel over the same rotating batches (so launch gaps count against it),
+against 8.0 TB/s (MI355X_MICROARCH.md).  `frac_rocprof` is the same bytes over the
+rocprofv3 average from the committed profiles/ summary of this workload, reported
+only when that summary profiled the very kernel this run launched (null
+otherwise).
 cpu_baseline: oracle/rs_cpu_baseline.c (AVX-512 GFNI / AVX2 split-nibble C
 restatement of klauspost's CPU kernels -- a port, not the Go reference, which is
 absent) on the host cores of this box, same workload, bounded sample.
@@ -118,11 +119,13 @@ class RSWorkload:
         d, p = self.bufs[i % self.nb]
         self.eng.encode(d, p, self.S, self.N)
 
-    def rec(self, i):
+    def rec(self, i, bound=0):
+        """bound: the caller's erasure bound (max_missing; 0 = m)."""
         d, p = self.bufs[i % self.nb]
-        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks[i % self.nb])
+        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks[i % self.nb],
+                                 max_missing=bound)
 
-    def rec1(self, i):
+    def rec1(self, i, bound=0):
         """1 erased shard per stripe (seeded uniform index, device masks)."""
         if not hasattr(self, "masks1"):
             rng = np.random.default_rng(0x5EED0003 + 1)
@@ -130,7 +133,8 @@ class RSWorkload:
             self.masks1 = [self.torch.from_numpy((full & ~(1 << rng.integers(0, self.k + self.m, self.N)))
                                                  .astype(np.uint32).view(np.int32)).cuda() for _ in range(self.nb)]
         d, p = self.bufs[i % self.nb]
-        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks1[i % self.nb])
+        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks1[i % self.nb],
+                                 max_missing=bound)
 
     def alg_bytes(self):
         return {"encode": self.N * self.S * (self.k + self.m), "reconstruct": self.N * self.S * (self.k + 2),
@@ -155,12 +159,12 @@ class RSWorkload:
         self.eng.sync()
         return dt
 
-    def kernel_ms(self, reps=100):
-        """Each kernel's average launch duration: one HIP event pair around `reps`
-        back-to-back launches on the launch stream (launch gaps included)."""
+    def kernel_ms(self, min_ms=100.0):
+        """Each kernel's average launch duration: one HIP event pair around >= min_ms
+        of back-to-back launches on the launch stream (launch gaps included)."""
         out = {}
         for name, fn in (("encode", self.enc), ("reconstruct", self.rec)):
-            out[name] = kernel_ms_events(self.torch, fn, reps, per_launch=False)
+            out[name] = sustained_kernel_ms(self.torch, fn, min_ms)[0]
         self.eng.sync()
         return out
 
@@ -201,6 +205,16 @@ def kernel_ms_events(torch, fn, reps, per_launch=False):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
+
+
+def sustained_kernel_ms(torch, fn, min_ms=100.0):
+    """Average launch duration of fn over back-to-back launches filling >= min_ms
+    (one HIP event pair): long enough for the clock to settle where it stays under
+    load (VALU-heavy kernels start at 2.25 GHz and drop within ~8
+    launches), the same window tools/profile_kmsweep_pmc.sh profiles."""
+    est = kernel_ms_events(torch, fn, 3)
+    reps = max(10, int(np.ceil(min_ms / max(est, 1e-3))))
+    return kernel_ms_events(torch, fn, reps), reps
 
 
 def cpu_info():
@@ -411,10 +425,13 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
                     "staged: every k+m slot DMA'd each way"}
 
 
-def kmsweep(torch, rdist, rotate):
+def kmsweep(torch, rdist, rotate, min_ms=100.0):
     """configs[3]: RS(4+2), RS(8+4), RS(10+4) at 64 KiB stripes, 16 384 stripes per
-    GPU (weak scaling): each kernel's average launch time (HIP events) on every
-    rank, the slowest rank's time taken, aggregate rate = world x per-GPU bytes."""
+    GPU (weak scaling): each kernel's average launch time over >= min_ms of
+    back-to-back launches (HIP events) on every rank, the slowest rank's time taken,
+    aggregate rate = world x per-GPU bytes.  Reconstructs with device masks run
+    twice: with the erasure bound the caller knows (max_missing = the 1 or 2 it
+    erased: rs_reconstruct_batch_out_devmask) and without (kernel sized for m)."""
     from replication_erasurecoding_object_store_amd.batch import BatchEngine
 
     _, _, world = rdist.world()
@@ -423,47 +440,43 @@ def kmsweep(torch, rdist, rotate):
         e2 = BatchEngine(kk, mm, torch.cuda.current_device())
         SS, NN = -(-65536 // kk), 16384
         w = RSWorkload(torch, e2, kk, mm, SS, NN, rotate, seed=0x5EED0004)
-        rdist.barrier()
-        enc_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.enc, 10))
-        pad_ms = None
+        alg = w.alg_bytes()
+        ent = {"shard_len": SS, "stripes_per_gpu": NN, "min_timed_ms": min_ms}
+        kern = {}
+
+        def timed(key, fn, bytes_):
+            rdist.barrier()
+            ms, reps = sustained_kernel_ms(torch, fn, min_ms)
+            ms = rdist.max_over_ranks(ms)
+            kern[key] = e2.last_kernel()
+            ent[f"{key}_GiBps"] = round(world * NN * kk * SS / (ms * 1e-3) / GiB, 1)
+            ent[f"{key}_hbm_frac"] = round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            ent[f"{key}_launches"] = reps
+
+        timed("encode", w.enc, alg["encode"])
         if SS % 128:
             # rs_set_parity_pad_writes: parity shards end on whole 128-B lines (the
             # bench's own layout, pitch 256-B aligned); bytes counted stay N*S*(K+M)
             e2.set_parity_pad_writes(True)
-            rdist.barrier()
-            pad_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.enc, 10))
+            timed("encode_parity_pad", w.enc, alg["encode"])
             e2.set_parity_pad_writes(False)
-        rdist.barrier()
-        rec_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec, 10))
-        rdist.barrier()
-        rec1_ms = rdist.max_over_ranks(kernel_ms_events(torch, w.rec1, 10))
-        ok = rdist.all_true(w.check())
-        alg = w.alg_bytes()
-        kern = e2.last_kernel()
+        timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"])
+        timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+        if mm > 2:
+            timed("reconstruct2_unbounded", w.rec, alg["reconstruct"])
+            timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])
+        ent["ok"] = rdist.all_true(w.check())
+        ent["kernels"] = kern
         w.close()
         e2.close()
         ceiling = PATTERN_CEILING.get((kk, mm, SS))
-        ent = {
-            "shard_len": SS, "stripes_per_gpu": NN,
-            "encode_GiBps": round(world * NN * kk * SS / (enc_ms * 1e-3) / GiB, 1),
-            "reconstruct2_GiBps": round(world * NN * kk * SS / (rec_ms * 1e-3) / GiB, 1),
-            "encode_hbm_frac": round(alg["encode"] / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "reconstruct2_hbm_frac": round(alg["reconstruct"] / (rec_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "reconstruct1_GiBps": round(world * NN * kk * SS / (rec1_ms * 1e-3) / GiB, 1),
-            "reconstruct1_hbm_frac": round(alg["reconstruct1"] / (rec1_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "ok": ok,
-            "reconstruct_kernel": kern,
-        }
-        if pad_ms:
-            ent["encode_parity_pad_GiBps"] = round(world * NN * kk * SS / (pad_ms * 1e-3) / GiB, 1)
-            ent["encode_parity_pad_hbm_frac"] = round(alg["encode"] / (pad_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         if ceiling:
             ent["pattern_ceiling_frac"] = ceiling
         sweep[f"rs{kk}{mm}_64KiB"] = ent
     return sweep
 
 
-def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
+def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006):
     """Device-resident verify / bit-rot scrub (rs_verify_batch): re-encode and
     compare every stripe, K+M shards read per stripe, nothing written but the
     per-stripe mismatch words.  Checks clean batches verify clean and one flipped
@@ -476,7 +489,7 @@ def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
     for d, p in bufs:
         eng.encode(d, p, S, N)
     bad = torch.empty(N, dtype=torch.int32, device="cuda")
-    ms = kernel_ms_events(torch, lambda i: eng.verify(*bufs[i % nb], bad, S, N), reps)
+    ms, reps = sustained_kernel_ms(torch, lambda i: eng.verify(*bufs[i % nb], bad, S, N))
     d, p = bufs[0]
     eng.verify(d, p, bad, S, N)
     torch.cuda.synchronize()
@@ -493,9 +506,9 @@ def scrub_rate(torch, eng, k, m, S, N, rotate_bytes, seed=0x5EED0006, reps=10):
             "hbm_frac": round(N * S * (k + m) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "ok": clean and hit}
 
 
-def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
+def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes):
     """Config 2's SoA layout variant and config 3's named erasure patterns, each as
-    kernel time per launch (HIP events, rotating >= 2 GiB).  Rates: user data
+    kernel time per launch (HIP events over >= 100 ms, rotating >= 2 GiB).  Rates: user data
     K*S*N per second and HBM fraction of the algorithmic bytes."""
     from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
 
@@ -520,21 +533,21 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes, reps=10):
         res[name] = {"user_GiBps": round(N * k * S / sec / GiB, 1),
                      "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4)}
 
-    put("rec1_per_stripe_out", kernel_ms_events(torch, lambda i: eng.reconstruct_out(
-        split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one), reps), 1)
+    put("rec1_per_stripe_out", sustained_kernel_ms(torch, lambda i: eng.reconstruct_out(
+        split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one, max_missing=1))[0], 1)
     for name, pat in (("rec_0_1_uniform_out", (0, 1)), ("rec_0_4_uniform_out", (0, 4)),
                       ("rec_4_5_uniform_out", (4, 5))):
         mask = full & ~sum(1 << j for j in pat)
-        put(name, kernel_ms_events(torch, lambda i: eng.reconstruct_out(
-            split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, present_masks=mask), reps), 2)
+        put(name, sustained_kernel_ms(torch, lambda i: eng.reconstruct_out(
+            split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, present_masks=mask))[0], 2)
     del split
     torch.cuda.empty_cache()
     # SoA: shard s of every stripe in one plane
     soa = [(torch.randint(0, 256, (k, N, P), dtype=torch.uint8, device="cuda", generator=g),
             torch.empty((m, N, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
-    put("soa_encode", kernel_ms_events(torch, lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N,
-                                                                   shard_pitch=N * P, data_stripe_pitch=P,
-                                                                   parity_stripe_pitch=P), reps), m)
+    put("soa_encode", sustained_kernel_ms(torch, lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N,
+                                                                      shard_pitch=N * P, data_stripe_pitch=P,
+                                                                      parity_stripe_pitch=P))[0], m)
     del soa
     torch.cuda.empty_cache()
     return res
@@ -571,6 +584,12 @@ def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
             "objects_per_s": round(N / sec), "ok": ok,
             "cpu_baseline_GiBps": round(cpu_rate, 2), "cpu_threads": threads,
             "cpu_kind": "port (oracle/sha256_cpu_baseline.c, " + ("SHA-NI" if ni else "scalar") + ")"}
+
+
+def kernel_key(name):
+    """'rs::apply_kernel<4, 2, 2, true>(rs::KernelArgs)' and rs_last_kernel()'s
+    'apply_kernel<4,2,2,true>' -> the same key."""
+    return name.split("(")[0].replace("rs::", "").replace(" ", "")
 
 
 def committed_profile(workload):
@@ -641,12 +660,15 @@ def main():
     prof = committed_profile(workload_key)
     frac_rocprof, traffic, rocprof_ns = None, None, None
     if prof:
+        # only a committed profile of the very kernel this run measured counts
         ent = next((v for kname, v in prof.get("kernels", {}).items()
-                    if kname.endswith("true>" if dom == "reconstruct" else "false>") and "apply_kernel" in kname), None)
+                    if kernel_key(kname) == kernel_key(kernel_names.get(dom, ""))), None)
         if ent:
             rocprof_ns = ent["avg_ns"]
             frac_rocprof = round(alg[dom] / rocprof_ns / HBM_PEAK_GBS, 4)
-        traffic = prof.get("hbm_bytes_per_launch", {}).get(dom)
+            traffic = prof.get("hbm_bytes_per_launch", {}).get(dom)
+        else:
+            prof = None
 
     out = {
         "metric": "GiB/s device-resident RS(4+2) encode + 2-erasure reconstruct, batched stripes",
@@ -671,15 +693,14 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": f"{kernel_names.get(dom)} ({dom}; rocprof name rs::apply_kernel<{k}, {m}, "
-                      f"{2 if dom == 'reconstruct' else m}, {'true' if dom == 'reconstruct' else 'false'}>)",
-            "timing": "one HIP event pair around 100 back-to-back launches per kernel, on the launch stream",
+            "kernel": f"{kernel_names.get(dom)} ({dom})",
+            "timing": "one HIP event pair around >= 100 ms of back-to-back launches per kernel, on the launch stream",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "frac_rocprof": frac_rocprof,
+            "frac_rocprof": frac_rocprof,  # from the committed profile of this kernel, not this run
             "rocprof_avg_ns": rocprof_ns,
             "rocprof_summary": prof["_path"] if prof else None,
             "pattern_ceiling_frac": PATTERN_CEILING.get((k, m, S)),

@@ -139,8 +139,8 @@ int rs_reconstruct_batch(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch, u
 /* Device-resident masks (RS_MEM_DEVICE only, k+m <= 16): present_masks_dev is a
  * device array of n_stripes uint32.  Stripes with < k present are left untouched
  * and reported by the next rs_sync on THAT stream as RS_ERR_TOO_FEW_SHARDS (each
- * stream has its own deferred-error word; rs_sync on another stream neither sees
- * nor clears it). */
+ * stream has its own deferred-error word, however many streams there are; rs_sync
+ * on another stream neither sees nor clears it). */
 int rs_reconstruct_batch_devmask(rs_ctx *ctx, uint8_t *data, size_t data_stripe_pitch,
                                  uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
                                  size_t shard_len, size_t n_stripes,
@@ -160,6 +160,19 @@ int rs_reconstruct_batch_out(rs_ctx *ctx, const uint8_t *data, size_t data_strip
                              size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
                              size_t n_masks, int masks_on_device, uint8_t *out,
                              size_t out_stripe_pitch, void *stream);
+/* The same with device masks and a caller-known bound on the erasures per stripe:
+ * 1 <= max_missing <= m (0 = m).  Host masks give the engine their maximum; device
+ * masks cannot, and a kernel sized for m outputs per stripe carries registers and
+ * work a batch of 1-2 erasure repairs never uses (the healer's case, poller.go:282;
+ * a degraded read, readservice.go:285).  out_stripe_pitch >= max_missing *
+ * shard_pitch.  A stripe missing more than max_missing shards is left untouched
+ * and reported by rs_sync on the stream as RS_ERR_INVALID_ARG (one with < k present
+ * as RS_ERR_TOO_FEW_SHARDS, which takes precedence). */
+int rs_reconstruct_batch_out_devmask(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch,
+                                     const uint8_t *parity, size_t parity_stripe_pitch,
+                                     size_t shard_pitch, size_t shard_len, size_t n_stripes,
+                                     const uint32_t *present_masks_dev, int max_missing, uint8_t *out,
+                                     size_t out_stripe_pitch, void *stream);
 /* Batched parity verify / bit-rot scrub ([upstream reedsolomon.go Verify], per
  * object: rs_verify).  Recomputes every parity shard from the data shards and
  * compares it with the stored one: bad[i] = bitmask of stripe i's parity shards
@@ -169,8 +182,12 @@ int rs_reconstruct_batch_out(rs_ctx *ctx, const uint8_t *data, size_t data_strip
 int rs_verify_batch(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch,
                     const uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
                     size_t shard_len, size_t n_stripes, uint32_t *bad, int mem, void *stream);
-/* Wait for `stream` and return any deferred device-side error. */
+/* Wait for `stream` and return (and clear) its deferred device-side errors. */
 int rs_sync(rs_ctx *ctx, void *stream);
+/* rs_sync, then forget the stream: its deferred-error word goes back to the engine.
+ * Call it before destroying a stream that ran device-mask batches, so a later stream
+ * that gets the same handle starts with no errors and no word is kept for it. */
+int rs_stream_release(rs_ctx *ctx, void *stream);
 
 /* ---- batch coalescer (per-object calls -> device batches) ------------------
  * Drop-in for the per-object entry points when many threads call them at once
@@ -216,6 +233,20 @@ int rs_co_reconstruct_many(rs_coalescer *co, size_t n_objects, uint8_t *const *s
                            int *rcs);
 int rs_co_encode_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards,
                       const size_t *lens, int *rcs);
+/* Encode + cold_hash in one coalesced batch: the write path
+ * hashes the very value it splits and encodes -- Split writeservice.go:218, Encode
+ * :222, cold_hash = computeSHA256Hex(value) :267 (:51-54); hybrid writes :326,
+ * :382-386.  rs_co_encode's contract, and digest (32 bytes, FIPS 180-4 order) =
+ * SHA-256 of the first value_len bytes of data shards 0..k-1 taken in order -- the
+ * Split input, since Split's data shards are the value followed by zero padding.
+ * 0 <= value_len <= k * S (RS_ERR_INVALID_ARG otherwise).  The hash runs on the GPU
+ * over the same staged shards as the encode, in the same batch (one lane per object:
+ * SHA-256 is a serial chain, so a batch of large objects takes longer than its
+ * encode). */
+int rs_co_encode_hash(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, size_t value_len,
+                      uint8_t *digest);
+int rs_co_encode_hash_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards, const size_t *lens,
+                           const size_t *value_lens, uint8_t *digests, int *rcs);
 /* Counters since creation: calls, device batches, stripes batched, largest batch. */
 int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
                 uint64_t *max_batch);
@@ -246,11 +277,6 @@ int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *
 /* Tuning knob: workgroups (256 threads) per CU for the batched kernels
  * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
-/* Tuning knob: kernel family for the batched encode / reconstruct (0 = by shape,
- * 1 = grid-stride kernels, 2 / 3 = pipelined kernel with 2 / 3 task slots per wave,
- * 4 = grid-stride lookup kernels only (no bitsliced encode);
- * shapes without a specialisation always run the generic kernel). */
-int rs_set_kernel_variant(rs_ctx *ctx, int variant);
 /* Batched encode may write each parity slot's padding up to the next 128-B line
  * (bytes [S, min(pitch, round_up(S, 128))) of every parity slot; never past the
  * pitch) and reads the data slots' padding over the same range: every parity shard

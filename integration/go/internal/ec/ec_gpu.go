@@ -91,8 +91,15 @@ func NewService() interfaces.IEcDriver {
 	return &Service{ctx: ctx, co: co}
 }
 
-// Split keeps klauspost's semantics in Go (no arithmetic): data shards alias
-// `data`, the short last shard and all parity shards are fresh zeroed slices.
+// Split is klauspost v1.12.1's Split (reedsolomon.go) in Go -- no arithmetic, so it
+// never reaches the GPU (ec.go:48-50, writeservice.go:218,382):
+//   - perShard = ceil(len/K); len(data) == 0 -> ErrShortData;
+//   - spare capacity of `data` is used before anything is allocated: data is
+//     extended to min(cap, (K+M)*perShard) and zeroed past len, so with enough
+//     capacity every shard -- parity included -- aliases the caller's buffer;
+//   - only the shards that do not fit get fresh zeroed storage, the first of them
+//     holding the tail of the payload;
+//   - every shard is capped at perShard (data[:perShard:perShard]).
 func (s *Service) Split(data []byte) ([][]byte, error) {
 	if s.cpu != nil {
 		return s.cpu.Split(data)
@@ -101,18 +108,47 @@ func (s *Service) Split(data []byte) ([][]byte, error) {
 		return nil, reedsolomon.ErrShortData
 	}
 	k, total := config.K, config.K+config.M
+	if total == 1 {
+		return [][]byte{data}, nil
+	}
+	dataLen := len(data)
 	perShard := (len(data) + k - 1) / k
+	needTotal := total * perShard
+	if cap(data) > len(data) {
+		if cap(data) > needTotal {
+			data = data[:needTotal]
+		} else {
+			data = data[:cap(data)]
+		}
+		clear(data[dataLen:])
+	}
+	var padding [][]byte
+	if len(data) < needTotal {
+		fullShards := len(data) / perShard // shards that fit in data (its spare capacity included)
+		buf := make([]byte, (total-fullShards)*perShard)
+		padding = make([][]byte, total-fullShards)
+		for i := range padding {
+			padding[i] = buf[i*perShard : (i+1)*perShard : (i+1)*perShard]
+		}
+		if dataLen > perShard*fullShards { // the payload's tail does not fill a whole shard
+			copyFrom := data[perShard*fullShards : dataLen]
+			for i := range padding {
+				if len(copyFrom) == 0 {
+					break
+				}
+				copyFrom = copyFrom[copy(padding[i], copyFrom):]
+			}
+		}
+	}
 	dst := make([][]byte, total)
 	i := 0
 	for ; i < total && len(data) >= perShard; i++ {
 		dst[i] = data[:perShard:perShard]
 		data = data[perShard:]
 	}
-	for ; i < total; i++ {
-		b := make([]byte, perShard)
-		copy(b, data)
-		data = data[min(len(data), perShard):]
-		dst[i] = b
+	for j := 0; i+j < total; j++ {
+		dst[i+j] = padding[0]
+		padding = padding[1:]
 	}
 	return dst, nil
 }

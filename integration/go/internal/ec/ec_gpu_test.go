@@ -11,6 +11,7 @@ import (
 	"math/rand"
 	"runtime"
 	"testing"
+	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
 
@@ -89,6 +90,59 @@ func TestNoGPUFallsBackToKlauspost(t *testing.T) {
 	for i := range want {
 		if !bytes.Equal(got[i], want[i]) {
 			t.Fatalf("shard %d differs", i)
+		}
+	}
+}
+
+// Split must be klauspost's own, spare capacity included (writeservice.go:218): with
+// cap(data) >= (K+M)*perShard every shard aliases data's buffer; with less, the shards
+// that fit alias it and the rest are fresh; bytes past len are zeroed in both.
+func TestSplitSpareCapacityMatchesKlauspost(t *testing.T) {
+	ref, _ := reedsolomon.New(config.K, config.M)
+	gpu := NewService()
+	total := config.K + config.M
+	for _, n := range []int{1, 2, 10, 410, 4096, 100000} {
+		perShard := (n + config.K - 1) / config.K
+		for _, spare := range []int{0, 1, perShard - 1, perShard, 2*perShard + 3, total*perShard - n, total*perShard - n + 64} {
+			if spare < 0 {
+				continue
+			}
+			mk := func() []byte {
+				b := make([]byte, n, n+spare)
+				full := b[:cap(b)]
+				for i := range full {
+					full[i] = byte(i*7 + 1) // garbage past len: must be zeroed
+				}
+				return b
+			}
+			wantBuf, gotBuf := mk(), mk()
+			want, err1 := ref.Split(wantBuf)
+			got, err2 := gpu.Split(gotBuf)
+			if err1 != nil || err2 != nil {
+				t.Fatal(err1, err2)
+			}
+			base := func(b []byte) uintptr { return uintptr(unsafe.Pointer(&b[:1][0])) }
+			for i := 0; i < total; i++ {
+				if !bytes.Equal(got[i], want[i]) || cap(got[i]) != cap(want[i]) {
+					t.Fatalf("n %d spare %d shard %d: bytes or cap differ", n, spare, i)
+				}
+				wOff := int64(base(want[i])) - int64(base(wantBuf))
+				gOff := int64(base(got[i])) - int64(base(gotBuf))
+				wIn := wOff >= 0 && wOff < int64(cap(wantBuf))
+				gIn := gOff >= 0 && gOff < int64(cap(gotBuf))
+				if wIn != gIn || (wIn && wOff != gOff) {
+					t.Fatalf("n %d spare %d shard %d: aliasing differs (klauspost %v@%d, gpu %v@%d)", n, spare, i, wIn, wOff, gIn, gOff)
+				}
+			}
+			if err := gpu.Encode(got); err != nil {
+				t.Fatal(err)
+			}
+			_ = ref.Encode(want)
+			for i := range want {
+				if !bytes.Equal(got[i], want[i]) {
+					t.Fatalf("n %d spare %d: parity shard %d differs", n, spare, i)
+				}
+			}
 		}
 	}
 }

@@ -41,27 +41,27 @@ typedef struct {
     atomic_size_t next;
 } job_t;
 
-static void stripe_scalar(const job_t *j, uint8_t *st) {
+/* One stripe: in[c] / out[r] are its k input and e output shards, S bytes each. */
+static void stripe_scalar(const job_t *j, const uint8_t *const *in, uint8_t *const *out, size_t S) {
     for (int r = 0; r < j->e; r++) {
-        uint8_t *o = st + (size_t)j->out_idx[r] * j->shard_pitch;
-        for (size_t b = 0; b < j->S; b++) {
+        uint8_t *o = out[r];
+        for (size_t b = 0; b < S; b++) {
             uint8_t acc = 0;
-            for (int c = 0; c < j->k; c++)
-                acc ^= j->mul[r * j->k + c][st[(size_t)j->in_idx[c] * j->shard_pitch + b]];
+            for (int c = 0; c < j->k; c++) acc ^= j->mul[r * j->k + c][in[c][b]];
             o[b] = acc;
         }
     }
 }
 
-__attribute__((target("avx2"))) static void stripe_avx2(const job_t *j, uint8_t *st) {
-    const size_t S = j->S, full = S & ~(size_t)31;
+__attribute__((target("avx2"))) static void stripe_avx2(const job_t *j, const uint8_t *const *in,
+                                                       uint8_t *const *out, size_t S) {
+    const size_t full = S & ~(size_t)31;
     const __m256i mask = _mm256_set1_epi8(0x0f);
     __m256i acc[MAXE];
     for (size_t b = 0; b < full; b += 32) {
         for (int r = 0; r < j->e; r++) acc[r] = _mm256_setzero_si256();
         for (int c = 0; c < j->k; c++) {
-            __m256i x = _mm256_loadu_si256(
-                (const __m256i *)(st + (size_t)j->in_idx[c] * j->shard_pitch + b));
+            __m256i x = _mm256_loadu_si256((const __m256i *)(in[c] + b));
             __m256i xl = _mm256_and_si256(x, mask);
             __m256i xh = _mm256_and_si256(_mm256_srli_epi64(x, 4), mask);
             for (int r = 0; r < j->e; r++) {
@@ -73,40 +73,46 @@ __attribute__((target("avx2"))) static void stripe_avx2(const job_t *j, uint8_t 
             }
         }
         for (int r = 0; r < j->e; r++)
-            _mm256_storeu_si256((__m256i *)(st + (size_t)j->out_idx[r] * j->shard_pitch + b), acc[r]);
+            _mm256_storeu_si256((__m256i *)(out[r] + b), acc[r]);
     }
     for (size_t b = full; b < S; b++)
         for (int r = 0; r < j->e; r++) {
             uint8_t a = 0;
             for (int c = 0; c < j->k; c++)
-                a ^= j->mul[r * j->k + c][st[(size_t)j->in_idx[c] * j->shard_pitch + b]];
-            st[(size_t)j->out_idx[r] * j->shard_pitch + b] = a;
+                a ^= j->mul[r * j->k + c][in[c][b]];
+            out[r][b] = a;
         }
 }
 
-__attribute__((target("avx512f,avx512bw,gfni"))) static void stripe_gfni(const job_t *j, uint8_t *st) {
-    const size_t S = j->S, full = S & ~(size_t)63;
+__attribute__((target("avx512f,avx512bw,gfni"))) static void stripe_gfni(const job_t *j, const uint8_t *const *in,
+                                                                       uint8_t *const *out, size_t S) {
+    const size_t full = S & ~(size_t)63;
     __m512i acc[MAXE];
     for (size_t b = 0; b < full; b += 64) {
         for (int r = 0; r < j->e; r++) acc[r] = _mm512_setzero_si512();
         for (int c = 0; c < j->k; c++) {
-            __m512i x = _mm512_loadu_si512(
-                (const void *)(st + (size_t)j->in_idx[c] * j->shard_pitch + b));
+            __m512i x = _mm512_loadu_si512((const void *)(in[c] + b));
             for (int r = 0; r < j->e; r++) {
                 __m512i a = _mm512_set1_epi64((long long)j->gfni[r * j->k + c]);
                 acc[r] = _mm512_xor_si512(acc[r], _mm512_gf2p8affine_epi64_epi8(x, a, 0));
             }
         }
         for (int r = 0; r < j->e; r++)
-            _mm512_storeu_si512((void *)(st + (size_t)j->out_idx[r] * j->shard_pitch + b), acc[r]);
+            _mm512_storeu_si512((void *)(out[r] + b), acc[r]);
     }
     for (size_t b = full; b < S; b++)
         for (int r = 0; r < j->e; r++) {
             uint8_t a = 0;
             for (int c = 0; c < j->k; c++)
-                a ^= j->mul[r * j->k + c][st[(size_t)j->in_idx[c] * j->shard_pitch + b]];
-            st[(size_t)j->out_idx[r] * j->shard_pitch + b] = a;
+                a ^= j->mul[r * j->k + c][in[c][b]];
+            out[r][b] = a;
         }
+}
+
+static void stripe_apply(const job_t *j, const uint8_t *const *in, uint8_t *const *out, size_t S) {
+    if (j->level == 3) stripe_gfni(j, in, out, S);
+    else if (j->level == 2) stripe_avx2(j, in, out, S);
+    else stripe_scalar(j, in, out, S);
 }
 
 static void *worker(void *arg) {
@@ -117,22 +123,22 @@ static void *worker(void *arg) {
         size_t end = i + 16 < j->N ? i + 16 : j->N;
         for (; i < end; i++) {
             uint8_t *st = j->base + i * j->stripe_pitch;
-            if (j->level == 3) stripe_gfni(j, st);
-            else if (j->level == 2) stripe_avx2(j, st);
-            else stripe_scalar(j, st);
+            const uint8_t *in[MAXK];
+            uint8_t *out[MAXE];
+            for (int c = 0; c < j->k; c++) in[c] = st + (size_t)j->in_idx[c] * j->shard_pitch;
+            for (int r = 0; r < j->e; r++) out[r] = st + (size_t)j->out_idx[r] * j->shard_pitch;
+            stripe_apply(j, in, out, j->S);
         }
     }
     return NULL;
 }
 
-int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_idx,
-                             const int *out_idx, uint8_t *base, size_t stripe_pitch,
-                             size_t shard_pitch, size_t S, size_t N, int threads) {
-    if (k > MAXK || e > MAXE || k <= 0 || e < 0) return -1;
+/* Tables for an e x k coefficient matrix (scalar, split-nibble, GFNI affine). */
+static job_t *job_new(int k, int e, const uint8_t *rows) {
+    if (k > MAXK || e > MAXE || k <= 0 || e < 0) return NULL;
     job_t *j = (job_t *)aligned_alloc(64, (sizeof(job_t) + 63) & ~(size_t)63);
     memset(j, 0, sizeof(*j));
-    j->k = k; j->e = e; j->in_idx = in_idx; j->out_idx = out_idx; j->base = base;
-    j->stripe_pitch = stripe_pitch; j->shard_pitch = shard_pitch; j->S = S; j->N = N;
+    j->k = k; j->e = e;
     for (int q = 0; q < e * k; q++) {
         uint8_t f = rows[q];
         for (int v = 0; v < 256; v++) j->mul[q][v] = rso_gf_mul(f, (uint8_t)v);
@@ -166,6 +172,16 @@ int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_id
             if (f < j->level) j->level = f == 1 ? 0 : f;
         }
     }
+    return j;
+}
+
+int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_idx,
+                             const int *out_idx, uint8_t *base, size_t stripe_pitch,
+                             size_t shard_pitch, size_t S, size_t N, int threads) {
+    job_t *j = job_new(k, e, rows);
+    if (!j) return -1;
+    j->in_idx = in_idx; j->out_idx = out_idx; j->base = base;
+    j->stripe_pitch = stripe_pitch; j->shard_pitch = shard_pitch; j->S = S; j->N = N;
     atomic_init(&j->next, 0);
     if (threads < 1) threads = 1;
     pthread_t *tid = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
@@ -176,4 +192,15 @@ int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_id
     int level = j->level;
     free(j);
     return level;
+}
+
+void *rso_baseline_plan_new(int k, int e, const uint8_t *rows) { return job_new(k, e, rows); }
+
+void rso_baseline_plan_free(void *plan) { free(plan); }
+
+int rso_baseline_plan_apply(const void *plan, const uint8_t *const *in, uint8_t *const *out, size_t S) {
+    const job_t *j = (const job_t *)plan;
+    if (!j) return -1;
+    stripe_apply(j, in, out, S);
+    return j->level;
 }

@@ -84,6 +84,13 @@ void rso_encode_batch_scalar(int k, int m, uint8_t *base, size_t stripe_pitch,
 int rso_baseline_apply_batch(int k, int e, const uint8_t *rows, const int *in_idx,
                              const int *out_idx, uint8_t *base, size_t stripe_pitch,
                              size_t shard_pitch, size_t S, size_t N, int threads);
+/* The same kernels per object with tables prepared once (klauspost keeps its
+ * encode tables in the Encoder and caches decode matrices per erasure pattern):
+ * plan = e x k rows; apply computes out[r] (e shards) from in[c] (k shards), S
+ * bytes, on the calling thread.  Returns the SIMD level (-1: bad plan). */
+void *rso_baseline_plan_new(int k, int e, const uint8_t *rows);
+void rso_baseline_plan_free(void *plan);
+int rso_baseline_plan_apply(const void *plan, const uint8_t *const *in, uint8_t *const *out, size_t S);
 
 
 /* ---- SHA-256 (FIPS 180-4), the reference's cold_hash (writeservice.go:51-54,267) ---- */

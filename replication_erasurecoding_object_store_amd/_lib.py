@@ -62,7 +62,9 @@ SIGNATURES = {
     "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
     "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
     "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
+    "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
     "rs_sync": (_i, [_vp, _vp]),
+    "rs_stream_release": (_i, [_vp, _vp]),
     "rs_sha256_batch": (_i, [_vp, _vp, _sz, _sz, _sz, _vp, _vp]),
     "rs_sha256_batch_var": (_i, [_vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     "rs_coalescer_create": (_i, [_vp, _vp, _vp]),
@@ -74,12 +76,13 @@ SIGNATURES = {
     "rs_co_stats": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "rs_co_reconstruct_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_encode_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
+    "rs_co_encode_hash": (_i, [_vp, _u8pp, _szp, _sz, _u8p]),
+    "rs_co_encode_hash_many": (_i, [_vp, _sz, _u8pp, _szp, _szp, _u8p, ctypes.POINTER(_i)]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
     "rs_device_copy": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "rs_set_blocks_per_cu": (_i, [_vp, _i]),
-    "rs_set_kernel_variant": (_i, [_vp, _i]),
     "rs_set_parity_pad_writes": (_i, [_vp, _i]),
     "rs_set_host_zero_copy": (_i, [_vp, _i]),
     "rs_last_host_path": (ctypes.c_char_p, [_vp]),

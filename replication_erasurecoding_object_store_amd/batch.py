@@ -79,11 +79,19 @@ class BatchEngine(Service):
                                                        _stream_handle(stream)))
 
     def reconstruct_out(self, data, parity, out, shard_len: int, n_stripes: int, present_masks=None,
-                        masks_dev=None, shard_pitch: Optional[int] = None, stream=None) -> None:
+                        masks_dev=None, shard_pitch: Optional[int] = None, stream=None,
+                        max_missing: int = 0) -> None:
         """Out-of-place: the r-th missing shard of stripe i goes to out[i, r].
-        `present_masks` (host: int or uint32 array) or `masks_dev` (device tensor)."""
+        `present_masks` (host: int or uint32 array) or `masks_dev` (device tensor);
+        with device masks, `max_missing` > 0 is the caller's bound on erasures per
+        stripe (rs_reconstruct_batch_out_devmask)."""
         P = shard_pitch or data.shape[-1]
         osp = out.shape[-2] * out.shape[-1] if out.dim() == 3 else self.m * P
+        if masks_dev is not None and max_missing:
+            _check(_lib.lib().rs_reconstruct_batch_out_devmask(
+                self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(), self.m * P, P, shard_len, n_stripes,
+                masks_dev.data_ptr(), max_missing, out.data_ptr(), osp, _stream_handle(stream)))
+            return
         if masks_dev is not None:
             mptr, n, on_dev = ctypes.c_void_p(masks_dev.data_ptr()), n_stripes, 1
             keep = None
@@ -156,6 +164,10 @@ class BatchEngine(Service):
     def sync(self, stream=None) -> None:
         _check(_lib.lib().rs_sync(self.ctx, _stream_handle(stream)))
 
+    def stream_release(self, stream=None) -> None:
+        """rs_sync, then the engine forgets the stream (before destroying it)."""
+        _check(_lib.lib().rs_stream_release(self.ctx, _stream_handle(stream)))
+
     # ---- host-resident (synchronous, pipelined H2D / kernel / D2H) -------------------
     def encode_host(self, data: np.ndarray, parity: np.ndarray, shard_len: int, n_stripes: int,
                     shard_pitch: Optional[int] = None) -> None:
@@ -221,7 +233,3 @@ class BatchEngine(Service):
     def set_parity_pad_writes(self, enable: bool) -> None:
         """Encode may write parity slot padding up to the next 128-B line (rsgpu.h)."""
         _check(_lib.lib().rs_set_parity_pad_writes(self.ctx, 1 if enable else 0))
-
-    def set_kernel_variant(self, v: int) -> None:
-        """0 = by shape, 1 = grid-stride kernels, 2/3 = pipelined (2/3 task slots)."""
-        _check(_lib.lib().rs_set_kernel_variant(self.ctx, v))

@@ -77,6 +77,42 @@ class CoalescingService(Service):
     def EncodeMany(self, objects: Sequence[List[bytearray]]) -> List[Optional[ECError]]:
         return self._many("encode", objects, False)
 
+    def EncodeHash(self, shards: List[bytearray], value_len: int) -> bytes:
+        """Encode (parity in place) plus the write path's cold_hash in the same
+        coalesced batch (rs_co_encode_hash): returns SHA-256 of the first value_len
+        bytes of the data shards -- the value Split was given (writeservice.go:218-222,
+        :267)."""
+        if len(shards) != self.k + self.m:
+            raise ECError(ErrTooFewShards)
+        ptrs, lens, keep = _shard_array(shards, 0, fill_missing=False)
+        digest = (ctypes.c_uint8 * 32)()
+        _check(_lib.lib().rs_co_encode_hash(self._co, ptrs, lens, value_len, ctypes.cast(digest, _lib._u8p)))
+        del keep
+        return bytes(digest)
+
+    def EncodeHashMany(self, objects: Sequence[List[bytearray]], value_lens: Sequence[int]):
+        """rs_co_encode_hash_many: per object (error or None, digest or None)."""
+        t = self.k + self.m
+        n = len(objects)
+        ptrs = (_lib._u8p * (n * t))()
+        lens = (ctypes.c_size_t * (n * t))()
+        keep = []
+        for i, sh in enumerate(objects):
+            if len(sh) != t:
+                raise ECError(ErrTooFewShards)
+            p, ln, kp = _shard_array(sh, 0, fill_missing=False)
+            keep.append(kp)
+            for q in range(t):
+                ptrs[i * t + q] = p[q]
+                lens[i * t + q] = ln[q]
+        vl = (ctypes.c_size_t * max(1, n))(*value_lens)
+        digests = (ctypes.c_uint8 * (32 * max(1, n)))()
+        rcs = (ctypes.c_int * max(1, n))()
+        _check(_lib.lib().rs_co_encode_hash_many(self._co, n, ptrs, lens, vl, ctypes.cast(digests, _lib._u8p), rcs))
+        del keep
+        raw = bytes(digests)
+        return [(ECError(rcs[i]) if rcs[i] else None, None if rcs[i] else raw[32 * i:32 * i + 32]) for i in range(n)]
+
     def stats(self) -> dict:
         v = [ctypes.c_uint64() for _ in range(4)]
         _check(_lib.lib().rs_co_stats(self._co, *[ctypes.byref(x) for x in v]))

@@ -54,6 +54,7 @@
 #include "../../include/rsgpu.h"
 #include "rs_engine.hpp"
 #include "rs_host_util.hpp"
+#include "rs_sha256.hpp"
 
 namespace {
 
@@ -101,6 +102,8 @@ struct Batch {
   std::atomic<uint64_t> ticket{kClosedBit};
   std::atomic<uint32_t> parity_in{0};  // some slot needs its parity shards uploaded
   std::atomic<uint32_t> fill_err{0};   // a slot's plan could not be resolved (plan mode)
+  std::atomic<uint32_t> max_missing{0};  // most shards any slot fills: the launch's erasure bound
+  std::atomic<uint32_t> hash_in{0};      // some slot wants the SHA-256 of its value (cold_hash)
   size_t n_final = 0;          // slots of the closed batch (published by the group words)
   int rc = RS_OK;              // published by the group words
   Clock::time_point deadline;
@@ -137,7 +140,8 @@ struct Batch {
   rs::PinnedBuf host;
   rs::DevBuf dev;
   // region offsets (same in host staging and device slab)
-  size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_plans = 0, o_bad = 0, bytes = 0;
+  size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_plans = 0, o_bad = 0, o_hoff = 0, o_hlen = 0,
+         o_digest = 0, bytes = 0;
 };
 
 // Reserves up to `want` consecutive slots of batch b in generation gen.
@@ -201,6 +205,11 @@ struct Dispatcher {
   std::thread launcher, completer;
   std::atomic<uint32_t> work{0};      // bumped on every event the launcher may act on
   std::atomic<bool> launcher_idle{false};
+  // Set before the launcher sleeps: true if a newly staged slot could start a batch
+  // (an execution slot was free), false if only a completion can (then callers
+  // skip the wake-up syscall: with callers outnumbering cores that was one futex
+  // wake per call while the launcher waited for the device).
+  std::atomic<bool> launcher_wants_callers{true};
   std::atomic<int> executing{0};
   std::mutex run_mu;
   std::condition_variable run_cv;
@@ -211,10 +220,14 @@ struct Dispatcher {
 // Wakes the launcher if it sleeps.  The handshake with launcher_loop's sleep
 // (idle = true, then re-read work) is store -> load on both sides, so both are
 // sequentially consistent: with acquire / release alone x86 may reorder each
-// side's load before its store and both miss (a lost wake-up).
-void poke(Dispatcher* d) {
+// side's load before its store and both miss (a lost wake-up).  A caller's poke
+// (from_caller) wakes the launcher only if it went to sleep able to start a batch;
+// completions and shutdown always wake it.
+void poke(Dispatcher* d, bool from_caller = false) {
   d->work.fetch_add(1, std::memory_order_seq_cst);
-  if (d->launcher_idle.load(std::memory_order_seq_cst)) futex_wake(&d->work, 1);
+  if (d->launcher_idle.load(std::memory_order_seq_cst) &&
+      (!from_caller || d->launcher_wants_callers.load(std::memory_order_seq_cst)))
+    futex_wake(&d->work, 1);
 }
 
 }  // namespace
@@ -244,13 +257,13 @@ struct rs_coalescer {
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
   // diagnostics (printed at destroy when RS_CO_DEBUG is set)
-  std::atomic<uint64_t> straggle_ns{0}, exec_ns{0}, free_waits{0}, launches_idle{0};
+  std::atomic<uint64_t> straggle_ns{0}, exec_ns{0}, free_waits{0}, launches_idle{0}, launch_ns{0};
 
   ~rs_coalescer() {
     if (std::getenv("RS_CO_DEBUG"))
-      std::fprintf(stderr, "[rs_coalescer] batches %llu straggle_ms %.1f exec_ms %.1f free_waits %llu\n",
-                   (unsigned long long)n_batches.load(), straggle_ns.load() / 1e6, exec_ns.load() / 1e6,
-                   (unsigned long long)free_waits.load());
+      std::fprintf(stderr, "[rs_coalescer] batches %llu straggle_ms %.1f launch_ms %.1f exec_ms %.1f free_waits %llu\n",
+                   (unsigned long long)n_batches.load(), straggle_ns.load() / 1e6, launch_ns.load() / 1e6,
+                   exec_ns.load() / 1e6, (unsigned long long)free_waits.load());
     stop.store(true, std::memory_order_release);
     for (auto& d : disp) {
       poke(d.get());
@@ -286,7 +299,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->S = S;
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
   rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, b->engine)));
-  const size_t per = b->P * (k + 2 * m) + 16;  // shards + out + mask + plan + bad
+  const size_t per = b->P * (k + 2 * m) + 64;  // shards + out + mask + plan + bad + hash args + digest
   const size_t cap = std::max<size_t>(
       1, std::min({co->max_batch, co->max_bytes / per, size_t(b->n_groups_alloc) * Batch::kGroup}));
   b->cap.store(cap, std::memory_order_relaxed);
@@ -296,7 +309,10 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->o_masks = b->o_out + round_up(cap * m * b->P, 256);
   b->o_plans = b->o_masks + round_up(cap * 4, 256);
   b->o_bad = b->o_plans + round_up(cap * 8, 256);
-  b->bytes = b->o_bad + round_up(cap * 4, 256);
+  b->o_hoff = b->o_bad + round_up(cap * 4, 256);
+  b->o_hlen = b->o_hoff + round_up(cap * 8, 256);
+  b->o_digest = b->o_hlen + round_up(cap * 8, 256);
+  b->bytes = b->o_digest + round_up(cap * 32, 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   if (!b->done_ev) RS_HIP(hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming));
   if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
@@ -311,6 +327,8 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->released.store(0, std::memory_order_relaxed);
   b->parity_in.store(0, std::memory_order_relaxed);
   b->fill_err.store(0, std::memory_order_relaxed);
+  b->max_missing.store(0, std::memory_order_relaxed);
+  b->hash_in.store(0, std::memory_order_relaxed);
   b->rc = RS_OK;
   b->free = false;
   b->deadline = Clock::now() + co->max_wait;
@@ -344,6 +362,10 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_masks), host_at(b, b->o_masks), n * 4, hipMemcpyHostToDevice, st));
     if (b->kind == Kind::kApply && !co->per_stripe)
       RS_HIP(hipMemcpyAsync(dev_at(b, b->o_plans), host_at(b, b->o_plans), n * 8, hipMemcpyHostToDevice, st));
+    if (b->hash_in.load(std::memory_order_relaxed)) {
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_hoff), host_at(b, b->o_hoff), n * 8, hipMemcpyHostToDevice, st));
+      RS_HIP(hipMemcpyAsync(dev_at(b, b->o_hlen), host_at(b, b->o_hlen), n * 8, hipMemcpyHostToDevice, st));
+    }
   }
   int rc;
   if (b->kind == Kind::kVerify) {
@@ -355,20 +377,40 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
   } else {
     if (b->fill_err.load(std::memory_order_acquire)) return RS_ERR_DEVICE;
     if (co->per_stripe) {
+      // erasure bound = the most any slot misses (an encode slot: m): a batch of
+      // 1-2 erasure repairs runs the E = 1 / 2 kernels
+      const int bound = static_cast<int>(b->max_missing.load(std::memory_order_acquire));
       rc = rs::engine_reconstruct_batch_out(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
-                                            reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, at(b->o_out),
-                                            m * P, st);
+                                            reinterpret_cast<const uint32_t*>(at(b->o_masks)), n, 1, bound,
+                                            at(b->o_out), m * P, st);
     } else {  // k+m > 16: every slot names its plan (encode, reconstruct or ReconstructData)
       rc = rs::engine_apply_batch_plans(eng, at(b->o_data), k * P, at(b->o_parity), m * P, P, b->S, n,
                                         reinterpret_cast<const uint64_t*>(at(b->o_plans)), at(b->o_out), m * P,
                                         st);
     }
     if (rc) return rc;
+    if (b->hash_in.load(std::memory_order_relaxed)) {
+      // cold_hash of every slot that asked for it, over the same staged data shards
+      // (value byte o in data shard o / S of the slot, offset o % S)
+      rs::Sha256Args ha{at(b->o_data), 0, reinterpret_cast<const uint64_t*>(at(b->o_hoff)),
+                        reinterpret_cast<const uint64_t*>(at(b->o_hlen)), 0, static_cast<uint32_t>(n),
+                        at(b->o_digest), b->S, P};
+      if (rs::launch_sha256(ha, st)) return RS_ERR_DEVICE;
+      if (!zc)
+        RS_HIP(hipMemcpyAsync(host_at(b, b->o_digest), dev_at(b, b->o_digest), n * 32, hipMemcpyDeviceToHost, st));
+    }
     if (!zc)
       RS_HIP(hipMemcpyAsync(host_at(b, b->o_out), dev_at(b, b->o_out), n * m * P, hipMemcpyDeviceToHost, st));
   }
   RS_HIP(hipEventRecord(b->done_ev, st));
   return RS_OK;  // every mask was checked (>= k present) before it was staged
+}
+
+// Raises a batch's erasure bound to at least e (a slot's missing-shard count).
+void note_missing(Batch* b, uint32_t e) {
+  uint32_t cur = b->max_missing.load(std::memory_order_relaxed);
+  while (cur < e && !b->max_missing.compare_exchange_weak(cur, e, std::memory_order_release, std::memory_order_relaxed)) {
+  }
 }
 
 uint64_t hot_word(uint32_t gen, int index) {
@@ -477,7 +519,10 @@ void launcher_loop(rs_coalescer* co, Dispatcher* d) {
                                 std::memory_order_relaxed);
       pick->n_final = n;
       d->executing.fetch_add(1, std::memory_order_acq_rel);
+      const auto tl0 = Clock::now();
       const int rc = launch_batch(co, pick, n);
+      co->launch_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count(),
+                              std::memory_order_relaxed);
       if (rc) {
         complete(co, d, pick, rc);
         continue;
@@ -488,6 +533,7 @@ void launcher_loop(rs_coalescer* co, Dispatcher* d) {
       continue;
     }
     // nothing to start: sleep until a caller stages, a slot frees or a linger ends
+    d->launcher_wants_callers.store(slot, std::memory_order_seq_cst);
     d->launcher_idle.store(true, std::memory_order_seq_cst);
     if (d->work.load(std::memory_order_seq_cst) == w && !co->stop.load(std::memory_order_acquire)) {
       if (wake_at != Clock::time_point::max()) {
@@ -613,7 +659,7 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
       if (b->slot_state[slot0 + j].compare_exchange_strong(st, kSlotStaged, std::memory_order_acq_rel)) ++staged;
     }
     if (staged) b->filled.fetch_add(staged, std::memory_order_release);
-    poke(co->disp[static_cast<size_t>(b->engine)].get());
+    poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
     wait_epoch(&b->grp[grp], epoch);
     wake_more(b, epoch, 2);
     const int rc = b->rc;
@@ -702,19 +748,30 @@ void set_plan(const rs_coalescer* co, Batch* b, size_t slot, uint64_t present, b
   reinterpret_cast<uint64_t*>(host_at(b, b->o_plans))[slot] = reinterpret_cast<uint64_t>(plan);
 }
 
+// Per-slot cold_hash request: the first value_len bytes of the slot's k data
+// shards (offsets relative to the data region), or kSha256Skip for none.
+void set_hash(Batch* b, int k, size_t slot, uint64_t value_len) {
+  reinterpret_cast<uint64_t*>(host_at(b, b->o_hlen))[slot] = value_len;
+  reinterpret_cast<uint64_t*>(host_at(b, b->o_hoff))[slot] = static_cast<uint64_t>(slot) * k * b->P;
+  if (value_len != rs::kSha256Skip) b->hash_in.store(1, std::memory_order_relaxed);
+}
+
 void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
   const int k = co->k, m = co->m, t = k + m;
   const size_t P = b->P;
+  set_hash(b, k, slot, rs::kSha256Skip);
   for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
     if (!it.lens[i]) continue;
     ++staged;
     uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P) : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
     std::memcpy(dst, it.shards[i], it.S);
   }
-  if (co->per_stripe)
+  if (co->per_stripe) {
     reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
-  else
+    note_missing(b, static_cast<uint32_t>(t - __builtin_popcount(it.present)));
+  } else {
     set_plan(co, b, slot, it.present, data_only, false);
+  }
 }
 
 void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
@@ -812,28 +869,47 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
 
 void rs_coalescer_destroy(rs_coalescer* co) { delete co; }
 
-int rs_co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens) {
+// Encode, and with value_len != kSha256Skip also the SHA-256 of the value's first
+// value_len bytes (its data shards in order) into digest.
+static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, uint64_t value_len,
+                     uint8_t* digest) {
   if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
   const int k = co->k, m = co->m;
+  const bool hash = value_len != rs::kSha256Skip;
+  if (hash && !digest) return RS_ERR_INVALID_ARG;
   size_t S = 0;
   int rc = rs::check_shards(k + m, lens, false, &S);
   if (rc) return rc;
-  if (m == 0) return RS_OK;
+  if (hash && value_len > static_cast<uint64_t>(k) * S) return RS_ERR_INVALID_ARG;
+  if (m == 0) return hash ? RS_ERR_NOT_SUPPORTED : RS_OK;
   for (int i = 0; i < k + m; ++i)
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
   auto fill = [&](Batch* b, size_t slot) {
     for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    if (co->per_stripe)
+    set_hash(b, k, slot, value_len);
+    if (co->per_stripe) {
       reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
-    else
+      note_missing(b, static_cast<uint32_t>(m));
+    } else {
       set_plan(co, b, slot, data_mask, false, true);
+    }
   };
   auto drain = [&](Batch* b, size_t slot) {
     for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+    if (hash) std::memcpy(digest, host_at(b, b->o_digest + slot * 32), 32);
   };
   return submit(co, Kind::kApply, S, false, fill, drain);
+}
+
+int rs_co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens) {
+  return co_encode(co, shards, lens, rs::kSha256Skip, nullptr);
+}
+
+int rs_co_encode_hash(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, size_t value_len,
+                      uint8_t* digest) {
+  return co_encode(co, shards, lens, value_len, digest);
 }
 
 int rs_co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens) {
@@ -896,13 +972,16 @@ int rs_co_reconstruct_many(rs_coalescer* co, size_t n_objects, uint8_t* const* s
 }
 
 // Bulk encode of many objects (e.g. a batch of writes): per object rs_encode's
-// contract, results in rcs[i].
-int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, const size_t* lens, int* rcs) {
+// contract, results in rcs[i]; with value_lens / digests, also each object's
+// cold_hash (rs_co_encode_hash's contract).
+static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, const size_t* lens,
+                          const size_t* value_lens, uint8_t* digests, int* rcs) {
   if (!co || (n_objects && (!shards || !lens || !rcs))) return RS_ERR_INVALID_ARG;
+  if (n_objects && (value_lens != nullptr) != (digests != nullptr)) return RS_ERR_INVALID_ARG;
   const int k = co->k, m = co->m;
   const size_t t = static_cast<size_t>(k + m);
+  const bool hash = value_lens != nullptr;
   co->calls.fetch_add(n_objects, std::memory_order_relaxed);
-  std::vector<size_t> Ss(n_objects, 0);
   std::map<size_t, std::vector<size_t>> by_len;
   for (size_t i = 0; i < n_objects; ++i) {
     size_t S = 0;
@@ -910,8 +989,9 @@ int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards
     for (size_t j = 0; rc == RS_OK && j < t; ++j)
       if (!shards[i * t + j]) rc = RS_ERR_INVALID_ARG;
     if (rc == RS_OK && S > 0xFFFFFFF0u) rc = RS_ERR_INVALID_ARG;
+    if (rc == RS_OK && hash && value_lens[i] > static_cast<uint64_t>(k) * S) rc = RS_ERR_INVALID_ARG;
+    if (rc == RS_OK && hash && m == 0) rc = RS_ERR_NOT_SUPPORTED;
     rcs[i] = rc;
-    Ss[i] = S;
     if (rc == RS_OK && m > 0) by_len[S].push_back(i);
   }
   const uint32_t data_mask = (1u << k) - 1u;
@@ -923,14 +1003,18 @@ int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards
         [&](Batch* b, size_t slot, size_t j) {
           uint8_t* const* sh = shards + idx[j] * t;
           for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
-          if (co->per_stripe)
+          set_hash(b, k, slot, hash ? value_lens[idx[j]] : rs::kSha256Skip);
+          if (co->per_stripe) {
             reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
-          else
+            note_missing(b, static_cast<uint32_t>(m));
+          } else {
             set_plan(co, b, slot, data_mask, false, true);
+          }
         },
         [&](Batch* b, size_t slot, size_t j) {
           uint8_t* const* sh = shards + idx[j] * t;
           for (int r = 0; r < m; ++r) std::memcpy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+          if (hash) std::memcpy(digests + idx[j] * 32, host_at(b, b->o_digest + slot * 32), 32);
         });
     if (rc) {
       for (size_t i : idx) rcs[i] = rc;
@@ -938,6 +1022,16 @@ int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards
     }
   }
   return RS_OK;
+}
+
+int rs_co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, const size_t* lens, int* rcs) {
+  return co_encode_many(co, n_objects, shards, lens, nullptr, nullptr, rcs);
+}
+
+int rs_co_encode_hash_many(rs_coalescer* co, size_t n_objects, uint8_t* const* shards, const size_t* lens,
+                           const size_t* value_lens, uint8_t* digests, int* rcs) {
+  if (n_objects && (!value_lens || !digests)) return RS_ERR_INVALID_ARG;
+  return co_encode_many(co, n_objects, shards, lens, value_lens, digests, rcs);
 }
 
 int rs_co_stats(rs_coalescer* co, uint64_t* calls, uint64_t* batches, uint64_t* stripes, uint64_t* max_batch) {

@@ -32,7 +32,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <fstream>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -115,23 +117,6 @@ using rs::round_up;
 // pattern wants few waves (tools/hbm_probe2.hip: 1-2 WG/CU beat higher occupancy)
 // until the per-byte VALU work (K*E lookups) needs more waves to hide latency.
 int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
-
-// Default kernel family per shape (rs_set_kernel_variant): 1 = grid-stride
-// apply / bitsliced encode, 2 / 3 = pipelined with 2 / 3 task slots per wave,
-// 4 = grid-stride lookup kernels only.
-// RS_KERNEL_VARIANT=<1..3> in the environment overrides it (tests run the whole
-// suite on each family).
-int default_variant(int k, int e, bool per_stripe) {
-  static const int forced = [] {
-    const char* v = std::getenv("RS_KERNEL_VARIANT");
-    return v ? std::atoi(v) : 0;
-  }();
-  if (forced >= 1 && forced <= 4) return forced;
-  (void)k;
-  (void)e;
-  (void)per_stripe;
-  return 1;
-}
 
 // ---- plan construction -----------------------------------------------------
 // 3-chunk v_perm tables for coefficient f (see rs_kernels.hip):
@@ -256,7 +241,16 @@ struct Layout {
 constexpr int kHostStreams = 4;
 constexpr size_t kHostChunkBytes = size_t(16) << 20;  // device bytes per chunk
 constexpr size_t kUploadSlots = 8;
-constexpr uint32_t kStatusWords = 1024;  // per-stream deferred-error words per engine
+constexpr uint32_t kStatusChunk = 1024;  // per-stream deferred-error words per allocation
+constexpr uint32_t kStatusChunks = 4096;  // at most 4 M streams with words at once per engine
+
+// Device words the per-stripe kernels OR their errors into, and the pinned words
+// rs_sync reads them back through.  Chunks are never freed before the engine, so a
+// word's address stays valid for the kernels that hold it.
+struct StatusChunk {
+  DevBuf dev;
+  PinnedBuf host;
+};
 
 // Context-wide "what ran last" (measurement helpers).
 struct Shared {
@@ -275,7 +269,6 @@ struct Engine {
   const std::vector<uint32_t>* h_lut = nullptr;
   Shared* shared = nullptr;
   int blocks_per_cu = 0;                  // 0 = by shape
-  int variant = 0;                        // kernel family (rs_set_kernel_variant): 0 = by shape
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
@@ -289,10 +282,12 @@ struct Engine {
 
   // Deferred per-stripe errors (device-resident masks): one word per stream, so
   // rs_sync(stream) reports and clears exactly the errors of kernels on that stream.
+  // rs_stream_release(stream) returns the stream's word to status_free.
   std::mutex status_mu;
   std::unordered_map<hipStream_t, uint32_t> status_idx;
-  DevBuf d_status;
-  PinnedBuf h_status;
+  std::vector<uint32_t> status_free;
+  std::unique_ptr<StatusChunk> status_chunks[kStatusChunks];  // fixed slots: read without the mutex
+  uint32_t status_next = 0;  // words handed out from the chunks so far
 
   std::mutex lane_mu;
   std::condition_variable lane_cv;
@@ -312,7 +307,47 @@ struct Engine {
 
   std::atomic<int> inflight{0};           // calls running on this engine (dispatch)
 
+  // One persistent host thread per engine runs its share of a multi-GPU host batch
+  // (fan_out), started on first use.
+  std::mutex work_mu;
+  std::condition_variable work_cv;
+  std::deque<std::function<void()>> work;
+  std::thread worker;
+  bool work_stop = false;
+
+  // Queues fn on this engine's worker; false if the thread cannot be started.
+  bool post(std::function<void()> fn) {
+    std::lock_guard<std::mutex> g(work_mu);
+    if (!worker.joinable()) {
+      try {
+        worker = std::thread([this] {
+          std::unique_lock<std::mutex> lk(work_mu);
+          for (;;) {
+            work_cv.wait(lk, [this] { return work_stop || !work.empty(); });
+            if (work.empty()) return;  // stopping, nothing queued
+            std::function<void()> f = std::move(work.front());
+            work.pop_front();
+            lk.unlock();
+            f();
+            lk.lock();
+          }
+        });
+      } catch (...) {
+        return false;
+      }
+    }
+    work.push_back(std::move(fn));
+    work_cv.notify_one();
+    return true;
+  }
+
   ~Engine() {  // runs under the rs_ctx destructor's DeviceScope
+    {
+      std::lock_guard<std::mutex> g(work_mu);
+      work_stop = true;
+      work_cv.notify_all();
+    }
+    if (worker.joinable()) worker.join();
     (void)hipDeviceSynchronize();
     for (auto& s : uploads)
       if (s.done) (void)hipEventDestroy(s.done);
@@ -390,9 +425,10 @@ Engine* engine_for_stream(rs_ctx* c, hipStream_t s) {
 }
 
 // Runs fn(engine, first_stripe, n_stripes) over contiguous near-equal stripe
-// ranges, one per engine, in parallel (one host thread per engine).
-// Small batches stay on one engine: a share below ~8 MiB of user data is not worth
-// a thread and a second device's launch.
+// ranges, one per engine, in parallel: range 0 on the calling
+// thread, the others on the engines' persistent worker threads.  Small batches stay
+// on one engine: a share below ~8 MiB of user data is not worth a second device's
+// launch.  Never throws (a range whose worker cannot run is run inline).
 template <class Fn>
 int fan_out(rs_ctx* c, size_t N, size_t user_bytes_per_stripe, Fn&& fn) {
   const size_t ne = c->engines.size();
@@ -420,30 +456,78 @@ int fan_out(rs_ctx* c, size_t N, size_t user_bytes_per_stripe, Fn&& fn) {
     }
     const size_t base = N / use, extra = N % use;
     const size_t s0 = j * base + std::min(j, extra);
-    rcs[j] = fn(e, s0, base + (j < extra ? 1 : 0));
+    try {
+      rcs[j] = fn(e, s0, base + (j < extra ? 1 : 0));
+    } catch (...) {
+      rcs[j] = RS_ERR_DEVICE;
+    }
   };
-  std::vector<std::thread> th;
-  th.reserve(use - 1);
-  for (size_t j = 1; j < use; ++j) th.emplace_back(run, j);
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t left = use - 1;
+  auto done_one = [&] {
+    std::lock_guard<std::mutex> g(mu);
+    if (--left == 0) cv.notify_all();
+  };
+  for (size_t j = 1; j < use; ++j) {
+    Engine* e = c->engines[(start + j) % ne].get();
+    bool posted = false;
+    try {
+      posted = e->post([&, j] {
+        run(j);
+        done_one();
+      });
+    } catch (...) {
+    }
+    if (!posted) {
+      run(j);
+      done_one();
+    }
+  }
   run(0);
-  for (auto& t : th) t.join();
+  {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return left == 0; });
+  }
   for (int rc : rcs)
     if (rc) return rc;
   return RS_OK;
 }
 
+uint32_t* status_dev(Engine* e, uint32_t idx) {
+  return static_cast<uint32_t*>(e->status_chunks[idx / kStatusChunk]->dev.p) + idx % kStatusChunk;
+}
+uint32_t* status_host(Engine* e, uint32_t idx) {
+  return static_cast<uint32_t*>(e->status_chunks[idx / kStatusChunk]->host.p) + idx % kStatusChunk;
+}
+
+// The deferred-error word of stream s (a new zeroed one on its first per-stripe
+// launch), or nullptr if no memory is left for it.  Caller holds a DeviceScope.
 uint32_t* status_word(Engine* e, hipStream_t s) {
   std::lock_guard<std::mutex> g(e->status_mu);
   auto it = e->status_idx.find(s);
+  if (it != e->status_idx.end()) return status_dev(e, it->second);
   uint32_t idx;
-  if (it != e->status_idx.end()) {
-    idx = it->second;
+  if (!e->status_free.empty()) {
+    idx = e->status_free.back();  // zeroed when it was released
+    e->status_free.pop_back();
   } else {
-    // the last word is shared by streams beyond the first kStatusWords-1
-    idx = static_cast<uint32_t>(std::min<size_t>(e->status_idx.size(), kStatusWords - 1));
-    e->status_idx.emplace(s, idx);
+    idx = e->status_next;
+    if (idx / kStatusChunk >= kStatusChunks) return nullptr;
+    if (!e->status_chunks[idx / kStatusChunk]) {
+      auto ch = std::make_unique<StatusChunk>();
+      ch->host.numa = e->numa;
+      if (ch->dev.ensure(kStatusChunk * 4) || ch->host.ensure(kStatusChunk * 4) ||
+          hipMemset(ch->dev.p, 0, kStatusChunk * 4) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      e->status_chunks[idx / kStatusChunk] = std::move(ch);
+    }
+    ++e->status_next;
   }
-  return static_cast<uint32_t*>(e->d_status.p) + idx;
+  e->status_idx.emplace(s, idx);
+  return status_dev(e, idx);
 }
 
 rs::KernelArgs make_args(Engine* e, const Layout& L, size_t S, size_t N) {
@@ -473,7 +557,7 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   // the encode plan with a verified generated XOR program -> bitsliced kernel
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
-  a.status = per_stripe ? status_word(e, s) : nullptr;
+  if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
   if (e->parity_pad && a.data_inputs && !a.out) {
     // rs_set_parity_pad_writes: run encode over whole 128-B lines of the slot
     const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
@@ -483,10 +567,9 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
       a.full_cols = static_cast<uint32_t>(s_eff / 16);
     }
   }
-  const int variant = e->variant > 0 ? e->variant : default_variant(e->k, e_out, per_stripe);
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : ((variant == 2 || variant == 3) ? 1 : default_blocks_per_cu(e->k, e_out));
-  const char* name = rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc),
-                                      static_cast<uint32_t>(e->cu_count), s, false, variant);
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
+  const char* name =
+      rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
   e->shared->last_kernel.store(name);
   RS_HIP(hipGetLastError());
@@ -497,7 +580,7 @@ int launch_verify_args(Engine* e, rs::KernelArgs& a, hipStream_t s) {
   a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e->m);
   const char* name =
-      rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s, false);
+      rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
   e->shared->last_kernel.store(name);
   RS_HIP(hipGetLastError());
@@ -894,9 +977,6 @@ int create_engine(rs_ctx* c, int device, const PlanSet& ps, std::unique_ptr<Engi
       return RS_ERR_DEVICE;
     e->have_lut = true;
   }
-  e->h_status.numa = e->numa;
-  if (e->d_status.ensure(kStatusWords * 4) || e->h_status.ensure(kStatusWords * 4)) return RS_ERR_DEVICE;
-  if (hipMemset(e->d_status.p, 0, kStatusWords * 4) != hipSuccess) return RS_ERR_DEVICE;
   *out = std::move(e);
   return RS_OK;
 }
@@ -967,7 +1047,8 @@ int engine_encode_batch(Engine* e, const uint8_t* data, size_t data_sp, uint8_t*
 
 int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
                                  size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
-                                 size_t n_masks, int masks_on_device, uint8_t* out, size_t out_sp, hipStream_t s) {
+                                 size_t n_masks, int masks_on_device, int max_missing, uint8_t* out, size_t out_sp,
+                                 hipStream_t s) {
   if (N == 0) return RS_OK;
   if (S == 0) return RS_ERR_SHARD_NO_DATA;
   if (!batch_sizes_ok(S, N, pitch)) return RS_ERR_INVALID_ARG;
@@ -980,26 +1061,28 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
   a.out_sp = out_sp;
   if (masks_on_device) {
     if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
-    if (!out_layout_ok(out_sp, pitch, S, N, e->m)) return RS_ERR_INVALID_ARG;
+    if (max_missing < 0) return RS_ERR_INVALID_ARG;
+    const int bound = max_missing > 0 ? std::min(max_missing, e->m) : e->m;
+    if (!out_layout_ok(out_sp, pitch, S, N, bound)) return RS_ERR_INVALID_ARG;
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
     a.present_masks = masks;
-    return launch(e, a, e->m, true, s);
+    return launch(e, a, bound, true, s);
   }
   if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
-  int max_missing = 0;
+  int most = 0;
   for (size_t i = 0; i < n_masks; ++i) {
     const int np = __builtin_popcount(masks[i] & full);
     if (np < e->k) return RS_ERR_TOO_FEW_SHARDS;
-    max_missing = std::max(max_missing, t - np);
+    most = std::max(most, t - np);
   }
-  if (max_missing == 0) return RS_OK;
-  if (!out_layout_ok(out_sp, pitch, S, N, max_missing)) return RS_ERR_INVALID_ARG;
+  if (most == 0) return RS_OK;
+  if (!out_layout_ok(out_sp, pitch, S, N, most)) return RS_ERR_INVALID_ARG;
   if (n_masks == 1) {
     const uint8_t* plan = nullptr;
     int rc = uniform_plan(e, masks[0] & full, false, &plan);
     if (rc) return rc;
     a.plans = plan;
-    return launch(e, a, max_missing, false, s);
+    return launch(e, a, most, false, s);
   }
   if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
   UploadGuard ug;
@@ -1008,7 +1091,7 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
   if (rc) return rc;
   a.plans = static_cast<const uint8_t*>(e->d_plans.p);
   a.present_masks = dm;
-  return launch(e, a, max_missing, true, s);
+  return launch(e, a, most, true, s);
 }
 
 int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan) {
@@ -1138,7 +1221,7 @@ int rs_create_multi(int k, int m, uint64_t device_mask, int flags, rs_ctx** out)
     }
     devs.push_back(d);
   }
-  if (device_mask >> std::min(ndev, 64)) return RS_ERR_NO_DEVICE;  // names a device that does not exist
+  if (ndev < 64 && (device_mask >> ndev)) return RS_ERR_NO_DEVICE;  // names a device that does not exist
   if (devs.empty()) return RS_ERR_NO_DEVICE;
   return rs_create_devices(k, m, devs.data(), static_cast<int>(devs.size()), flags, out);
 }
@@ -1317,7 +1400,20 @@ int rs_reconstruct_batch_out(rs_ctx* c, const uint8_t* data, size_t data_sp, con
   if (!e) return RS_ERR_INVALID_ARG;
   DeviceScope ds(e->device);
   return rs::engine_reconstruct_batch_out(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, masks, n_masks,
-                                          masks_on_device, out, out_sp, as_stream(stream));
+                                          masks_on_device, 0, out, out_sp, as_stream(stream));
+}
+
+int rs_reconstruct_batch_out_devmask(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                     size_t parity_sp, size_t shard_pitch, size_t S, size_t N,
+                                     const uint32_t* masks_dev, int max_missing, uint8_t* out, size_t out_sp,
+                                     void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !masks_dev || !out) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
+  return rs::engine_reconstruct_batch_out(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, masks_dev, N, 1,
+                                          max_missing, out, out_sp, as_stream(stream));
 }
 
 int rs_verify_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
@@ -1362,7 +1458,10 @@ int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8
   return launch(e, a, c->m, true, as_stream(stream));
 }
 
-int rs_sync(rs_ctx* c, void* stream) {
+// Waits for stream s; returns and clears its deferred per-stripe errors (bit 0: a
+// stripe with < k present, bit 1: a stripe beyond the launch's erasure bound).
+// release: also gives the stream's word back (rs_stream_release).
+static int sync_stream(rs_ctx* c, void* stream, bool release) {
   if (!c) return RS_ERR_INVALID_ARG;
   hipStream_t s = as_stream(stream);
   Engine* e = engine_for_stream(c, s);
@@ -1378,17 +1477,27 @@ int rs_sync(rs_ctx* c, void* stream) {
     }
     idx = it->second;
   }
-  uint32_t* dw = static_cast<uint32_t*>(e->d_status.p) + idx;
-  volatile uint32_t* hw = static_cast<uint32_t*>(e->h_status.p) + idx;
+  uint32_t* dw = status_dev(e, idx);
+  volatile uint32_t* hw = status_host(e, idx);
   RS_HIP(hipMemcpyAsync(const_cast<uint32_t*>(hw), dw, 4, hipMemcpyDeviceToHost, s));
   RS_HIP(hipStreamSynchronize(s));
-  if (*hw) {
+  const uint32_t word = *hw;
+  if (word) {
     RS_HIP(hipMemsetAsync(dw, 0, 4, s));
     RS_HIP(hipStreamSynchronize(s));
-    return RS_ERR_TOO_FEW_SHARDS;
   }
+  if (release) {  // the word is zero and no kernel of s holds it any more
+    std::lock_guard<std::mutex> g(e->status_mu);
+    e->status_idx.erase(s);
+    e->status_free.push_back(idx);
+  }
+  if (word & 1u) return RS_ERR_TOO_FEW_SHARDS;
+  if (word & 2u) return RS_ERR_INVALID_ARG;
   return RS_OK;
 }
+
+int rs_sync(rs_ctx* c, void* stream) { return sync_stream(c, stream, false); }
+int rs_stream_release(rs_ctx* c, void* stream) { return sync_stream(c, stream, true); }
 
 // Pins for every GPU of the process (portable) and maps into their address spaces.
 int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
@@ -1465,12 +1574,6 @@ const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_
 int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->parity_pad = enable != 0;
-  return RS_OK;
-}
-
-int rs_set_kernel_variant(rs_ctx* c, int variant) {
-  if (!c || variant < 0 || variant > 4) return RS_ERR_INVALID_ARG;
-  for (auto& e : c->engines) e->variant = variant;  // 0 = by shape
   return RS_OK;
 }
 

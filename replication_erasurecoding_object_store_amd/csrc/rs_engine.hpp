@@ -49,13 +49,15 @@ class DeviceScope {
 
 // Device-resident batch entry points on one Engine (asynchronous on s, which must
 // belong to the engine's device; the caller holds a DeviceScope for it).
-// Contracts as rs_encode_batch / rs_reconstruct_batch_out / rs_verify_batch with
-// RS_MEM_DEVICE; the pointers may also be GPU-mapped pinned host memory.
+// Contracts as rs_encode_batch / rs_reconstruct_batch_out(_devmask) / rs_verify_batch
+// with RS_MEM_DEVICE; the pointers may also be GPU-mapped pinned host memory.
+// max_missing bounds device masks (0 = m; see rs_reconstruct_batch_out_devmask).
 int engine_encode_batch(Engine* e, const uint8_t* data, size_t data_sp, uint8_t* parity, size_t parity_sp,
                         size_t pitch, size_t S, size_t N, hipStream_t s);
 int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
                                  size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
-                                 size_t n_masks, int masks_on_device, uint8_t* out, size_t out_sp, hipStream_t s);
+                                 size_t n_masks, int masks_on_device, int max_missing, uint8_t* out, size_t out_sp,
+                                 hipStream_t s);
 int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
                         size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s);
 // Device address of the plan for one pattern on this engine (cached; thread-safe):

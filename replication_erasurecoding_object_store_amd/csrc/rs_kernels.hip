@@ -201,15 +201,6 @@ __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t
                : slot_ptr(a, k, stripe, slot);
 }
 
-// Shard slot s of a stripe whose data / parity regions start at bd / bp, branch-free
-// (the host launches the pipelined kernel only when (k+m) * pitch < 2^31).
-__device__ __forceinline__ const uint8_t* slot_at(uint64_t bd, uint64_t bp, uint32_t pitch, uint32_t s, int k) {
-  const bool par = s >= static_cast<uint32_t>(k);
-  const uint64_t b = par ? bp : bd;
-  const uint32_t idx = par ? s - static_cast<uint32_t>(k) : s;
-  return reinterpret_cast<const uint8_t*>(b + idx * pitch);
-}
-
 // Slot index of the i-th set bit of a wave-uniform mask walk: s = lowest set bit.
 __device__ __forceinline__ uint32_t pop_low(uint32_t& bits) {
   const uint32_t s = static_cast<uint32_t>(__builtin_ctz(bits | 0x80000000u));
@@ -290,11 +281,19 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 
 // ---------------------------------------------------------------------------
 // Main kernel: compile-time K, plan layout M, E outputs per task (M for encode,
-// #erasures for a uniform reconstruct, the batch's max for per-stripe patterns).
+// #erasures for a uniform reconstruct, the batch's bound for per-stripe patterns).
+//
+// Uniform plans (encode, one erasure pattern for the whole batch): the input and
+// output slots are resolved once per launch, so a task's K loads issue at its top
+// with addresses from loop-invariant SGPRs.  (Round 2 loaded the plan's slot list
+// per task behind an s_waitcnt vmcnt(0) that also drained the previous task's
+// stores: config 3's uniform 4 KiB patterns fell from 72-77 % to 67-70 %.)
 //
 // Per-stripe batches sized for E > 2 outputs (device masks: E = M) split every
 // input's bytes into chunk indices once (K x 12 VGPRs) and then compute only the
 // rows the stripe misses, one row at a time (gf_row_ix), in wave-uniform branches.
+// A stripe missing more than E shards (possible with device masks under a caller's
+// max_missing bound) is skipped and flagged (status bit 1).
 // Every trip issues the same loads and stores (dropped when not live); the
 // wave-uniform branches hold VALU work only, so the compiler's vmcnt bookkeeping
 // stays exact across them.
@@ -315,6 +314,18 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     return a.present_masks[tt / bps];
   };
 
+  // uniform plan: slots once per launch
+  uint32_t uin[PER_STRIPE ? 1 : K], uout[PER_STRIPE ? 1 : E];
+  uint32_t u_nout = 0u;
+  if constexpr (!PER_STRIPE) {
+    const PlanView pv0(uniform_ptr(a.plans), K, M);
+    u_nout = wave_uniform(pv0.n_out());
+#pragma unroll
+    for (int c = 0; c < K; ++c) uin[c] = wave_uniform(pv0.in_idx(c));
+#pragma unroll
+    for (int r = 0; r < E; ++r) uout[r] = wave_uniform(static_cast<uint32_t>(r) < u_nout ? pv0.out_idx(r) : 0u);
+  }
+
   uint32_t mask = 0u;
   if (PER_STRIPE && wave < ntasks) mask = load_mask(wave);
   for (uint32_t t = wave; t < ntasks; t += nwaves) {
@@ -328,6 +339,11 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       uint32_t pid = as_const<uint32_t>(a.lut)[missing];
       bad |= (pid == kPlanInvalid) ? 1u : 0u;
       pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
+      if constexpr (E < M) {  // more erasures than this launch's bound: skip, flag
+        const bool over = static_cast<uint32_t>(__builtin_popcount(missing)) > static_cast<uint32_t>(E);
+        bad |= over ? 2u : 0u;
+        pid = over ? 0u : pid;
+      }
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     }
     if constexpr (K * ((PER_STRIPE && E > 2) ? 2 : E) * 5 > 48) {
@@ -344,16 +360,8 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
 
     u32x4 x[K];
-    if (!PER_STRIPE && a.data_inputs) {
-      // the plan reads data shards 0..K-1 (encode): addresses need no plan load,
-      // so the K loads issue at the top of the task
-      const uint8_t* db = a.data + static_cast<uint64_t>(stripe) * a.data_sp;
 #pragma unroll
-      for (int c = 0; c < K; ++c) x[c] = load16(db + static_cast<uint64_t>(c) * a.shard_pitch + off);
-    } else {
-#pragma unroll
-      for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, pv.in_idx(c)) + off);
-    }
+    for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, PER_STRIPE ? pv.in_idx(c) : uin[c]) + off);
 
     u32x4 y[E];
     if constexpr (PER_STRIPE && E > 2) {
@@ -378,324 +386,20 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     } else {
       gf_rows<K, M, 0, E>(plan, x, y);
     }
-    const uint32_t n_out = pv.n_out();
+    const uint32_t n_out = PER_STRIPE ? pv.n_out() : u_nout;
 #pragma unroll
     for (int r = 0; r < E; ++r)
-      store16_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, full && static_cast<uint32_t>(r) < n_out, y[r]);
+      store16_or_drop(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                      full && static_cast<uint32_t>(r) < n_out, y[r]);
     if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
       const bool part = col == a.full_cols;
 #pragma unroll
       for (int r = 0; r < E; ++r)
-        store_part_or_drop(out_ptr(a, K, stripe, r, pv.out_idx(r)), off, part && static_cast<uint32_t>(r) < n_out,
-                           y[r], nb);
+        store_part_or_drop(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                           part && static_cast<uint32_t>(r) < n_out, y[r], nb);
     }
   }
-  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
-}
-
-// ---------------------------------------------------------------------------
-// Pipelined kernel: one 256-thread workgroup per CU = one wave per SIMD, so each
-// wave has the whole 512-VGPR file and the chip has exactly 1024 streams in flight
-// (the HBM pattern probes run fastest with few, deep streams:
-// profiles/r02_pattern_probe_gf_compute.log "D+gf pipelined bpc=1").
-//
-// A wave owns D task slots (register sets).  Slot j's K input loads for its next
-// task are issued right after its current task is stored, so while the wave
-// computes one task the loads of the other D-1 are in flight; every loop trip
-// issues the same vector-memory sequence (no branch around a load or a store), so
-// the compiler's s_waitcnt vmcnt(N) leaves the other slots' loads outstanding.
-//
-// Inputs / outputs come straight from the stripe's present mask (first K present
-// shards in index order / every missing one -- exactly how the plans are built), so
-// a task's loads depend on its mask only; the plan (tables) is looked up at issue
-// time and needed one slot later.  Tables:
-//   uniform plan  : all E*K*5 table dwords loaded once into VGPRs (v_perm reads them
-//                   directly, no scalar loads in the loop);
-//   per stripe    : one input's E*5 dwords per contiguous scalar load, the next
-//                   input's issued after the current one has landed and before it is
-//                   used (one input of compute hides the scalar-cache latency);
-//                   stripes missing <= 2 shards compute 2 rows when E > 2.
-template <int K, int NR, int RT>
-__device__ __forceinline__ void gf_rows_vtab(const uint32_t (&tab)[RT][K][5], const u32x4 (&x)[K],
-                                             u32x4 (&y)[NR]) {
-  u32x4 pend[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    Idx3 ix[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const uint32_t* q = tab[r][c];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t prod = lookup3(ix[d], q[0], q[1], q[2], q[3], q[4]);
-        if (c & 1)
-          y[r][d] = xor3(y[r][d], pend[r][d], prod);
-        else if (c == K - 1)
-          y[r][d] ^= prod;
-        else
-          pend[r][d] = prod;
-      }
-    }
-  }
-}
-
-template <int K, int M, int NR>
-__device__ __forceinline__ void gf_rows_stab(const uint8_t* plan, const u32x4 (&x)[K], u32x4 (&y)[NR]) {
-  u32x4 pend[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
-  auto tabs_of = [&](int c, uint32_t (&t)[NR * 5]) {
-    const uint8_t* p = plan;
-    asm volatile("" : "+s"(p));  // per input: never merged with / hoisted above other inputs' loads
-    const RS_CONST uint32_t* q = as_const<uint32_t>(p + plan_tab_offset(K, M)) + c * M * 5;
-#pragma unroll
-    for (int i = 0; i < NR * 5; ++i) t[i] = q[i];
-  };
-  uint32_t cur[NR * 5], nxt[NR * 5];
-  tabs_of(0, cur);
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    // wait for this input's tables (lgkmcnt(0): scalar loads return out of order)
-    // BEFORE the next input's loads are issued, so those stay in flight meanwhile
-#pragma unroll
-    for (int i = 0; i < NR * 5; ++i) asm volatile("" ::"s"(cur[i]));
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < K) tabs_of(c + 1, nxt);
-    __builtin_amdgcn_sched_barrier(0);
-    Idx3 ix[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const uint32_t* q = cur + r * 5;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t prod = lookup3(ix[d], q[0], q[1], q[2], q[3], q[4]);
-        if (c & 1)
-          y[r][d] = xor3(y[r][d], pend[r][d], prod);
-        else if (c == K - 1)
-          y[r][d] ^= prod;
-        else
-          pend[r][d] = prod;
-      }
-    }
-    // pin this input's products here (between its table wait and the next one's):
-    // otherwise instruction selection sinks all lookups to the stores and every
-    // input's tables are live in SGPRs at once
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (c & 1 || c == K - 1)
-        asm volatile("" : "+v"(y[r]));
-      else
-        asm volatile("" : "+v"(pend[r]));
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < NR * 5; ++i) cur[i] = nxt[i];
-  }
-}
-
-template <int K, int M, int E, bool PER_STRIPE, int D>
-__global__ __launch_bounds__(256, 1) void pipe_kernel(const KernelArgs a) {
-  static_assert(D >= 1 && D <= 4, "1..4 task slots");
-  // uniform plans with few table dwords keep them in VGPRs for the whole launch
-  constexpr bool kVTab = !PER_STRIPE && E * K * 5 <= 100;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_index();
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t bps = a.blocks_per_stripe;  // the partial last column included
-  const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
-  if (wave >= ntasks) return;
-  const uint32_t cols = (a.shard_len + 15u) >> 4;
-  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
-  const uint32_t mine = (ntasks - 1u - wave) / nwaves + 1u;  // tasks of this wave
-  const uint32_t last_t = wave + (mine - 1u) * nwaves;       // where dead slots read
-  const uint32_t last_s = last_t / bps, last_b = last_t - last_s * bps;
-  // task t -> (stripe, blk); slots advance by D*nwaves tasks per round
-  const uint32_t step = static_cast<uint32_t>(D) * nwaves;
-  const uint32_t step_s = step / bps, step_b = step - step_s * bps;
-  const uint32_t full = a.full_mask;
-  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
-
-  // uniform plan: slots (and tables) once per launch
-  uint32_t u_present = 0u, u_nout = 0u, u_out[E];
-  uint32_t vt[kVTab ? E : 1][K][5];
-  const uint8_t* u_plan = uniform_ptr(a.plans);
-  if constexpr (!PER_STRIPE) {
-    const PlanView pv(u_plan, K, M);
-    u_present = pv.present();
-    u_nout = pv.n_out();
-#pragma unroll
-    for (int r = 0; r < E; ++r) u_out[r] = pv.out_idx(r);
-    if constexpr (kVTab) {
-#pragma unroll
-      for (int r = 0; r < E; ++r)
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-#pragma unroll
-          for (int i = 0; i < 5; ++i) {
-            vt[r][c][i] = pv.quad(r, c)[i];
-            asm volatile("" : "+v"(vt[r][c][i]));  // keep in VGPRs (v_perm operands)
-          }
-    }
-  }
-
-  u32x4 xs[D][K];
-  uint32_t st_s[D], st_b[D], st_present[D], st_mask[D];
-  const uint8_t* st_plan[D];
-  uint32_t bad = 0u;
-
-  auto load_mask = [&](uint32_t stripe) -> uint32_t {
-    return a.present_masks[stripe < a.n_stripes ? stripe : last_s];  // one request per wave
-  };
-  auto advance = [&](uint32_t& st, uint32_t& bl) {
-    bl += step_b;
-    st += step_s;
-    if (bl >= bps) {
-      bl -= bps;
-      ++st;
-    }
-  };
-
-  // Issue slot j's loads for its task (st_s/st_b; a stripe past the end is a dead
-  // slot: it re-reads this wave's last task and stores nothing).
-  auto issue = [&](auto jtag) {
-    constexpr int j = decltype(jtag)::value;
-    const bool live = st_s[j] < a.n_stripes;
-    const uint32_t stripe = live ? st_s[j] : last_s, blk = live ? st_b[j] : last_b;
-    uint32_t present;
-    if constexpr (PER_STRIPE) {
-      const uint32_t pm = wave_uniform(st_mask[j]) & full;
-      {  // the mask this slot needs next round
-        uint32_t ns = st_s[j], nbk = st_b[j];
-        advance(ns, nbk);
-        st_mask[j] = load_mask(ns);
-      }
-      const bool valid = static_cast<uint32_t>(__builtin_popcount(pm)) >= static_cast<uint32_t>(K);
-      present = valid ? pm : ((1u << K) - 1u);  // invalid: read the data slots, store nothing
-      const uint32_t missing = valid ? (~pm & full) : 0u;
-      uint32_t pid = as_const<uint32_t>(a.lut)[missing];
-      pid = (pid == kPlanInvalid) ? 0u : pid;
-      st_plan[j] = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
-      st_present[j] = valid ? pm : 0xFFFFFFFFu;  // all-ones = invalid marker
-    } else {
-      present = u_present;
-    }
-    const uint32_t col = blk * 64u + lane;
-    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
-    const uint64_t bd = reinterpret_cast<uint64_t>(a.data) + static_cast<uint64_t>(stripe) * a.data_sp;
-    const uint64_t bp = reinterpret_cast<uint64_t>(a.parity) + static_cast<uint64_t>(stripe) * a.parity_sp;
-    uint32_t bits = present;
-#pragma unroll
-    for (int c = 0; c < K; ++c) xs[j][c] = load16(slot_at(bd, bp, pitch, pop_low(bits), K) + off);
-  };
-
-  auto run = [&](auto jtag) {
-    constexpr int j = decltype(jtag)::value;
-    const bool live = st_s[j] < a.n_stripes;
-    const uint32_t stripe = live ? st_s[j] : last_s, blk = live ? st_b[j] : last_b;
-    u32x4 y[E];
-    uint32_t n_out, obits = 0u;
-    if constexpr (PER_STRIPE) {
-      const uint32_t pm = st_present[j];
-      const bool valid = pm != 0xFFFFFFFFu;
-      bad |= (!valid && live) ? 1u : 0u;
-      obits = valid ? (~pm & full) : 0u;
-      n_out = static_cast<uint32_t>(__builtin_popcount(obits));
-      if constexpr (E > 2) {
-        if (n_out <= 2u) {
-          u32x4 y2[2];
-          gf_rows_stab<K, M, 2>(st_plan[j], xs[j], y2);
-#pragma unroll
-          for (int r = 0; r < E; ++r) y[r] = y2[r < 2 ? r : 0];  // rows >= 2 dropped
-        } else {
-          gf_rows_stab<K, M, E>(st_plan[j], xs[j], y);
-        }
-      } else {
-        gf_rows_stab<K, M, E>(st_plan[j], xs[j], y);
-      }
-    } else {
-      n_out = u_nout;
-      if constexpr (kVTab)
-        gf_rows_vtab<K, E, E>(vt, xs[j], y);
-      else
-        gf_rows_stab<K, M, E>(u_plan, xs[j], y);
-    }
-    if (!live) n_out = 0u;
-    const uint32_t col = blk * 64u + lane;
-    const bool fullc = col < a.full_cols;
-    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
-    // output r: out of place at out + stripe*out_sp + r*pitch, else its shard slot
-    uint8_t* obase[E];
-    {
-      const uint64_t bd = reinterpret_cast<uint64_t>(a.data) + static_cast<uint64_t>(stripe) * a.data_sp;
-      const uint64_t bp = reinterpret_cast<uint64_t>(a.parity) + static_cast<uint64_t>(stripe) * a.parity_sp;
-      const uint64_t bo = reinterpret_cast<uint64_t>(a.out) + static_cast<uint64_t>(stripe) * a.out_sp;
-#pragma unroll
-      for (int r = 0; r < E; ++r) {
-        uint32_t slot;
-        if constexpr (PER_STRIPE)
-          slot = min(pop_low(obits), static_cast<uint32_t>(K + M - 1));
-        else
-          slot = u_out[r];
-        obase[r] = a.out ? reinterpret_cast<uint8_t*>(bo + static_cast<uint32_t>(r) * pitch)
-                         : const_cast<uint8_t*>(slot_at(bd, bp, pitch, slot, K));
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-      store16_or_drop(obase[r], off, fullc && static_cast<uint32_t>(r) < n_out, y[r]);
-    if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
-      const bool part = col == a.full_cols;
-#pragma unroll
-      for (int r = 0; r < E; ++r)
-        store_part_or_drop(obase[r], off, part && static_cast<uint32_t>(r) < n_out, y[r], nb);
-    }
-  };
-
-  // prologue: slot j starts at task wave + j*nwaves
-  {
-    uint32_t t = wave;
-#pragma unroll
-    for (int j = 0; j < D; ++j, t += nwaves) {
-      st_s[j] = t / bps;  // >= n_stripes when past the end (dead)
-      st_b[j] = t - st_s[j] * bps;
-      if (t >= ntasks) st_s[j] = a.n_stripes;
-      if constexpr (PER_STRIPE) st_mask[j] = load_mask(st_s[j]);
-    }
-  }
-  issue(std::integral_constant<int, 0>{});
-  if constexpr (D > 1) issue(std::integral_constant<int, 1>{});
-  if constexpr (D > 2) issue(std::integral_constant<int, 2>{});
-  if constexpr (D > 3) issue(std::integral_constant<int, 3>{});
-
-  auto turn = [&](auto jtag) {  // compute + store slot j, then load its next task
-    constexpr int j = decltype(jtag)::value;
-    run(jtag);
-    advance(st_s[j], st_b[j]);
-    if (st_s[j] > a.n_stripes) st_s[j] = a.n_stripes;  // keep dead slots dead (no wrap)
-    issue(jtag);
-  };
-  const uint32_t rounds = (mine + D - 1u) / D;
-  for (uint32_t rr = 1; rr < rounds; ++rr) {
-    turn(std::integral_constant<int, 0>{});
-    if constexpr (D > 1) turn(std::integral_constant<int, 1>{});
-    if constexpr (D > 2) turn(std::integral_constant<int, 2>{});
-    if constexpr (D > 3) turn(std::integral_constant<int, 3>{});
-  }
-  // last round: no further loads
-  run(std::integral_constant<int, 0>{});
-  if constexpr (D > 1)
-    if (st_s[1] < a.n_stripes) run(std::integral_constant<int, 1>{});
-  if constexpr (D > 2)
-    if (st_s[2] < a.n_stripes) run(std::integral_constant<int, 2>{});
-  if constexpr (D > 3)
-    if (st_s[3] < a.n_stripes) run(std::integral_constant<int, 3>{});
-  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, 1u);
+  if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -732,6 +436,10 @@ __global__ __launch_bounds__(256) void apply_kernel_generic(const KernelArgs a) 
     }
     const PlanView pv(plan, K, M);
     const int n_out = static_cast<int>(pv.n_out());
+    if (PER_STRIPE && static_cast<uint32_t>(n_out) > a.max_out) {  // beyond the launch's erasure bound
+      if (lane == 0 && blk == 0) atomicOr(a.status, 2u);
+      continue;
+    }
     const uint32_t off = (blk * 64u + lane) * 16u;
     if (n_out == 0 || off >= a.shard_len) continue;
     const uint32_t tail = a.shard_len - off;
@@ -993,6 +701,47 @@ __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t*
   return y;
 }
 
+// Rows 0..NR-1 input-outer (as gf_rows) with table dwords chosen per lane between
+// two plans: no chunk-index array (K x 12 VGPRs) is kept, each input is split and
+// used once.  For flat per-stripe launches bounded to E <= 2 erasures.
+template <int K, int M, int NR>
+__device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* planB, bool inB, const u32x4 (&x)[K],
+                                         u32x4 (&y)[NR]) {
+  u32x4 pend[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
+  const uint32_t selB = inB ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    Idx3 ix[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
+    const uint8_t* pa = planA;
+    const uint8_t* pb = planB;
+    asm volatile("" : "+s"(pa));
+    asm volatile("" : "+s"(pb));
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(r, c);
+      const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(r, c);
+      uint32_t q[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) q[i] = __builtin_amdgcn_bitop3_b32(selB, tb[i], ta[i], 0xCA);  // selB ? tb : ta
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t prod = lookup3(ix[d], q[0], q[1], q[2], q[3], q[4]);
+        if (c & 1)
+          y[r][d] = xor3(y[r][d], pend[r][d], prod);
+        else if (c == K - 1)
+          y[r][d] ^= prod;
+        else
+          pend[r][d] = prod;
+      }
+    }
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int K, int M, int E>
 __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -1018,8 +767,14 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
     uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
     bad |= (pid == kPlanInvalid) ? 1u : 0u;
-    m = (pid == kPlanInvalid) ? full : present;
-    pid = (pid == kPlanInvalid) ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
+    bool skip = pid == kPlanInvalid;
+    if constexpr (E < M) {  // more erasures than this launch's bound: skip, flag
+      const bool over = static_cast<uint32_t>(__builtin_popcount((~present) & full)) > static_cast<uint32_t>(E);
+      bad |= over ? 2u : 0u;
+      skip = skip || over;
+    }
+    m = skip ? full : present;
+    pid = skip ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
     const uint8_t* p = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
     nout = PlanView(p, K, M).n_out();
     return p;
@@ -1067,13 +822,21 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
         x[c] = xd | xp;
       }
     }
+    const uint32_t nmax = nA > nB ? nA : nB;
+    u32x4 y[E];
+    if constexpr (E <= 2) {
+      // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
+      // launch computes a row it does not store): x[K] only, no index array
+      if (!diff)
+        gf_rows<K, M, 0, E>(planA, x, y);
+      else
+        gf_rows2<K, M, E>(planA, planB, inB, x, y);
+    } else {
     Idx3 ix[K][4];
 #pragma unroll
     for (int c = 0; c < K; ++c)
 #pragma unroll
       for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
-    const uint32_t nmax = nA > nB ? nA : nB;
-    u32x4 y[E];
     if (!diff) {
       y[0] = gf_row_ix<K, M>(planA, ix, 0);
 #pragma unroll
@@ -1088,6 +851,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
         y[r] = y[0];
         if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix2<K, M>(planA, planB, inB, ix, r);
       }
+    }
     }
     // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
     const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
@@ -1111,7 +875,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       ++s0;
     }
   }
-  if (bad && lane == 0u) atomicOr(a.status, 1u);
+  if (bad && lane == 0u) atomicOr(a.status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -1351,26 +1115,12 @@ static const void* spec_fn(bool per_stripe) {
                     : reinterpret_cast<const void*>(&apply_kernel<K, M, E, false>);
 }
 
-// Specialised kernels: (K, M, E) with E <= M.  variant: 0/1 grid-stride
-// apply_kernel, 2/3 pipe_kernel with 2/3 task slots.
-template <int K, int M, int E>
-static const void* pipe_fn(bool per_stripe, int variant) {
-  if (variant == 3)
-    return per_stripe ? reinterpret_cast<const void*>(&pipe_kernel<K, M, E, true, 3>)
-                      : reinterpret_cast<const void*>(&pipe_kernel<K, M, E, false, 3>);
-  return per_stripe ? reinterpret_cast<const void*>(&pipe_kernel<K, M, E, true, 2>)
-                    : reinterpret_cast<const void*>(&pipe_kernel<K, M, E, false, 2>);
-}
-
-static const void* pick_spec(int k, int m, int e, bool per_stripe, int variant, const char** name) {
-#define RS_SPEC(KK, MM, EE)                                 \
-  if (k == KK && m == MM && e == EE) {                      \
-    if (variant == 2 || variant == 3) {                     \
-      *name = variant == 3 ? "pipe_kernel<" #KK "," #MM "," #EE ",3>" : "pipe_kernel<" #KK "," #MM "," #EE ",2>"; \
-      return pipe_fn<KK, MM, EE>(per_stripe, variant);      \
-    }                                                       \
-    *name = "apply_kernel<" #KK "," #MM "," #EE ">";        \
-    return spec_fn<KK, MM, EE>(per_stripe);                 \
+// Specialised grid-stride kernels: (K, M, E) with E <= M.
+static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** name) {
+#define RS_SPEC(KK, MM, EE)                                                                             \
+  if (k == KK && m == MM && e == EE) {                                                                  \
+    *name = per_stripe ? "apply_kernel<" #KK "," #MM "," #EE ",true>" : "apply_kernel<" #KK "," #MM "," #EE ",false>"; \
+    return spec_fn<KK, MM, EE>(per_stripe);                                                             \
   }
   RS_SPEC(4, 2, 1) RS_SPEC(4, 2, 2)
   RS_SPEC(8, 4, 1) RS_SPEC(8, 4, 2) RS_SPEC(8, 4, 3) RS_SPEC(8, 4, 4)
@@ -1407,6 +1157,23 @@ static const void* pick_bitsliced(int k, int m, const char** name) {
   return nullptr;
 }
 
+// Flat per-stripe reconstruct for (K, M) and the launch's erasure bound E: E = M,
+// or the bound a caller (host masks: their maximum; device masks: max_missing)
+// gives -- E <= 2 runs input-outer with x[K] as the only per-input state.
+static const void* pick_flat_ps(int k, int m, int e, const char** name) {
+#define RS_PSFLAT(KK, MM, EE)                                                 \
+  if (k == KK && m == MM && e == EE) {                                        \
+    *name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                  \
+    return reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>); \
+  }
+  RS_PSFLAT(4, 2, 1) RS_PSFLAT(4, 2, 2)
+  RS_PSFLAT(8, 4, 1) RS_PSFLAT(8, 4, 2) RS_PSFLAT(8, 4, 4)
+  RS_PSFLAT(10, 4, 1) RS_PSFLAT(10, 4, 2) RS_PSFLAT(10, 4, 4)
+  RS_PSFLAT(6, 3, 1) RS_PSFLAT(6, 3, 2) RS_PSFLAT(6, 3, 3)
+#undef RS_PSFLAT
+  return nullptr;
+}
+
 // Grid for `waves` wave-tasks: 4 waves per workgroup, at most blocks_per_cu
 // workgroups per CU (the kernels grid-stride over the rest).
 static dim3 grid_for(uint64_t waves, uint32_t blocks_per_cu, uint32_t cu_count) {
@@ -1419,18 +1186,15 @@ static dim3 grid_for(uint64_t waves, uint32_t blocks_per_cu, uint32_t cu_count) 
 // One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
 // the dropped-store descriptors cover 2 GiB from the shard base).
 static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
-                                 uint32_t cu_count, hipStream_t s, bool force_generic, int variant) {
+                                 uint32_t cu_count, hipStream_t s) {
   void* args[] = {const_cast<KernelArgs*>(&a)};
   const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
   const char* name = nullptr;
-  if (a.stripe_plans) force_generic = true;  // only the generic kernel reads per-stripe plan addresses
-  // pipe_kernel addresses slots with 32-bit offsets: (k+m) * pitch < 2 GiB
-  if ((variant == 2 || variant == 3) && static_cast<uint64_t>(a.k + a.m) * a.shard_pitch >= (1ull << 31))
-    variant = 4;
-  if (a.encode_net && !per_stripe && !force_generic && e == a.m && variant < 2) {  // 4: lookup only
+  const bool generic = a.stripe_plans != nullptr;  // only the generic kernel reads per-stripe plan addresses
+  const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
+  if (a.encode_net && !per_stripe && !generic && e == a.m) {
     // flat 128-column tasks straddle at most two stripes (cols >= 128) and address
     // with 32-bit offsets off one stripe base per region
-    const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
     const bool flat_ok = cols >= 128u && a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31);
     const void* fn = flat_ok ? pick_bitsliced(a.k, a.m, &name) : nullptr;
     if (fn) {
@@ -1441,37 +1205,20 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       return name;
     }
   }
-#ifndef RS_FLAT_PS
-#define RS_FLAT_PS 1
-#endif
-  if (RS_FLAT_PS && per_stripe && !force_generic && a.out && variant < 2 && (e == a.m || e == 2) &&
-      cols >= 64u && cols % 64u != 0u) {
+  if (per_stripe && !generic && a.out && cols >= 64u && cols % 64u != 0u && a.data_sp + span < (1ull << 31) &&
+      a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
-    const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
-    if (a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
-      const void* ff = nullptr;
-#define RS_PSFLAT(KK, MM, EE)                                                    \
-      if (!ff && a.k == KK && a.m == MM && e == EE) {                            \
-        ff = reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>);   \
-        name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                  \
-      }
-      // E = M (device masks, mixed encode + reconstruct) and E = 2 (host masks of
-      // 1-2 erasures, e.g. healer batches: +2 points, profiles/r02c_ab_flat_ps_e2.log)
-      RS_PSFLAT(4, 2, 2) RS_PSFLAT(8, 4, 4) RS_PSFLAT(10, 4, 4) RS_PSFLAT(6, 3, 3)
-      RS_PSFLAT(8, 4, 2) RS_PSFLAT(10, 4, 2) RS_PSFLAT(6, 3, 2)
-#undef RS_PSFLAT
-      if (ff) {
-        const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
-        if (waves == 0) return name;
-        if (hipLaunchKernel(ff, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
-          return nullptr;
-        return name;
-      }
+    if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
+      const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
+      if (waves == 0) return name;
+      if (hipLaunchKernel(ff, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+        return nullptr;
+      return name;
     }
   }
-  const void* fn = force_generic ? nullptr : pick_spec(a.k, a.m, e, per_stripe, variant, &name);
+  const void* fn = generic ? nullptr : pick_spec(a.k, a.m, e, per_stripe, &name);
   if (!fn) {
-    name = "apply_kernel_generic";
+    name = per_stripe ? "apply_kernel_generic<true>" : "apply_kernel_generic<false>";
     fn = per_stripe ? reinterpret_cast<const void*>(&apply_kernel_generic<true>)
                     : reinterpret_cast<const void*>(&apply_kernel_generic<false>);
   }
@@ -1482,10 +1229,11 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   return name;
 }
 
-const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
-                         hipStream_t s, bool force_generic, int variant) {
-  if (a.shard_len <= kColumnWindow)
-    return launch_window(a, e, per_stripe, blocks_per_cu, cu_count, s, force_generic, variant);
+const char* launch_apply(const KernelArgs& args, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
+                         hipStream_t s) {
+  KernelArgs a = args;
+  a.max_out = static_cast<uint32_t>(e);
+  if (a.shard_len <= kColumnWindow) return launch_window(a, e, per_stripe, blocks_per_cu, cu_count, s);
   // Shards of 1 GiB or more (one huge Encode of an object of several GiB): the
   // codec is column-wise, so columns [x, x + W) of every shard are an independent
   // batch whose slots all start x bytes later.  Windows run in order on s.
@@ -1499,14 +1247,13 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
     w.shard_len = static_cast<uint32_t>(len);
     w.full_cols = w.shard_len / 16u;
     w.blocks_per_stripe = ((w.shard_len + 15u) / 16u + 63u) / 64u;
-    name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s, force_generic, variant);
+    name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s);
     if (!name) return nullptr;
   }
   return name;
 }
 
-const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s,
-                          bool force_generic) {
+const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s) {
   const void* fn = nullptr;
   const char* name = "verify_kernel_generic";
 #define RS_VSPEC(KK, MM)                                                  \
@@ -1514,9 +1261,7 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
     fn = reinterpret_cast<const void*>(&verify_kernel<KK, MM>);           \
     name = "verify_kernel<" #KK "," #MM ">";                              \
   }
-  if (!force_generic) {
-    RS_VSPEC(4, 2) RS_VSPEC(8, 4) RS_VSPEC(10, 4) RS_VSPEC(6, 3)
-  }
+  RS_VSPEC(4, 2) RS_VSPEC(8, 4) RS_VSPEC(10, 4) RS_VSPEC(6, 3)
 #undef RS_VSPEC
   if (!fn) fn = reinterpret_cast<const void*>(&verify_kernel_generic);
   if (hipMemsetAsync(a.bad, 0, static_cast<size_t>(a.n_stripes) * 4u, s) != hipSuccess) return nullptr;
@@ -1524,7 +1269,7 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
   // flat 64-column tasks when a stripe's columns do not fill whole 64-column blocks
   const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
   const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
-  if (!force_generic && cols >= 64u && cols % 64u != 0u && a.data_sp + span < (1ull << 31) &&
+  if (cols >= 64u && cols % 64u != 0u && a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31)) {
     const void* ff = nullptr;
 #define RS_VFLAT(KK, MM) \

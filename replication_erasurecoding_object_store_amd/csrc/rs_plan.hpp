@@ -88,7 +88,9 @@ struct KernelArgs {
   const uint8_t* plans;            // uniform plan, or plan array (PER_STRIPE)
   const uint32_t* present_masks;   // PER_STRIPE: bit s = shard s present
   const uint32_t* lut;             // PER_STRIPE: missing mask -> plan index
-  uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards
+  uint32_t* status;                // PER_STRIPE: bit 0 set if a stripe had < K shards, bit 1 if a
+                                   //   stripe missed more than max_out shards
+  uint32_t max_out;                // PER_STRIPE: the launch's erasure bound E (set by launch_apply)
   uint8_t* out;                    // null: outputs in place (slot addresses); else the
   uint64_t out_sp;                 //   r-th output of stripe i at out + i*out_sp + r*shard_pitch
   uint32_t* bad;                   // verify: per-stripe bit r set = parity r mismatches
@@ -105,18 +107,16 @@ struct KernelArgs {
 const uint8_t* bitsliced_encode_rows(int k, int m);
 
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
-// e = outputs per stripe to compute (<= m).  Returns the main kernel's name, or
-// nullptr if the launch failed.  Any shard_len up to 0xFFFFFFF0 (column windows).
-// variant: 0/1 grid-stride kernels (apply / bitsliced encode), 2/3 pipelined kernel
-// with 2/3 task slots per wave (specialised shapes only), 4 grid-stride lookup
-// kernels only (no bitsliced encode).
+// e = outputs per stripe to compute (<= m): for per-stripe plans the launch's erasure
+// bound (stripes missing more are skipped and flagged, status bit 1).  Returns the
+// main kernel's name, or nullptr if the launch failed.  Any shard_len up to
+// 0xFFFFFFF0 (column windows).
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
-                         uint32_t cu_count, hipStream_t s, bool force_generic, int variant);
+                         uint32_t cu_count, hipStream_t s);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.
 // a.bad must be zeroed first (launch_verify does it on s).
-const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s,
-                          bool force_generic);
+const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
 
 }  // namespace rs

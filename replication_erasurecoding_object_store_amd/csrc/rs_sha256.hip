@@ -92,11 +92,32 @@ __device__ __forceinline__ uint32_t load_word(const uint8_t* p, uint64_t off, ui
   return v;
 }
 
+// Message byte `off` of a chunked message (see Sha256Args).
+__device__ __forceinline__ const uint8_t* chunk_addr(const uint8_t* p, uint64_t off, uint64_t chunk, uint64_t pitch) {
+  const uint64_t c = off / chunk;
+  return p + c * pitch + (off - c * chunk);
+}
+
+// Big-endian word at message byte offset `off` of a chunked message (bytes past len:
+// the 0x80 terminator, then zeros).
+__device__ __forceinline__ uint32_t load_word_chunked(const uint8_t* p, uint64_t off, uint64_t len, uint64_t chunk,
+                                                      uint64_t pitch) {
+  uint32_t v = 0;
+  for (uint32_t q = 0; q < 4; ++q) {
+    const uint64_t o = off + q;
+    const uint32_t byte = o < len ? *chunk_addr(p, o, chunk, pitch) : (o == len ? 0x80u : 0u);
+    v |= byte << (24 - 8 * q);
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(64) void sha256_kernel(Sha256Args a) {
   const uint32_t i = blockIdx.x * 64u + threadIdx.x;
   if (i >= a.n) return;
   const uint64_t len = a.lens ? a.lens[i] : a.len;
+  if (len == kSha256Skip) return;
   const uint8_t* p = a.base + (a.offsets ? a.offsets[i] : static_cast<uint64_t>(i) * a.stride);
+  const bool chunked = a.chunk != 0 && len > a.chunk;  // a message inside its first chunk is contiguous
   const bool aligned = (reinterpret_cast<uintptr_t>(p) & 3u) == 0;
   const uint64_t nblocks = (len + 8u) / 64u + 1u;  // message + 0x80 + 64-bit length, padded
   State s = {{0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu,
@@ -104,15 +125,24 @@ __global__ __launch_bounds__(64) void sha256_kernel(Sha256Args a) {
   const uint64_t full = len / 64u;  // blocks made of message bytes only
   for (uint64_t blk = 0; blk < full; ++blk) {
     uint32_t w[16];
-    const uint8_t* q = p + blk * 64u;
-    if (aligned) {
+    const uint64_t o0 = blk * 64u;
+    const uint8_t* q = p + o0;
+    bool fast = aligned;
+    if (chunked) {  // contiguous only if the block lies in one chunk
+      const uint64_t c0 = o0 / a.chunk;
+      q = p + c0 * a.chunk_pitch + (o0 - c0 * a.chunk);
+      fast = (o0 + 63u) / a.chunk == c0 && (reinterpret_cast<uintptr_t>(q) & 3u) == 0;
+    }
+    if (fast) {
 #pragma unroll
       for (int t = 0; t < 16; ++t) w[t] = __builtin_bswap32(reinterpret_cast<const uint32_t*>(q)[t]);
-    } else {
+    } else if (!chunked) {
 #pragma unroll
       for (int t = 0; t < 16; ++t)
         w[t] = static_cast<uint32_t>(q[4 * t]) << 24 | static_cast<uint32_t>(q[4 * t + 1]) << 16 |
                static_cast<uint32_t>(q[4 * t + 2]) << 8 | q[4 * t + 3];
+    } else {
+      for (int t = 0; t < 16; ++t) w[t] = load_word_chunked(p, o0 + 4u * t, len, a.chunk, a.chunk_pitch);
     }
     compress(s, w);
   }
@@ -121,7 +151,9 @@ __global__ __launch_bounds__(64) void sha256_kernel(Sha256Args a) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
       const uint64_t off = blk * 64u + 4u * t;
-      w[t] = off <= len ? load_word(p, off, len, aligned) : 0u;
+      w[t] = off > len ? 0u
+             : chunked ? load_word_chunked(p, off, len, a.chunk, a.chunk_pitch)
+                       : load_word(p, off, len, aligned);
     }
     if (blk + 1 == nblocks) {
       const uint64_t bits = len * 8u;

@@ -30,6 +30,19 @@ constexpr int M = 2;  // internal/config/config.go:22
 using Shard = std::vector<uint8_t>;
 using Shards = std::vector<Shard>;
 
+// A Go []byte: len bytes at p with capacity cap, possibly aliasing a caller's
+// buffer (what klauspost's Split hands back); `owner` keeps storage the codec had
+// to allocate alive.  len == 0 is Go's nil / empty shard.
+struct Slice {
+  uint8_t* p = nullptr;
+  size_t len = 0, cap = 0;
+  std::shared_ptr<std::vector<uint8_t>> owner;
+  uint8_t* data() const { return p; }
+  size_t size() const { return len; }
+  bool empty() const { return len == 0; }
+};
+using Slices = std::vector<Slice>;
+
 // Go-style error value: code 0 is nil.
 struct Error {
   int code = RS_OK;
@@ -101,6 +114,73 @@ class Service final : public IEcDriver {
       }
     }
     return Error{};
+  }
+
+  // [upstream reedsolomon.go Split] with Go's aliasing, on a byte vector whose
+  // size() is len(data) and capacity() is cap(data): spare capacity is used first
+  // (data is resized -- never reallocated -- to min(capacity, (K+M)*perShard) and
+  // zero-filled past its old size), so with enough capacity every shard, parity
+  // included, is a view into `data`; only shards that do not fit get fresh zeroed
+  // storage, the first of them holding the payload's tail.  `data` must outlive
+  // the slices and not be reallocated while they are in use.
+  Error Split(std::vector<uint8_t>& data, Slices* out) {
+    if (data.empty()) return Error{RS_ERR_SHORT_DATA};
+    const size_t total = static_cast<size_t>(k_ + m_);
+    const size_t data_len = data.size();
+    const size_t per = rs_shard_size(ctx_, data_len);
+    const size_t need = total * per;
+    if (data.capacity() > data.size()) data.resize(std::min(data.capacity(), need), 0);  // within capacity
+    out->assign(total, Slice{});
+    size_t i = 0;
+    for (; i < total && (i + 1) * per <= data.size(); ++i) out->at(i) = Slice{data.data() + i * per, per, per, nullptr};
+    if (i < total) {
+      auto pad = std::make_shared<std::vector<uint8_t>>((total - i) * per, 0);
+      if (data_len > i * per)  // the payload's tail did not fill a whole shard
+        std::copy(data.begin() + static_cast<std::ptrdiff_t>(i * per),
+                  data.begin() + static_cast<std::ptrdiff_t>(data_len), pad->begin());
+      for (size_t j = 0; i + j < total; ++j) out->at(i + j) = Slice{pad->data() + j * per, per, per, pad};
+    }
+    return Error{};
+  }
+
+  // Encode / Reconstruct on Go-style slices (the shards Split(vector&) returns).
+  Error Encode(Slices& shards) {
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      p[i] = shards[i].p;
+      n[i] = shards[i].len;
+    }
+    return Error{co_ ? rs_co_encode(co_, p.data(), n.data()) : rs_encode(ctx_, p.data(), n.data())};
+  }
+  // Fills every empty entry (a slice with cap >= the shard size is reused, as
+  // klauspost reuses capacity; others get fresh storage).
+  Error Reconstruct(Slices& shards) {
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    size_t S = 0;
+    for (const Slice& s : shards)
+      if (!s.empty()) {
+        S = s.len;
+        break;
+      }
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      Slice& s = shards[i];
+      if (s.empty() && S > 0 && s.cap < S) {
+        s.owner = std::make_shared<std::vector<uint8_t>>(S, 0);
+        s.p = s.owner->data();
+        s.cap = S;
+      }
+      p[i] = s.p;
+      n[i] = s.len;
+    }
+    Error e{co_ ? rs_co_reconstruct(co_, p.data(), n.data()) : rs_reconstruct(ctx_, p.data(), n.data())};
+    if (e) return e;
+    for (size_t i = 0; i < shards.size(); ++i)
+      if (shards[i].empty() && n[i] == S) shards[i].len = S;
+    return e;
   }
 
   Error Encode(Shards& shards) override {

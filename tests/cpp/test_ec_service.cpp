@@ -3,6 +3,7 @@
 // (readservice.go:281-304), healer repair (poller.go:274-302).  Every parity and
 // reconstructed byte is checked against the CPU oracle (oracle/librs_oracle.so,
 // linked as the checker only).  Needs a GPU; prints "ALL OK" on success.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -164,6 +165,49 @@ static void test_coalesces_exactly() {
   CHECK(calls == 16 && batches == 1 && stripes == 16 && maxb == 16);
 }
 
+// klauspost's Split with spare capacity (writeservice.go:218 hands Split the
+// request body): shards that fit in the vector's capacity are views into it (parity
+// included), the rest fresh; bytes = the oracle's split + encode; a degraded read
+// through the views returns the payload.
+static void test_split_spare_capacity(ec::Service& svc) {
+  const size_t total = ec::K + ec::M;
+  for (size_t n : {1ul, 2ul, 10ul, 410ul, 4096ul, 100000ul}) {
+    const size_t per = (n + ec::K - 1) / ec::K;
+    for (size_t spare : {0ul, 1ul, per, 2 * per + 3, total * per - n, total * per - n + 64}) {
+      const std::vector<uint8_t> value = rand_bytes(n * 131 + spare, n);
+      std::vector<uint8_t> buf;
+      buf.reserve(n + spare);
+      buf.assign(value.begin(), value.end());
+      const uint8_t* base = buf.data();
+      const size_t cap = buf.capacity();  // >= n + spare
+      ec::Slices sh;
+      CHECK(!svc.Split(buf, &sh));
+      CHECK(buf.data() == base);  // never reallocated
+      const size_t fit = std::min(total, cap / per);
+      for (size_t i = 0; i < total; ++i) {
+        CHECK(sh[i].len == per && sh[i].cap == per);
+        CHECK((i < fit) == (sh[i].p >= base && sh[i].p < base + cap));
+        if (i < fit) CHECK(sh[i].p == base + i * per);
+      }
+      CHECK(!svc.Encode(sh));
+      ec::Shards want;  // oracle: the same payload split and encoded
+      CHECK(!svc.Split(value.data(), value.size(), &want));
+      want = oracle_encode(ec::K, ec::M, want);
+      for (size_t i = 0; i < total; ++i)
+        CHECK(std::equal(sh[i].p, sh[i].p + per, want[i].begin()));
+      ec::Slices got = sh;  // readservice.go:285 with nodes 0 and 5 down
+      got[0] = ec::Slice{};
+      got[5] = ec::Slice{};
+      CHECK(!svc.Reconstruct(got));
+      std::vector<uint8_t> joined;
+      for (int i = 0; i < ec::K; ++i) joined.insert(joined.end(), got[i].p, got[i].p + got[i].len);
+      joined.resize(n);
+      CHECK(joined == value);
+      CHECK(std::equal(got[5].p, got[5].p + per, want[5].begin()));
+    }
+  }
+}
+
 int main() {
   ec::Error err;
   auto svc = ec::Service::NewService(ec::K, ec::M, 0, &err);
@@ -176,6 +220,7 @@ int main() {
   test_healer_all_patterns(*svc);
   test_errors(*svc);
   test_concurrent(*svc);
+  test_split_spare_capacity(*svc);
   // the same flows through the batch coalescer (small batches + short wait so the
   // full-batch and timed-close paths both run)
   rs_coalescer_opts opts{8, 300, 3, 0};
@@ -186,6 +231,7 @@ int main() {
     test_healer_all_patterns(*co);
     test_errors(*co);
     test_concurrent(*co);
+    test_split_spare_capacity(*co);
     uint64_t calls = 0, batches = 0, stripes = 0, maxb = 0;
     CHECK(rs_co_stats(co->coalescer(), &calls, &batches, &stripes, &maxb) == RS_OK);
     std::printf("coalescer: %llu calls, %llu batches, %llu stripes, largest batch %llu\n",

@@ -306,3 +306,57 @@ def test_many_and_single_callers_share_batches(gpu):
         assert st["stripes"] == 12 * 20 * 13 + 36 * 20
     finally:
         svc.close()
+
+
+@pytest.mark.parametrize("staged_dma", [False, True])
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3)])
+def test_encode_hash_matches_hashlib_and_oracle(gpu, k, m, staged_dma):
+    """rs_co_encode_hash: the write path's Split -> Encode -> cold_hash
+    (writeservice.go:218-222, :267) in one coalesced batch.  Parity = the oracle's,
+    digest = hashlib.sha256(value), for values whose shard length is and is not a
+    multiple of 16 (the staged shards then sit at a 16-B pitch with gaps: the
+    kernel reads the value across them), mixed in batches with plain encodes and
+    reconstructs from concurrent callers."""
+    import hashlib
+
+    svc = CoalescingService(k, m, max_batch=48, max_wait_us=300, inflight=3, staged_dma=staged_dma)
+    try:
+        sizes = [1, 2, 3, 63, 64, 65, 1000, 4096, 4097, 10 * 1024 + 7, 100 * 1024, 65536 + 5]
+
+        def worker(t):
+            rng = np.random.default_rng(100 + t)
+            for j in range(len(sizes)):
+                length = sizes[(t + j) % len(sizes)]
+                data = xoshiro_bytes(t * 7919 + j, length)
+                shards = svc.Split(data)
+                ref = rs_oracle.split(k, m, data)
+                assert rs_oracle.encode(k, m, ref) == 0
+                if j % 3 == 2:  # a plain encode / a repair in the same batches
+                    svc.Encode(shards)
+                    got = [None if i == int(rng.integers(0, k + m)) else bytearray(s) for i, s in enumerate(shards)]
+                    svc.Reconstruct(got)
+                    assert [bytes(s) for s in got] == [bytes(s) for s in ref]
+                    continue
+                digest = svc.EncodeHash(shards, len(data))
+                assert [bytes(s) for s in shards] == [bytes(s) for s in ref], (length, "parity")
+                assert digest == hashlib.sha256(data).digest(), (length, "cold_hash")
+
+        _run_threads(8, worker)
+        # many objects in one call; value_len may stop short of the padded shards
+        objs, vals = [], []
+        for i, length in enumerate(sizes):
+            data = xoshiro_bytes(555 + i, length)
+            objs.append(svc.Split(data))
+            vals.append(data)
+        res = svc.EncodeHashMany(objs, [len(v) for v in vals])
+        for (err, dig), data, sh in zip(res, vals, objs):
+            assert err is None and dig == hashlib.sha256(data).digest()
+            ref = rs_oracle.split(k, m, data)
+            assert rs_oracle.encode(k, m, ref) == 0
+            assert [bytes(s) for s in sh] == [bytes(s) for s in ref]
+        # a value_len past the k data shards is rejected, nothing written
+        sh = svc.Split(b"abc" * 100)
+        with pytest.raises(ECError):
+            svc.EncodeHash(sh, k * len(sh[0]) + 1)
+    finally:
+        svc.close()

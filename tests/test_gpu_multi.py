@@ -237,6 +237,49 @@ def test_deferred_errors_are_per_stream(gpu):
         eng.close()
 
 
+def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
+    """More streams than one status chunk (1 024 words): every stream keeps its own
+    deferred-error word (streams past the 1 023rd shared the last word),
+    and a released stream's word comes back clean to whichever stream gets it next."""
+    import torch
+
+    k, m, S, N = 4, 2, 256, 8
+    P = shard_pitch_for(S)
+    eng = BatchEngine(k, m, 0)
+    try:
+        d = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda")
+        p = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+        eng.encode(d, p, S, N)
+        good = torch.full((N,), 0b111110, dtype=torch.int32, device="cuda")
+        bad = good.clone()
+        bad[3] = 0b000011
+        torch.cuda.synchronize()
+        streams = [torch.cuda.Stream() for _ in range(1100)]
+        for i, s in enumerate(streams):  # every 7th stream gets an invalid mask
+            eng.reconstruct_devmask(d, p, S, N, bad if i % 7 == 0 else good, stream=s)
+        for i, s in enumerate(streams):
+            if i % 7 == 0:
+                with pytest.raises(ECError, match="too few shards given"):
+                    eng.sync(stream=s)
+            else:
+                eng.sync(stream=s)
+        # release half of them with an error pending: the words come back zeroed
+        for i, s in enumerate(streams[:550]):
+            eng.reconstruct_devmask(d, p, S, N, bad, stream=s)
+            with pytest.raises(ECError):
+                eng.stream_release(stream=s)
+        fresh = [torch.cuda.Stream() for _ in range(550)]  # reuse the released words
+        for s in fresh:
+            eng.reconstruct_devmask(d, p, S, N, good, stream=s)
+        for s in fresh:
+            eng.sync(stream=s)
+            eng.stream_release(stream=s)
+        for s in streams[550:]:
+            eng.stream_release(stream=s)
+    finally:
+        eng.close()
+
+
 def test_host_mask_uploads_survive_queued_kernels(gpu):
     """Per-stripe host masks for asynchronous device calls, many calls queued behind
     a long kernel on one stream and more on a second stream: every call must use

@@ -1,21 +1,24 @@
-"""Every batched kernel family against the CPU oracle, in one process.
+"""Every batched kernel path of each specialised shape against the CPU oracle, in
+one process.
 
-rs_set_kernel_variant selects the family the specialised shapes launch:
-  1  grid-stride apply_kernel + bitsliced encode (the default)
-  2  pipe_kernel, one wave per SIMD, 2 task slots per wave
-  3  pipe_kernel, 3 task slots
-  4  grid-stride apply_kernel for encode too (no bitsliced program)
-Each must give the oracle's bytes for encode, uniform reconstruct, per-stripe
-reconstruct (host and device masks) and out-of-place reconstruct, with the slot
-padding untouched, on the BASELINE shapes and a tail length (S % 16 != 0).
+The engine picks the kernel by shape and call: bitsliced or lookup encode,
+stripe-aligned or flat-task per-stripe reconstruct, uniform-plan reconstruct (slots
+resolved once per launch), and for device masks the erasure bound E of the launch
+(rs_reconstruct_batch_out_devmask's max_missing; E <= 2 runs the input-outer flat
+kernel).  Each must give the oracle's bytes, with slot padding untouched, on the
+BASELINE shapes and a tail length (S % 16 != 0).
 """
 import numpy as np
 import pytest
 
 from oracle import rs_oracle
+from replication_erasurecoding_object_store_amd import _lib
 from replication_erasurecoding_object_store_amd.batch import BatchEngine, shard_pitch_for
+from replication_erasurecoding_object_store_amd.ec import ECError
 
 pytestmark = pytest.mark.gpu
+
+SHAPES = [(4, 2, 1024), (8, 4, 8192), (10, 4, 6554), (10, 4, 413), (6, 3, 1000), (4, 2, 1000)]
 
 
 @pytest.fixture(scope="module")
@@ -26,73 +29,137 @@ def engines(gpu):
         e.close()
 
 
-def _masks(rng, N, t, m):
+def _engine(engines, k, m):
+    if (k, m) not in engines:
+        engines[(k, m)] = BatchEngine(k, m, 0)
+    return engines[(k, m)]
+
+
+def _masks(rng, N, t, lo, hi):
+    """Per-stripe present masks with lo..hi erasures each."""
     masks = np.full(N, (1 << t) - 1, np.uint32)
     for i in range(N):
-        for j in rng.choice(t, size=rng.integers(0, m + 1), replace=False):
+        for j in rng.choice(t, size=rng.integers(lo, hi + 1), replace=False):
             masks[i] &= ~np.uint32(1 << int(j))
     return masks
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4])
-@pytest.mark.parametrize("k,m,S", [(4, 2, 1024), (8, 4, 8192), (10, 4, 6554), (10, 4, 413), (6, 3, 1000)])
-def test_variant_matches_oracle(engines, variant, k, m, S):
+def _codewords(eng, k, m, S, N, seed):
     import torch
 
-    if (k, m) not in engines:
-        engines[(k, m)] = BatchEngine(k, m, 0)
-    eng = engines[(k, m)]
-    eng.set_kernel_variant(variant)
-    try:
-        t, N, P = k + m, 300, shard_pitch_for(S)
-        g = torch.Generator(device="cuda").manual_seed(variant * 1000 + k * 31 + S)
-        data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
-        parity = torch.full((N, m, P), 0xEE, dtype=torch.uint8, device="cuda")
-        eng.encode(data, parity, S, N)
-        torch.cuda.synchronize()
-        uni = np.zeros((N, t, P), np.uint8)
-        uni[:, :k] = data.cpu().numpy()
-        rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), t * P, P, S, N)
-        par = parity.cpu().numpy()
-        assert np.array_equal(par[:, :, :S], uni[:, k:, :S]), "encode != oracle"
-        assert (par[:, :, S:] == 0xEE).all(), "slot padding written"
+    t, P = k + m, shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.full((N, m, P), 0xEE, dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    torch.cuda.synchronize()
+    uni = np.zeros((N, t, P), np.uint8)
+    uni[:, :k] = data.cpu().numpy()
+    rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), t * P, P, S, N)
+    par = parity.cpu().numpy()
+    assert np.array_equal(par[:, :, :S], uni[:, k:, :S]), "encode != oracle"
+    assert (par[:, :, S:] == 0xEE).all(), "slot padding written"
+    return data, parity, uni
 
-        rng = np.random.default_rng(variant + S)
-        # uniform pattern (two shards, one data one parity), in place
-        one = np.uint32(((1 << t) - 1) & ~((1 << 1) | (1 << k)))
+
+@pytest.mark.parametrize("k,m,S", SHAPES)
+def test_paths_match_oracle(engines, k, m, S):
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, N, P = k + m, 300, shard_pitch_for(S)
+    data, parity, uni = _codewords(eng, k, m, S, N, k * 31 + S)
+    rng = np.random.default_rng(S)
+    # uniform patterns (slots resolved once per launch), in place: one data + one
+    # parity shard, two data shards, the parity shards only
+    for lost in ((1, k), (0, 1), tuple(range(k, t))):
+        one = np.uint32(((1 << t) - 1) & ~sum(1 << j for j in lost))
         d2, p2 = data.clone(), parity.clone()
-        d2[:, 1, :S] = 0x33
-        p2[:, 0, :S] = 0x33
+        for j in lost:
+            (d2[:, j] if j < k else p2[:, j - k])[:, :S] = 0x33
         eng.reconstruct(d2, p2, S, N, one)
         torch.cuda.synchronize()
-        assert torch.equal(d2[:, :, :S], data[:, :, :S]) and torch.equal(p2[:, :, :S], parity[:, :, :S])
+        assert torch.equal(d2, data) and torch.equal(p2, parity), lost
 
-        # per-stripe patterns, 0..m erasures: host masks then device masks, in place
-        for use_dev in (False, True):
-            masks = _masks(rng, N, t, m)
-            lost = ((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0
-            d2, p2 = data.clone(), parity.clone()
-            d2[:, :, :S][torch.from_numpy(lost[:, :k]).cuda()] = 0x33
-            p2[:, :, :S][torch.from_numpy(lost[:, k:]).cuda()] = 0x33
-            if use_dev:
-                eng.reconstruct_devmask(d2, p2, S, N, torch.from_numpy(masks.view(np.int32)).cuda())
-                eng.sync()
-            else:
-                eng.reconstruct(d2, p2, S, N, masks)
-            torch.cuda.synchronize()
-            assert torch.equal(d2[:, :, :S], data[:, :, :S]), (variant, use_dev)
-            assert torch.equal(p2[:, :, :S], parity[:, :, :S]), (variant, use_dev)
+    # per-stripe patterns, 0..m erasures: host masks then device masks, in place
+    for use_dev in (False, True):
+        masks = _masks(rng, N, t, 0, m)
+        lost = ((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0
+        d2, p2 = data.clone(), parity.clone()
+        d2[:, :, :S][torch.from_numpy(lost[:, :k]).cuda()] = 0x33
+        p2[:, :, :S][torch.from_numpy(lost[:, k:]).cuda()] = 0x33
+        if use_dev:
+            eng.reconstruct_devmask(d2, p2, S, N, torch.from_numpy(masks.view(np.int32)).cuda())
+            eng.sync()
+        else:
+            eng.reconstruct(d2, p2, S, N, masks)
+        torch.cuda.synchronize()
+        assert torch.equal(d2, data), use_dev
+        assert torch.equal(p2, parity), use_dev
 
-        # out of place, device masks: the r-th missing shard at out[i, r]
-        masks = _masks(rng, N, t, m)
+    # out of place: uniform host mask, then device masks with and without a bound
+    for lost in ((0, 1), (1, k)):
+        one = ((1 << t) - 1) & ~sum(1 << j for j in lost)
         out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
-        eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
+        eng.reconstruct_out(data, parity, out, S, N, present_masks=one)
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        for r, s in enumerate(lost):
+            assert np.array_equal(o[:, r, :S], uni[:, s, :S]), (lost, s)
+        assert (o[:, len(lost):] == 0xC3).all() and (o[:, :, S:] == 0xC3).all()
+    for bound in (0, 1, 2, m):
+        hi = bound or m
+        masks = _masks(rng, N, t, 1 if bound == 1 else 0, hi)
+        out = torch.full((N, max(hi, 1), P), 0xC3, dtype=torch.uint8, device="cuda")
+        eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
+                            max_missing=bound)
         eng.sync()
         o = out.cpu().numpy()
         for i in range(N):
             miss = [s for s in range(t) if not (masks[i] >> s) & 1]
             for r, s in enumerate(miss):
-                assert np.array_equal(o[i, r, :S], uni[i, s, :S]), (variant, i, s)
+                assert np.array_equal(o[i, r, :S], uni[i, s, :S]), (bound, i, s)
             assert (o[i, len(miss):] == 0xC3).all() and (o[i, :, S:] == 0xC3).all()
-    finally:
-        eng.set_kernel_variant(0)
+
+
+@pytest.mark.parametrize("k,m,S", [(10, 4, 6554), (8, 4, 8192), (4, 2, 1024), (10, 4, 413)])
+@pytest.mark.parametrize("bound", [1, 2])
+def test_devmask_bound_flags_and_skips_excess(engines, k, m, S, bound):
+    """Stripes missing more than max_missing shards are left untouched and reported
+    by rs_sync as RS_ERR_INVALID_ARG; every other stripe is still rebuilt; a stripe
+    with < k present wins as RS_ERR_TOO_FEW_SHARDS."""
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, N, P = k + m, 257, shard_pitch_for(S)
+    data, parity, uni = _codewords(eng, k, m, S, N, 77 + bound)
+    rng = np.random.default_rng(bound * 7 + S)
+    masks = _masks(rng, N, t, 1, bound)
+    over = [5, 64, 65, 200]  # neighbours of straddling flat tasks included
+    for i in over:
+        masks[i] = ((1 << t) - 1) & ~((1 << (bound + 1)) - 1)  # bound + 1 erasures
+    out = torch.full((N, bound, P), 0xC3, dtype=torch.uint8, device="cuda")
+    mdev = torch.from_numpy(masks.view(np.int32)).cuda()
+    eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=bound)
+    with pytest.raises(ECError) as ei:
+        eng.sync()
+    assert ei.value.code == _lib.RS_ERR_INVALID_ARG
+    eng.sync()  # cleared
+    o = out.cpu().numpy()
+    for i in range(N):
+        if i in over:
+            assert (o[i] == 0xC3).all(), i
+            continue
+        miss = [s for s in range(t) if not (masks[i] >> s) & 1]
+        for r, s in enumerate(miss):
+            assert np.array_equal(o[i, r, :S], uni[i, s, :S]), (i, s)
+    # a stripe with fewer than k present as well: TOO_FEW_SHARDS takes precedence
+    masks[9] = (1 << (k - 1)) - 1
+    eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
+                        max_missing=bound)
+    with pytest.raises(ECError) as ei:
+        eng.sync()
+    assert ei.value.code == _lib.RS_ERR_TOO_FEW_SHARDS
+    # the bound is checked against the out layout and m
+    with pytest.raises(ECError):
+        eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=-1)

@@ -1,8 +1,10 @@
-"""A/B kernel variants and occupancy in ONE process, interleaved rounds
+"""Kernel timing per workload and occupancy in ONE process, interleaved rounds
 (cdna_hip_programming.md §5.4 rule 24).  Prints HBM GB/s (algorithmic bytes /
-event-timed kernel time) per (workload, variant, blocks/CU).
+event-timed kernel time) per (workload, blocks/CU).  A/B of kernel variants: build
+them as separate libraries (tools/build_ab.sh) and alternate them with
+tools/run_ab.sh, which runs this script once per library.
 
-Usage: python tools/ab_bench.py [--rounds 3] [--quick]
+Usage: python tools/ab_bench.py [--rounds 3] [--workloads a,b] [--bpc 0]
 """
 import argparse
 import itertools
@@ -35,6 +37,14 @@ WORKLOADS = {
     "rs42_4K_rec1p_out": (4, 2, 1024, 65536, "rec1p_out"),
     "rs104_64K_rec1p_out": (10, 4, 6554, 16384, "rec1p_out"),
     "rs104_64K_rec4p_out": (10, 4, 6554, 16384, "rec4p_out"),
+    # device masks with the caller's erasure bound (rs_reconstruct_batch_out_devmask)
+    "rs104_64K_rec1pb_out": (10, 4, 6554, 16384, "rec1pb_out"),
+    "rs104_64K_rec2pb_out": (10, 4, 6554, 16384, "rec2pb_out"),
+    "rs84_64K_rec1pb_out": (8, 4, 8192, 16384, "rec1pb_out"),
+    "rs84_64K_rec2pb_out": (8, 4, 8192, 16384, "rec2pb_out"),
+    "rs84_64K_rec1p_out": (8, 4, 8192, 16384, "rec1p_out"),
+    "rs42_4K_rec04u_out": (4, 2, 1024, 65536, "rec04u_out"),
+    "rs42_4K_rec45u_out": (4, 2, 1024, 65536, "rec45u_out"),
     "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
     "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),
     "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
@@ -57,7 +67,7 @@ WORKLOADS = {
 def alg_bytes(name):
     """Algorithmic HBM bytes of one launch of workload `name`."""
     k, m, S, N, mode = WORKLOADS[name]
-    e = {"enc": m, "ver": m, "encu_out": m, "rec1p_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
+    e = {"enc": m, "ver": m, "encu_out": m, "rec1p_out": 1, "rec1pb_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
     return N * S * (k + e)
 
 
@@ -65,8 +75,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--min-ms", type=float, default=0.0,
+                    help="time at least this many ms of back-to-back launches per round (sustained clocks)")
     ap.add_argument("--bpc", default="1,2,3,4,8")
-    ap.add_argument("--variants", default="0")
     ap.add_argument("--workloads", default="all")
     ap.add_argument("--pads", default="0", help="comma-separated extra bytes added to the shard pitch "
                                                 "(multiples of 16), each its own workload line")
@@ -81,7 +92,6 @@ def main():
     workloads = dict(WORKLOADS)
     if args.workloads != "all":
         workloads = {k: v for k, v in workloads.items() if k in args.workloads.split(",")}
-    variants = [int(v) for v in args.variants.split(",")]
     bpcs = [int(b) for b in args.bpc.split(",")]
     results = {}
     engines = {}
@@ -139,6 +149,14 @@ def main():
                 eng.reconstruct_devmask(d, p, S, N, m45)
             elif mode == "rec1p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks1)
+            elif mode == "rec1pb_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks1, max_missing=1)
+            elif mode == "rec2pb_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb], max_missing=2)
+            elif mode == "rec04u_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=((1 << t) - 1) & ~0b10001)
+            elif mode == "rec45u_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=0b001111)
             elif mode == "rec4p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks4)
             elif mode == "rec2p_out":
@@ -155,43 +173,42 @@ def main():
                 eng.reconstruct_devmask(d, p, S, N, masks[i % nb])
 
         for rnd in range(args.rounds):
-            for v in variants:
-                for bpc in bpcs:
-                    eng.set_kernel_variant(v)
-                    eng.set_blocks_per_cu(bpc)
-                    for i in range(2):
-                        run(i)
+            for bpc in bpcs:
+                eng.set_blocks_per_cu(bpc)
+                for i in range(2):
+                    run(i)
+                iters = args.iters
+                for rep in range(2 if args.min_ms > 0 else 1):  # first pass sizes the second
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    for i in range(args.iters):
+                    for i in range(iters):
                         run(i)
                     e1.record()
                     torch.cuda.synchronize()
-                    ms = e0.elapsed_time(e1) / args.iters
-                    results.setdefault((name, v, bpc), []).append(alg / (ms * 1e-3) / 1e9)
-                    knames[(v, bpc)] = eng.last_kernel()
-                    # outputs of buffer 0 under this variant (must agree across variants)
-                    run(0)
-                    torch.cuda.synchronize()
-                    o = outs[0] if outs else (bufs[0][1] if mode == "enc" else
-                                              (bad if mode == "ver" else torch.cat([bufs[0][0], bufs[0][1]], 1)))
-                    digests.setdefault(name, set()).add(hash(o.cpu().numpy().tobytes()))
+                    ms = e0.elapsed_time(e1) / iters
+                    iters = max(args.iters, int(np.ceil(args.min_ms / max(ms, 1e-3))))
+                results.setdefault((name, bpc), []).append(alg / (ms * 1e-3) / 1e9)
+                knames[bpc] = eng.last_kernel()
+                # outputs of buffer 0 at this occupancy (must agree across occupancies)
+                run(0)
+                torch.cuda.synchronize()
+                o = outs[0] if outs else (bufs[0][1] if mode == "enc" else
+                                          (bad if mode == "ver" else torch.cat([bufs[0][0], bufs[0][1]], 1)))
+                digests.setdefault(name, set()).add(hash(o.cpu().numpy().tobytes()))
         eng.sync()
         # correctness spot check after all variants: stripes reconstruct to the encoded bytes
         d, p = bufs[0]
         chk = torch.empty_like(p[:256])
         eng.set_blocks_per_cu(0)
-        eng.set_kernel_variant(0)
         eng.encode(d[:256], chk, S, 256)
         torch.cuda.synchronize()
         ok = bool(torch.equal(chk[:, :, :S], p[:256, :, :S]))
-        for v in variants:
-            for bpc in bpcs:
-                r = results[(name, v, bpc)]
-                print(f"{name:18s} v{v} bpc={bpc:2d}: median {np.median(r):7.1f} GB/s  max {np.max(r):7.1f}  "
-                      f"({np.median(r) / 8000 * 100:4.1f}% of 8 TB/s)  {knames[(v, bpc)]}", flush=True)
-        print(f"{name:18s} parity-consistent after all runs: {ok}; variants agree on outputs: "
+        for bpc in bpcs:
+            r = results[(name, bpc)]
+            print(f"{name:18s} bpc={bpc:2d}: median {np.median(r):7.1f} GB/s  max {np.max(r):7.1f}  "
+                  f"({np.median(r) / 8000 * 100:4.1f}% of 8 TB/s)  {knames[bpc]}", flush=True)
+        print(f"{name:18s} parity-consistent after all runs: {ok}; occupancies agree on outputs: "
               f"{len(digests[name]) == 1}", flush=True)
         del bufs, masks
         torch.cuda.empty_cache()

@@ -1,15 +1,20 @@
 // coalesce_bench.cpp -- per-object IEcDriver throughput with T concurrent callers
-// (the gateway's goroutine-per-request model, cmd/api/main.go:227), direct
-// (rs_encode / rs_reconstruct: one H2D->kernel->D2H per object) vs through the
-// batch coalescer (rs_co_*).  Objects: 4 KiB RS(4+2) (S = 1024), host memory.
-// Workload per call: "enc" = Encode; "mix" = 50/50 Encode and 1-erasure
+// (the gateway's goroutine-per-request model, cmd/api/main.go:227): direct
+// (rs_encode / rs_reconstruct: one H2D->kernel->D2H per object), through the batch
+// coalescer (rs_co_*), or the CPU codec on the caller's own thread ("cpu": the
+// oracle/ C restatement of klauspost's AVX-512 GFNI / AVX2 kernels with tables
+// prepared once, as klauspost keeps them in its Encoder -- the reported baseline,
+// single goroutine per call as ec.go:26 configures it).  RS(4+2) objects of
+// obj_bytes (4 KiB default; the reference's payloads: 10 / 100 / 800 KiB,
+// benchmark/k6/benchmark.js:14-19, and 1500 KiB, go-ycsb hybridstore db.go:56), host
+// memory.  Workload per call: "enc" = Encode; "mix" = 50/50 Encode and 1-erasure
 // Reconstruct (SURVEY.md §8d config 5's mix).  Prints one JSON line per run.
 //
 // Build: g++ -std=c++17 -O2 -pthread tools/coalesce_bench.cpp -o tools/coalesce_bench \
-//          -Ireplication_erasurecoding_object_store_amd -Lreplication_erasurecoding_object_store_amd \
-//          -lrsgpu -Wl,-rpath,$PWD/replication_erasurecoding_object_store_amd \
-//          -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
-// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight]
+//          -Lreplication_erasurecoding_object_store_amd -lrsgpu \
+//          -Wl,-rpath,$PWD/replication_erasurecoding_object_store_amd -Loracle -lrs_oracle \
+//          -Wl,-rpath,$PWD/oracle -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
+// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co|cpu> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight]
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -20,6 +25,7 @@
 #include <vector>
 
 #include "../include/rsgpu.h"
+#include "../oracle/rs_oracle.h"
 
 int main(int argc, char** argv) {
   if (argc < 5) {
@@ -31,6 +37,7 @@ int main(int argc, char** argv) {
   const double secs = std::atof(argv[2]);
   const bool mix = std::strcmp(argv[3], "mix") == 0;
   const bool co_mode = std::strcmp(argv[4], "co") == 0;
+  const bool cpu_mode = std::strcmp(argv[4], "cpu") == 0;
   rs_coalescer_opts opts{0, 0, 0, 0, 0, 0};
   if (argc > 5) opts.max_batch = std::strtoull(argv[5], nullptr, 10);
   if (argc > 6) opts.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
@@ -47,6 +54,23 @@ int main(int argc, char** argv) {
   rs_coalescer* co = nullptr;
   if (co_mode && rs_coalescer_create(ctx, &opts, &co)) return 1;
   const size_t S = rs_shard_size(ctx, obj);
+  // CPU codec plans: encode rows, and per lost shard the composed decode row over
+  // the first k survivors (klauspost caches decode matrices per erasure pattern)
+  void* enc_plan = nullptr;
+  std::vector<void*> rec_plan(k + m, nullptr);
+  std::vector<std::vector<int>> rec_in(k + m, std::vector<int>(k));
+  if (cpu_mode) {
+    std::vector<uint8_t> mat((k + m) * k);
+    rso_build_matrix(k, m, mat.data());
+    enc_plan = rso_baseline_plan_new(k, m, mat.data() + k * k);
+    for (int lost = 0; lost < k + m; ++lost) {
+      std::vector<uint8_t> present(k + m, 1), rows(m * k);
+      present[lost] = 0;
+      int miss[32], nmiss = 0;
+      rso_decode_rows(k, m, present.data(), rec_in[lost].data(), miss, &nmiss, rows.data());
+      rec_plan[lost] = rso_baseline_plan_new(k, nmiss, rows.data());
+    }
+  }
   std::atomic<bool> stop{false}, start{false};
   std::atomic<uint64_t> ops{0}, bad{0};
   std::vector<std::thread> ts;
@@ -76,10 +100,20 @@ int main(int argc, char** argv) {
           const int lost = static_cast<int>((j >> 1) % (k + m));
           n.assign(k + m, S);
           n[lost] = 0;
-          rc = co ? rs_co_reconstruct(co, p.data(), n.data()) : rs_reconstruct(ctx, p.data(), n.data());
+          if (cpu_mode) {
+            const uint8_t* in[32];
+            for (int c = 0; c < k; ++c) in[c] = p[rec_in[lost][c]];
+            uint8_t* out[1] = {p[lost]};
+            rc = rso_baseline_plan_apply(rec_plan[lost], in, out, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
+          } else {
+            rc = co ? rs_co_reconstruct(co, p.data(), n.data()) : rs_reconstruct(ctx, p.data(), n.data());
+          }
         } else {
           n.assign(k + m, S);
-          rc = co ? rs_co_encode(co, p.data(), n.data()) : rs_encode(ctx, p.data(), n.data());
+          if (cpu_mode)
+            rc = rso_baseline_plan_apply(enc_plan, p.data(), p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
+          else
+            rc = co ? rs_co_encode(co, p.data(), n.data()) : rs_encode(ctx, p.data(), n.data());
         }
         if (rc != RS_OK) ++bad;
         for (int i = 0; i < k + m; ++i)
@@ -105,11 +139,14 @@ int main(int argc, char** argv) {
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
       "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d}\n",
-      co ? "coalesced" : "direct", mix ? "mix" : "enc", T, obj, dt, n_ops / dt,
+      co ? "coalesced" : (cpu_mode ? "cpu" : "direct"), mix ? "mix" : "enc", T, obj, dt, n_ops / dt,
       n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight);
   if (co) rs_coalescer_destroy(co);
+  if (enc_plan) rso_baseline_plan_free(enc_plan);
+  for (void* pl : rec_plan)
+    if (pl) rso_baseline_plan_free(pl);
   rs_destroy(ctx);
   return bad.load() ? 1 : 0;
 }
