@@ -670,11 +670,16 @@ def main():
         else:
             prof = None
 
+    # physical GPUs behind the ranks (PCI bus of each rank's device): a rehearsal of
+    # the N > 1 path with ranks sharing one GPU says so instead of passing for N GPUs
+    prop = torch.cuda.get_device_properties(torch.cuda.current_device())
+    physical_gpus = rdist.distinct_count((prop.pci_domain_id << 16) | (prop.pci_bus_id << 5) | prop.pci_device_id)
     out = {
         "metric": "GiB/s device-resident RS(4+2) encode + 2-erasure reconstruct, batched stripes",
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
+        "physical_gpus": physical_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),

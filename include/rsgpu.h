@@ -50,6 +50,7 @@ extern "C" {
 #define RS_ERR_NO_DEVICE 17     /* no usable GPU */
 #define RS_ERR_DEVICE 18        /* HIP runtime failure */
 #define RS_ERR_NOT_SUPPORTED 19 /* klauspost ErrNotSupported "operation not supported" */
+#define RS_ERR_BUSY 20          /* coalescer: every batch awaits rs_co_reap; reap, then resubmit */
 
 /* memory kinds for the batched entry points */
 #define RS_MEM_DEVICE 0 /* pointers are device memory; call is asynchronous on `stream` */
@@ -247,6 +248,28 @@ int rs_co_encode_hash(rs_coalescer *co, uint8_t *const *shards, const size_t *le
                       uint8_t *digest);
 int rs_co_encode_hash_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards, const size_t *lens,
                            const size_t *value_lens, uint8_t *digests, int *rcs);
+/* Asynchronous per-object calls, for callers that multiplex many requests on few
+ * threads (the Go runtime's goroutines on GOMAXPROCS threads, an event loop): a
+ * blocking call costs its thread a futex sleep and wake-up per object, several
+ * microseconds of CPU against ~1 us of codec work for a 4 KiB object on one core.
+ * rs_co_submit_* validate and stage the object exactly as rs_co_encode /
+ * rs_co_reconstruct do and return at once; the call completes when rs_co_reap
+ * returns its tag, with its code: encode -> every parity shard written;
+ * reconstruct -> every missing (len 0) shard filled with S bytes (lens is not
+ * written).  Until then the caller keeps every shard buffer valid and untouched
+ * (the arrays of pointers and lengths may be reused at once).  A call rejected at
+ * submit returns its code and is never reaped; RS_ERR_BUSY: every staging batch
+ * holds unreaped calls -- reap, then submit again (submit never blocks).  An object
+ * with nothing to compute (a reconstruct with nothing missing, m == 0) is rejected
+ * with RS_ERR_NOT_SUPPORTED.
+ * rs_co_reap: up to max completed calls -> tags[i], rcs[i]; copies their outputs
+ * into the callers' buffers on the reaping thread.  Waits up to timeout_us for at
+ * least one (0: poll, < 0: until one completes); returns how many (a negative
+ * code on bad arguments).  Any number of threads may submit and reap.  Reap every
+ * submitted call before rs_coalescer_destroy. */
+int rs_co_submit_encode(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, uint64_t tag);
+int rs_co_submit_reconstruct(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, uint64_t tag);
+int rs_co_reap(rs_coalescer *co, uint64_t *tags, int *rcs, int max, int timeout_us);
 /* Counters since creation: calls, device batches, stripes batched, largest batch. */
 int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
                 uint64_t *max_batch);

@@ -16,9 +16,11 @@ package ec
 import "C"
 
 import (
+	"crypto/sha256"
 	"errors"
 	"log"
 	"runtime"
+	"sync"
 	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
@@ -34,10 +36,61 @@ import (
 // every MI355X of the node (rs_create_multi): the coalescer spreads its batches
 // over the GPUs.  On a host with no usable GPU, cpu is the reference's own codec
 // (klauspost, configured exactly as ec.go:26) and every call goes to it.
+//
+// Encode and Reconstruct use the coalescer's asynchronous calls: the request
+// goroutine stages its object (rs_co_submit_*, no blocking in C), then parks on a
+// channel; one reaper goroutine collects finished calls (rs_co_reap) and wakes
+// their goroutines.  A blocking cgo call would instead hold an OS thread per
+// in-flight request and pay a futex sleep and wake-up per object.
 type Service struct {
 	ctx *C.rs_ctx
 	co  *C.rs_coalescer
 	cpu reedsolomon.Encoder
+
+	mu      sync.Mutex
+	nextTag uint64
+	waiting map[uint64]chan C.int
+}
+
+// call runs one asynchronous coalescer call: submit(tag) stages it; the result
+// arrives from the reaper.  The caller keeps its shard buffers pinned until then.
+func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
+	ch := make(chan C.int, 1)
+	s.mu.Lock()
+	s.nextTag++
+	tag := s.nextTag
+	s.waiting[tag] = ch
+	s.mu.Unlock()
+	for {
+		rc := submit(C.uint64_t(tag))
+		if rc == C.RS_OK {
+			return toErr(<-ch)
+		}
+		if rc != C.RS_ERR_BUSY { // rejected: never reaped
+			s.mu.Lock()
+			delete(s.waiting, tag)
+			s.mu.Unlock()
+			return toErr(rc)
+		}
+		runtime.Gosched() // every staging batch awaits the reaper: let it run, retry
+	}
+}
+
+// reap delivers finished calls to their goroutines (one goroutine per Service).
+func (s *Service) reap() {
+	const max = 256
+	tags := (*[max]C.uint64_t)(C.malloc(max * C.size_t(unsafe.Sizeof(C.uint64_t(0)))))
+	rcs := (*[max]C.int)(C.malloc(max * C.size_t(unsafe.Sizeof(C.int(0)))))
+	for {
+		n := int(C.rs_co_reap(s.co, &tags[0], &rcs[0], max, -1))
+		for i := 0; i < n; i++ {
+			s.mu.Lock()
+			ch := s.waiting[uint64(tags[i])]
+			delete(s.waiting, uint64(tags[i]))
+			s.mu.Unlock()
+			ch <- rcs[i]
+		}
+	}
 }
 
 // Keep klauspost's exported sentinels so errors.Is and %v output match ec.go.
@@ -88,7 +141,9 @@ func NewService() interfaces.IEcDriver {
 		log.Fatalf("Failed to create Reed-Solomon batch coalescer: %v", toErr(rc))
 	}
 	log.Printf("EC Driver loaded (k=%d, m=%d) on %s\n", config.K, config.M, C.GoString(C.rs_backend(ctx)))
-	return &Service{ctx: ctx, co: co}
+	s := &Service{ctx: ctx, co: co, waiting: make(map[uint64]chan C.int)}
+	go s.reap()
+	return s
 }
 
 // Split is klauspost v1.12.1's Split (reedsolomon.go) in Go -- no arithmetic, so it
@@ -179,10 +234,10 @@ func (s *Service) Encode(shards [][]byte) error {
 		return reedsolomon.ErrTooFewShards
 	}
 	var pin runtime.Pinner
-	defer pin.Unpin()
+	defer pin.Unpin() // after the call completed: the engine writes parity until then
 	p, l, free := shardArgs(shards, &pin)
 	defer free()
-	return toErr(C.rs_co_encode(s.co, p, l))
+	return s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_encode(s.co, p, l, tag) })
 }
 
 // Reconstruct fills every empty entry, data and parity (ec.go:59-61;
@@ -204,25 +259,81 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 	if size == 0 {
 		return reedsolomon.ErrShardNoData
 	}
+	missing := 0
 	for i := range shards {
-		if len(shards[i]) == 0 && cap(shards[i]) < size {
-			shards[i] = make([]byte, 0, size) // storage for the engine; len 0 = missing
+		if len(shards[i]) == 0 {
+			missing++
+			if cap(shards[i]) < size {
+				shards[i] = make([]byte, 0, size) // storage for the engine; len 0 = missing
+			}
 		}
+	}
+	if missing == 0 { // klauspost: nothing to do (shard sizes are still checked by it)
+		for _, sh := range shards {
+			if len(sh) != size {
+				return reedsolomon.ErrShardSize
+			}
+		}
+		return nil
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	p, l, free := shardArgs(shards, &pin)
 	defer free()
-	lens := unsafe.Slice(l, len(shards))
-	if err := toErr(C.rs_co_reconstruct(s.co, p, l)); err != nil {
+	if err := s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_reconstruct(s.co, p, l, tag) }); err != nil {
 		return err
 	}
-	for i := range shards {
-		if len(shards[i]) == 0 && int(lens[i]) == size {
+	for i := range shards { // every missing entry was filled
+		if len(shards[i]) == 0 {
 			shards[i] = shards[i][:size]
 		}
 	}
 	return nil
+}
+
+// EncodeHash is Encode plus the write path's cold_hash in the same GPU batch:
+// WriteEC splits and encodes `value` (writeservice.go:218-222) and later stores
+// computeSHA256Hex(value) (:267; hybrid writes :326, :382-386).  The data shards of
+// Split(value) are the value followed by zero padding, so the SHA-256 of their
+// first valueLen = len(value) bytes is that hash; the engine computes it over the
+// shards it has already staged for the encode (rs_co_encode_hash).  Not part of
+// IEcDriver: a caller type-asserts for
+//   interface{ EncodeHash([][]byte, int) ([32]byte, error) }
+// and keeps Encode + computeSHA256Hex otherwise.
+func (s *Service) EncodeHash(shards [][]byte, valueLen int) (sum [32]byte, err error) {
+	if s.cpu != nil {
+		if err = s.cpu.Encode(shards); err != nil {
+			return sum, err
+		}
+		h := sha256.New()
+		rem := valueLen
+		for i := 0; i < config.K && rem > 0; i++ {
+			n := min(rem, len(shards[i]))
+			h.Write(shards[i][:n])
+			rem -= n
+		}
+		if rem > 0 {
+			return sum, errors.New(C.GoString(C.rs_strerror(C.RS_ERR_INVALID_ARG)))
+		}
+		copy(sum[:], h.Sum(nil))
+		return sum, nil
+	}
+	if len(shards) != config.K+config.M {
+		return sum, reedsolomon.ErrTooFewShards
+	}
+	var pin runtime.Pinner
+	defer pin.Unpin()
+	p, l, free := shardArgs(shards, &pin)
+	defer free()
+	d := (*[32]C.uint8_t)(C.malloc(32))
+	defer C.free(unsafe.Pointer(d))
+	if err = toErr(C.rs_co_encode_hash(s.co, p, l, C.size_t(valueLen), &d[0])); err != nil {
+		return sum, err
+	}
+	for i := range sum {
+		sum[i] = byte(d[i])
+	}
+	return sum, nil
 }
 
 // ReconstructMany repairs many objects in one call (batched healer repair,

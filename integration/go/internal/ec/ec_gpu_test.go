@@ -8,6 +8,7 @@ package ec
 
 import (
 	"bytes"
+	"crypto/sha256"
 	"math/rand"
 	"runtime"
 	"testing"
@@ -142,6 +143,32 @@ func TestSplitSpareCapacityMatchesKlauspost(t *testing.T) {
 				if !bytes.Equal(got[i], want[i]) {
 					t.Fatalf("n %d spare %d: parity shard %d differs", n, spare, i)
 				}
+			}
+		}
+	}
+}
+
+// EncodeHash = Encode + sha256.Sum256(value) (writeservice.go:222,267).
+func TestEncodeHashMatchesSha256(t *testing.T) {
+	ref, _ := reedsolomon.New(config.K, config.M)
+	svc := NewService().(*Service)
+	rng := rand.New(rand.NewSource(0x5EED0007))
+	for _, n := range []int{1, 2, 3, 63, 64, 65, 1000, 4096, 10*1024 + 7, 100 * 1024, 1500 * 1024} {
+		value := make([]byte, n)
+		rng.Read(value)
+		want, _ := ref.Split(append([]byte(nil), value...))
+		_ = ref.Encode(want)
+		got, _ := svc.Split(append([]byte(nil), value...))
+		sum, err := svc.EncodeHash(got, len(value))
+		if err != nil {
+			t.Fatal(err)
+		}
+		if sum != sha256.Sum256(value) {
+			t.Fatalf("len %d: cold_hash differs", n)
+		}
+		for i := range want {
+			if !bytes.Equal(got[i], want[i]) {
+				t.Fatalf("len %d: shard %d differs", n, i)
 			}
 		}
 	}

@@ -26,6 +26,7 @@ RS_ERR_INVALID_ARG = 16
 RS_ERR_NO_DEVICE = 17
 RS_ERR_DEVICE = 18
 RS_ERR_NOT_SUPPORTED = 19
+RS_ERR_BUSY = 20
 
 RS_MEM_DEVICE = 0
 RS_MEM_HOST = 1
@@ -77,6 +78,9 @@ SIGNATURES = {
     "rs_co_reconstruct_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_encode_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_encode_hash": (_i, [_vp, _u8pp, _szp, _sz, _u8p]),
+    "rs_co_submit_encode": (_i, [_vp, _u8pp, _szp, ctypes.c_uint64]),
+    "rs_co_submit_reconstruct": (_i, [_vp, _u8pp, _szp, ctypes.c_uint64]),
+    "rs_co_reap": (_i, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(_i), _i, _i]),
     "rs_co_encode_hash_many": (_i, [_vp, _sz, _u8pp, _szp, _szp, _u8p, ctypes.POINTER(_i)]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),

@@ -89,6 +89,18 @@ constexpr uint32_t kSlotPublished = 1;  // FillReq published, not yet staged
 constexpr uint32_t kSlotStaged = 2;     // staged by its caller
 constexpr uint32_t kSlotTaken = 3;      // staged by the launcher
 
+constexpr int kMaxAsyncOut = 16;  // m <= 16 (rs_create)
+
+// Where an asynchronous call's outputs go (its shard buffers, kept valid by the
+// caller until rs_co_reap reports its tag).
+struct AsyncRec {
+  uint64_t tag = 0;
+  uint32_t slot = 0;           // the call's slot in its batch
+  uint32_t n_out = 0;          // outputs: out slot r of the batch -> out[r]
+  uint8_t* out[kMaxAsyncOut] = {};
+  uint8_t* digest = nullptr;   // encode + hash: 32 bytes
+};
+
 struct Batch {
   int index = 0;               // position in rs_coalescer::batches (the hot-slot id)
   int engine = 0;              // the GPU (engine index in the context) this batch runs on
@@ -104,6 +116,12 @@ struct Batch {
   std::atomic<uint32_t> fill_err{0};   // a slot's plan could not be resolved (plan mode)
   std::atomic<uint32_t> max_missing{0};  // most shards any slot fills: the launch's erasure bound
   std::atomic<uint32_t> hash_in{0};      // some slot wants the SHA-256 of its value (cold_hash)
+  // asynchronous calls of the current run: their records, how many were made, how
+  // many have been handed to reapers (under rs_coalescer::done_mu)
+  std::unique_ptr<AsyncRec[]> arec;
+  size_t arec_cap = 0;
+  std::atomic<uint32_t> n_async{0};
+  uint32_t async_cursor = 0;
   size_t n_final = 0;          // slots of the closed batch (published by the group words)
   int rc = RS_OK;              // published by the group words
   Clock::time_point deadline;
@@ -254,6 +272,10 @@ struct rs_coalescer {
   std::map<std::pair<int, size_t>, Batch*> open;  // (kind, S) -> batch accepting slots (mu)
   std::atomic<uint64_t> hot{0};  // last opened batch: hot_word(gen, index); 0 = none
   std::vector<std::unique_ptr<Dispatcher>> disp;  // one per engine
+  // finished batches with asynchronous calls not yet reaped (rs_co_reap)
+  std::mutex done_mu;
+  std::condition_variable done_cv;
+  std::deque<Batch*> done;
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
   // diagnostics (printed at destroy when RS_CO_DEBUG is set)
@@ -329,6 +351,12 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->fill_err.store(0, std::memory_order_relaxed);
   b->max_missing.store(0, std::memory_order_relaxed);
   b->hash_in.store(0, std::memory_order_relaxed);
+  b->n_async.store(0, std::memory_order_relaxed);
+  b->async_cursor = 0;
+  if (b->arec_cap < cap) {  // the batch is free: nobody reads the old records
+    b->arec.reset(new AsyncRec[cap]);
+    b->arec_cap = cap;
+  }
   b->rc = RS_OK;
   b->free = false;
   b->deadline = Clock::now() + co->max_wait;
@@ -459,6 +487,11 @@ void complete(rs_coalescer* co, Dispatcher* d, Batch* b, int rc) {
   b->wake.store(static_cast<uint64_t>(epoch) << 32, std::memory_order_release);
   d->executing.fetch_sub(1, std::memory_order_acq_rel);
   poke(d);  // an execution slot is free: the next batch may start before the wake-ups
+  if (b->n_async.load(std::memory_order_relaxed)) {  // staged before the launch (acquired there)
+    std::lock_guard<std::mutex> g(co->done_mu);
+    co->done.push_back(b);
+    co->done_cv.notify_all();
+  }
   wake_more(b, epoch, 2);
 }
 
@@ -570,73 +603,88 @@ void completer_loop(rs_coalescer* co, Dispatcher* d) {
   }
 }
 
+// Reserves up to `want` consecutive slots of an open batch for (kind, S), opening
+// one if needed.  With every batch in flight a blocking caller waits for one to
+// free (back-pressure); a non-blocking one gets RS_ERR_BUSY.  Returns RS_OK with
+// *take >= 1 slots from *slot0 of *bp.
+int reserve_slots(rs_coalescer* co, Kind kind, size_t S, size_t want, bool block, Batch** bp, size_t* slot0,
+                  size_t* take) {
+  const auto key = std::make_pair(static_cast<int>(kind), S);
+  // fast path: the most recently opened batch, no mutex
+  if (const uint64_t h = co->hot.load(std::memory_order_acquire)) {
+    Batch* hb = co->batches[(h & 0xFFFF) - 1].get();
+    const uint32_t hg = static_cast<uint32_t>(h >> 16);
+    if (hb->key_kind.load(std::memory_order_relaxed) == key.first &&
+        hb->key_S.load(std::memory_order_relaxed) == key.second && (*take = try_reserve(hb, hg, want, slot0))) {
+      *bp = hb;
+      return RS_OK;
+    }
+  }
+  std::unique_lock<std::mutex> lk(co->mu);
+  for (;;) {
+    auto it = co->open.find(key);
+    if (it != co->open.end()) {
+      Batch* ob = it->second;
+      if ((*take = try_reserve(ob, ob->gen, want, slot0))) {
+        *bp = ob;
+        return RS_OK;
+      }
+      co->open.erase(it);  // closed or full: stop offering it
+      continue;
+    }
+    if (!co->free_list.empty()) {
+      // the free batch of the least-loaded engine (the most recently freed one
+      // among equals: its staging is warm)
+      size_t pick = co->free_list.size() - 1;
+      for (size_t i = co->free_list.size(); i-- > 0;)
+        if (co->engine_load[co->free_list[i]->engine] < co->engine_load[co->free_list[pick]->engine]) pick = i;
+      Batch* nb = co->free_list[pick];
+      co->free_list.erase(co->free_list.begin() + static_cast<std::ptrdiff_t>(pick));
+      const int rc = prepare(co, nb, kind, S);
+      if (rc) {
+        nb->free = true;
+        co->free_list.push_back(nb);
+        if (co->free_waiters) co->free_cv.notify_one();
+        return rc;
+      }
+      ++co->engine_load[nb->engine];
+      *take = try_reserve(nb, nb->gen, want, slot0);
+      *bp = nb;
+      co->open[key] = nb;
+      co->hot.store(hot_word(nb->gen, nb->index), std::memory_order_release);
+      return RS_OK;
+    }
+    if (!block) return RS_ERR_BUSY;
+    ++co->free_waiters;  // every batch is in flight: back-pressure
+    co->free_waits.fetch_add(1, std::memory_order_relaxed);
+    co->free_cv.wait(lk);
+    --co->free_waiters;
+  }
+}
+
+// `count` slots of batch b have been drained: the last one hands the batch back.
+void release_slots(rs_coalescer* co, Batch* b, size_t count) {
+  if (b->released.fetch_add(static_cast<uint32_t>(count), std::memory_order_acq_rel) + count == b->n_final) {
+    std::lock_guard<std::mutex> g(co->mu);
+    b->free = true;
+    --co->engine_load[b->engine];
+    co->free_list.push_back(b);
+    if (co->free_waiters) co->free_cv.notify_one();
+  }
+}
+
 // One call through the coalescer.  fill(b, slot, item) stages the inputs,
 // drain(b, slot, item) copies the outputs back; both run in the caller's thread,
 // outside any lock.
 template <class Fill, class Drain>
 int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity_in, Fill&& fill, Drain&& drain) {
-  const auto key = std::make_pair(static_cast<int>(kind), S);
   int result = RS_OK;
   size_t done_items = 0;
   while (done_items < count) {
-    const size_t want = count - done_items;
     Batch* b = nullptr;
-    uint32_t gen = 0;
     size_t slot0 = 0, take = 0;
-    // fast path: the most recently opened batch, no mutex
-    if (const uint64_t h = co->hot.load(std::memory_order_acquire)) {
-      Batch* hb = co->batches[(h & 0xFFFF) - 1].get();
-      const uint32_t hg = static_cast<uint32_t>(h >> 16);
-      if (hb->key_kind.load(std::memory_order_relaxed) == key.first &&
-          hb->key_S.load(std::memory_order_relaxed) == key.second && (take = try_reserve(hb, hg, want, &slot0))) {
-        b = hb;
-        gen = hg;
-      }
-    }
-    if (!b) {
-      std::unique_lock<std::mutex> lk(co->mu);
-      for (;;) {
-        auto it = co->open.find(key);
-        if (it != co->open.end()) {
-          Batch* ob = it->second;
-          if ((take = try_reserve(ob, ob->gen, want, &slot0))) {
-            b = ob;
-            gen = ob->gen;
-            break;
-          }
-          co->open.erase(it);  // closed or full: stop offering it
-          continue;
-        }
-        if (!co->free_list.empty()) {
-          // the free batch of the least-loaded engine (the most recently freed one
-          // among equals: its staging is warm)
-          size_t pick = co->free_list.size() - 1;
-          for (size_t i = co->free_list.size(); i-- > 0;)
-            if (co->engine_load[co->free_list[i]->engine] < co->engine_load[co->free_list[pick]->engine]) pick = i;
-          Batch* nb = co->free_list[pick];
-          co->free_list.erase(co->free_list.begin() + static_cast<std::ptrdiff_t>(pick));
-          const int rc = prepare(co, nb, kind, S);
-          if (rc) {
-            nb->free = true;
-            co->free_list.push_back(nb);
-            if (co->free_waiters) co->free_cv.notify_one();
-            return rc;
-          }
-          ++co->engine_load[nb->engine];
-          take = try_reserve(nb, nb->gen, want, &slot0);
-          b = nb;
-          gen = nb->gen;
-          co->open[key] = nb;
-          co->hot.store(hot_word(gen, nb->index), std::memory_order_release);
-          break;
-        }
-        ++co->free_waiters;  // every batch is in flight: back-pressure
-        co->free_waits.fetch_add(1, std::memory_order_relaxed);
-        co->free_cv.wait(lk);
-        --co->free_waiters;
-      }
-    }
-    (void)gen;
+    const int rrc = reserve_slots(co, kind, S, count - done_items, true, &b, &slot0, &take);
+    if (rrc) return rrc;
     // the epoch was set before the ticket opened (acquired by the reservation)
     const uint32_t epoch = b->epoch;
     const uint32_t grp = static_cast<uint32_t>(slot0 / Batch::kGroup);
@@ -662,22 +710,37 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
     wait_epoch(&b->grp[grp], epoch);
     wake_more(b, epoch, 2);
-    const int rc = b->rc;
-    const size_t n = b->n_final;  // published by the group word (release / acquire)
+    const int rc = b->rc;  // published by the group word (release / acquire), as n_final
     if (rc == RS_OK)
       for (size_t j = 0; j < take; ++j) drain(b, slot0 + j, done_items + j);
     else if (result == RS_OK)
       result = rc;
-    if (b->released.fetch_add(static_cast<uint32_t>(take), std::memory_order_acq_rel) + take == n) {
-      std::lock_guard<std::mutex> g(co->mu);
-      b->free = true;
-      --co->engine_load[b->engine];
-      co->free_list.push_back(b);
-      if (co->free_waiters) co->free_cv.notify_one();
-    }
+    release_slots(co, b, take);
     done_items += take;
   }
   return result;
+}
+
+// An asynchronous call (rs_co_submit_*): reserve one slot, stage it here, record
+// where its outputs go, and return without waiting -- rs_co_reap drains it once
+// its batch has run.  Never blocks: with every batch in flight RS_ERR_BUSY tells
+// the caller to reap first.  The slot's FillReq is never published (the caller
+// stages before it returns, so the launcher never runs a fill on its stack).
+template <class Fill>
+int submit_async(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& fill, const AsyncRec& rec) {
+  Batch* b = nullptr;
+  size_t slot = 0, take = 0;
+  const int rrc = reserve_slots(co, kind, S, 1, false, &b, &slot, &take);
+  if (rrc) return rrc;
+  co->calls.fetch_add(1, std::memory_order_relaxed);
+  if (parity_in) b->parity_in.store(1, std::memory_order_relaxed);
+  fill(b, slot);
+  const uint32_t ai = b->n_async.fetch_add(1, std::memory_order_relaxed);
+  b->arec[ai] = rec;
+  b->arec[ai].slot = static_cast<uint32_t>(slot);
+  b->filled.fetch_add(1, std::memory_order_release);  // publishes the slot and its record
+  poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
+  return RS_OK;
 }
 
 // One object (the per-call IEcDriver entry points).
@@ -937,6 +1000,88 @@ int rs_co_verify(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, i
   };
   auto drain = [&](Batch* b, size_t slot) { *ok = reinterpret_cast<uint32_t*>(host_at(b, b->o_bad))[slot] == 0; };
   return submit(co, Kind::kVerify, S, true, fill, drain);
+}
+
+// ---- asynchronous calls ----------------------------------------------------------
+int rs_co_submit_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, uint64_t tag) {
+  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+  const int k = co->k, m = co->m;
+  size_t S = 0;
+  int rc = rs::check_shards(k + m, lens, false, &S);
+  if (rc) return rc;
+  for (int i = 0; i < k + m; ++i)
+    if (!shards[i]) return RS_ERR_INVALID_ARG;
+  if (m == 0) return RS_ERR_NOT_SUPPORTED;  // nothing to compute, nothing would be reaped
+  if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
+  const uint32_t data_mask = (1u << k) - 1u;
+  AsyncRec rec;
+  rec.tag = tag;
+  rec.n_out = static_cast<uint32_t>(m);
+  for (int r = 0; r < m; ++r) rec.out[r] = shards[k + r];
+  auto fill = [&](Batch* b, size_t slot) {
+    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    set_hash(b, k, slot, rs::kSha256Skip);
+    if (co->per_stripe) {
+      reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+      note_missing(b, static_cast<uint32_t>(m));
+    } else {
+      set_plan(co, b, slot, data_mask, false, true);
+    }
+  };
+  return submit_async(co, Kind::kApply, S, false, fill, rec);
+}
+
+int rs_co_submit_reconstruct(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, uint64_t tag) {
+  if (!co || !shards || !lens) return RS_ERR_INVALID_ARG;
+  RecItem it;
+  bool need = false;
+  const int rc = rec_check(co, shards, const_cast<size_t*>(lens), false, &it, &need);
+  if (rc) return rc;
+  if (!need) return RS_ERR_NOT_SUPPORTED;  // nothing missing: nothing would be reaped
+  AsyncRec rec;
+  rec.tag = tag;
+  for (int i = 0; i < co->k + co->m; ++i)
+    if (!lens[i]) rec.out[rec.n_out++] = shards[i];
+  return submit_async(
+      co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it, false); }, rec);
+}
+
+int rs_co_reap(rs_coalescer* co, uint64_t* tags, int* rcs, int max, int timeout_us) {
+  if (!co || !tags || !rcs || max <= 0) return -RS_ERR_INVALID_ARG;
+  const int m = co->m;
+  int got = 0;
+  std::unique_lock<std::mutex> lk(co->done_mu);
+  for (;;) {
+    while (got < max && !co->done.empty()) {
+      Batch* b = co->done.front();
+      const uint32_t na = b->n_async.load(std::memory_order_relaxed);
+      const uint32_t c0 = b->async_cursor;
+      const uint32_t take = std::min<uint32_t>(static_cast<uint32_t>(max - got), na - c0);
+      b->async_cursor += take;
+      if (b->async_cursor == na) co->done.pop_front();
+      lk.unlock();
+      const int brc = b->rc;
+      for (uint32_t j = c0; j < c0 + take; ++j) {
+        const AsyncRec& r = b->arec[j];
+        if (brc == RS_OK) {
+          for (uint32_t o = 0; o < r.n_out; ++o)
+            std::memcpy(r.out[o], host_at(b, b->o_out + (static_cast<size_t>(r.slot) * m + o) * b->P), b->S);
+        }
+        tags[got] = r.tag;
+        rcs[got] = brc;
+        ++got;
+      }
+      release_slots(co, b, take);
+      lk.lock();
+    }
+    if (got > 0 || timeout_us == 0 || co->stop.load(std::memory_order_acquire)) return got;
+    if (timeout_us < 0) {
+      co->done_cv.wait(lk);
+    } else if (co->done_cv.wait_for(lk, std::chrono::microseconds(timeout_us)) == std::cv_status::timeout &&
+               co->done.empty()) {
+      return 0;
+    }
+  }
 }
 
 // Batched healer repair: the objects a scan found damaged

@@ -1154,6 +1154,7 @@ const char* rs_strerror(int code) {
     case RS_ERR_NO_DEVICE: return "rsgpu: no usable GPU device";
     case RS_ERR_DEVICE: return "rsgpu: HIP runtime error";
     case RS_ERR_NOT_SUPPORTED: return "operation not supported";
+    case RS_ERR_BUSY: return "rsgpu: coalescer busy, reap completed calls and retry";
     default: return "rsgpu: unknown error";
   }
 }

@@ -75,6 +75,21 @@ def all_true(flag: bool) -> bool:
     return bool(t.item())
 
 
+def distinct_count(key: int) -> int:
+    """How many distinct values of `key` the ranks hold (e.g. how many physical GPUs
+    a run used: ranks may share one when rehearsing the N > 1 path)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return 1
+    ws = dist.get_world_size()
+    t = torch.tensor([key], dtype=torch.int64, device=_device())
+    out = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return len({int(x.item()) for x in out})
+
+
 def shutdown() -> None:
     import torch.distributed as dist
 

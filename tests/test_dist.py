@@ -52,8 +52,10 @@ def _worker(rank, ws, port, outdir):
     d.barrier()
     t = d.max_over_ranks(float(rank + 1))
     ok = d.all_true(rank != 1)
+    same = d.distinct_count(7)          # both ranks "on one device"
+    both = d.distinct_count(100 + rank)  # one device each
     with open(os.path.join(outdir, f"ctl{rank}.txt"), "w") as f:
-        f.write(f"{t} {int(ok)} {b} {e}\n")
+        f.write(f"{t} {int(ok)} {b} {e} {same} {both}\n")
     d.shutdown()
 
 
@@ -71,6 +73,7 @@ def test_two_rank_gloo_sharded_encode(tmp_path):
     parts = [np.load(tmp_path / f"part{r}.npy") for r in range(ws)]
     assert np.array_equal(np.concatenate(parts), ref)
     for r in range(ws):
-        t, ok, b, e = open(tmp_path / f"ctl{r}.txt").read().split()
+        t, ok, b, e, same, both = open(tmp_path / f"ctl{r}.txt").read().split()
         assert float(t) == 2.0  # max over ranks
         assert ok == "0"        # rank 1 reported a failure -> AND is false everywhere
+        assert (same, both) == ("1", "2")  # bench.py's physical_gpus count

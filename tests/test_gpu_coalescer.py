@@ -333,7 +333,8 @@ def test_encode_hash_matches_hashlib_and_oracle(gpu, k, m, staged_dma):
                 assert rs_oracle.encode(k, m, ref) == 0
                 if j % 3 == 2:  # a plain encode / a repair in the same batches
                     svc.Encode(shards)
-                    got = [None if i == int(rng.integers(0, k + m)) else bytearray(s) for i, s in enumerate(shards)]
+                    gone = int(rng.integers(0, k + m))
+                    got = [None if i == gone else bytearray(s) for i, s in enumerate(shards)]
                     svc.Reconstruct(got)
                     assert [bytes(s) for s in got] == [bytes(s) for s in ref]
                     continue
@@ -358,5 +359,83 @@ def test_encode_hash_matches_hashlib_and_oracle(gpu, k, m, staged_dma):
         sh = svc.Split(b"abc" * 100)
         with pytest.raises(ECError):
             svc.EncodeHash(sh, k * len(sh[0]) + 1)
+    finally:
+        svc.close()
+
+
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (17, 3)])
+def test_async_submit_reap_matches_oracle(gpu, k, m):
+    """rs_co_submit_encode / rs_co_submit_reconstruct / rs_co_reap: many calls in
+    flight from few threads (how an event loop or the Go runtime multiplexes
+    request goroutines), every output checked against the oracle once reaped;
+    RS_ERR_BUSY when all staging batches hold unreaped calls, after which reaping
+    and resubmitting goes on; rejected calls are never reaped."""
+    import ctypes
+
+    from replication_erasurecoding_object_store_amd import _lib
+    from replication_erasurecoding_object_store_amd.ec import _shard_array
+
+    L = _lib.lib()
+    svc = CoalescingService(k, m, max_batch=32, inflight=3)
+    try:
+        t = k + m
+        rng = np.random.default_rng(k * 100 + m)
+        pending = {}  # tag -> (kind, shards, expected, keepalive)
+        done = 0
+        busy = 0
+        tags = (ctypes.c_uint64 * 64)()
+        rcs = (ctypes.c_int * 64)()
+
+        def reap(timeout):
+            nonlocal done
+            n = L.rs_co_reap(svc._co, tags, rcs, 64, timeout)
+            assert n >= 0
+            for i in range(n):
+                kind, sh, exp, keep = pending.pop(tags[i])
+                assert rcs[i] == _lib.RS_OK
+                assert [bytes(x) for x in sh] == exp, (kind, tags[i])
+                done += 1
+            return n
+
+        for tag in range(400):
+            length = [4096, 1000, 65536 + 5, 3][tag % 4]
+            data = xoshiro_bytes(9000 + tag, length)
+            ref = rs_oracle.split(k, m, data)
+            assert rs_oracle.encode(k, m, ref) == 0
+            exp = [bytes(x) for x in ref]
+            sh = svc.Split(data)
+            lost = []
+            if tag % 2 == 0:
+                kind = "encode"
+                for j in range(k, t):
+                    sh[j][:] = b"\x5a" * len(sh[j])
+            else:
+                kind = "reconstruct"
+                sh = [bytearray(x) for x in ref]
+                lost = [int(j) for j in rng.choice(t, size=int(rng.integers(1, m + 1)), replace=False)]
+                for j in lost:
+                    sh[j][:] = b"\x00" * len(sh[j])  # storage stays; len 0 marks it missing
+            S = len(sh[0])
+            ptrs, lens, keep = _shard_array(sh, S, fill_missing=False)
+            for j in lost:
+                lens[j] = 0
+            fn = L.rs_co_submit_encode if kind == "encode" else L.rs_co_submit_reconstruct
+            while True:
+                rc = fn(svc._co, ptrs, lens, tag)
+                if rc != _lib.RS_ERR_BUSY:
+                    break
+                busy += 1
+                reap(-1)
+            assert rc == _lib.RS_OK, rc
+            pending[tag] = (kind, sh, exp, (ptrs, lens, keep))
+        while pending:
+            reap(-1)
+        assert done > 300 and busy > 0, (done, busy)
+        # a rejected call (shard sizes differ) returns its code and is never reaped
+        sh = svc.Split(b"x" * 100)
+        sh[1] = bytearray(len(sh[1]) + 1)
+        ptrs, lens, keep = _shard_array(sh, 0, fill_missing=False)
+        assert L.rs_co_submit_encode(svc._co, ptrs, lens, 7) == _lib.RS_ERR_SHARD_SIZE
+        assert L.rs_co_reap(svc._co, tags, rcs, 64, 0) == 0
     finally:
         svc.close()

@@ -237,6 +237,30 @@ def test_deferred_errors_are_per_stream(gpu):
         eng.close()
 
 
+def _hip_streams(n):
+    """n distinct raw HIP streams (torch.cuda.Stream() hands out a small pool of
+    reused handles), as torch ExternalStreams, and a destroyer."""
+    import ctypes
+    import importlib.util
+    import os
+
+    import torch
+
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(importlib.util.find_spec("torch").origin), "lib",
+                                   "libamdhip64.so"))
+    handles = []
+    for _ in range(n):
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        handles.append(h)
+
+    def destroy():
+        for h in handles:
+            hip.hipStreamDestroy(h)
+
+    return [torch.cuda.ExternalStream(h.value) for h in handles], destroy
+
+
 def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
     """More streams than one status chunk (1 024 words): every stream keeps its own
     deferred-error word (streams past the 1 023rd shared the last word),
@@ -246,6 +270,8 @@ def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
     k, m, S, N = 4, 2, 256, 8
     P = shard_pitch_for(S)
     eng = BatchEngine(k, m, 0)
+    streams, destroy = _hip_streams(1100)
+    fresh, destroy2 = [], None
     try:
         d = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda")
         p = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
@@ -254,7 +280,7 @@ def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
         bad = good.clone()
         bad[3] = 0b000011
         torch.cuda.synchronize()
-        streams = [torch.cuda.Stream() for _ in range(1100)]
+        assert len({s.cuda_stream for s in streams}) == 1100
         for i, s in enumerate(streams):  # every 7th stream gets an invalid mask
             eng.reconstruct_devmask(d, p, S, N, bad if i % 7 == 0 else good, stream=s)
         for i, s in enumerate(streams):
@@ -264,11 +290,11 @@ def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
             else:
                 eng.sync(stream=s)
         # release half of them with an error pending: the words come back zeroed
-        for i, s in enumerate(streams[:550]):
+        for s in streams[:550]:
             eng.reconstruct_devmask(d, p, S, N, bad, stream=s)
             with pytest.raises(ECError):
                 eng.stream_release(stream=s)
-        fresh = [torch.cuda.Stream() for _ in range(550)]  # reuse the released words
+        fresh, destroy2 = _hip_streams(550)  # their words are the released ones
         for s in fresh:
             eng.reconstruct_devmask(d, p, S, N, good, stream=s)
         for s in fresh:
@@ -277,6 +303,10 @@ def test_deferred_errors_per_stream_beyond_1024_streams(gpu):
         for s in streams[550:]:
             eng.stream_release(stream=s)
     finally:
+        torch.cuda.synchronize()
+        destroy()
+        if destroy2:
+            destroy2()
         eng.close()
 
 

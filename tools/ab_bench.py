@@ -44,6 +44,8 @@ WORKLOADS = {
     "rs84_64K_rec2pb_out": (8, 4, 8192, 16384, "rec2pb_out"),
     "rs84_64K_rec1p_out": (8, 4, 8192, 16384, "rec1p_out"),
     "rs42_4K_rec04u_out": (4, 2, 1024, 65536, "rec04u_out"),
+    "rs42_4K_rec1pb_out": (4, 2, 1024, 65536, "rec1pb_out"),
+    "rs42_64K_rec1pb_out": (4, 2, 16384, 16384, "rec1pb_out"),
     "rs42_4K_rec45u_out": (4, 2, 1024, 65536, "rec45u_out"),
     "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
     "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),

@@ -14,7 +14,10 @@
 //          -Lreplication_erasurecoding_object_store_amd -lrsgpu \
 //          -Wl,-rpath,$PWD/replication_erasurecoding_object_store_amd -Loracle -lrs_oracle \
 //          -Wl,-rpath,$PWD/oracle -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib
-// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co|cpu> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight]
+// "async": the coalescer's asynchronous calls (rs_co_submit_* / rs_co_reap), each
+// thread an event loop with `depth` calls in flight (the Go shim's model: request
+// goroutines park on a channel while one poller reaps).
+// Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co|cpu|async> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight] [depth]
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -38,6 +41,7 @@ int main(int argc, char** argv) {
   const bool mix = std::strcmp(argv[3], "mix") == 0;
   const bool co_mode = std::strcmp(argv[4], "co") == 0;
   const bool cpu_mode = std::strcmp(argv[4], "cpu") == 0;
+  const bool async_mode = std::strcmp(argv[4], "async") == 0;  // coalescer, rs_co_submit_* + rs_co_reap
   rs_coalescer_opts opts{0, 0, 0, 0, 0, 0};
   if (argc > 5) opts.max_batch = std::strtoull(argv[5], nullptr, 10);
   if (argc > 6) opts.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
@@ -52,7 +56,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   rs_coalescer* co = nullptr;
-  if (co_mode && rs_coalescer_create(ctx, &opts, &co)) return 1;
+  if ((co_mode || async_mode) && rs_coalescer_create(ctx, &opts, &co)) return 1;
   const size_t S = rs_shard_size(ctx, obj);
   // CPU codec plans: encode rows, and per lost shard the composed decode row over
   // the first k survivors (klauspost caches decode matrices per erasure pattern)
@@ -71,57 +75,132 @@ int main(int argc, char** argv) {
       rec_plan[lost] = rso_baseline_plan_new(k, nmiss, rows.data());
     }
   }
+  const int depth = argc > 11 ? std::atoi(argv[11]) : 64;  // async: calls in flight per thread
   std::atomic<bool> stop{false}, start{false};
-  std::atomic<uint64_t> ops{0}, bad{0};
+  std::atomic<uint64_t> ops{0}, bad{0}, busy{0};
   std::vector<std::thread> ts;
+  // One object's k+m shards; the reference parity comes from a direct call, and
+  // before every call the shards it must write are scribbled, so a call that writes
+  // nothing cannot pass.
+  struct Obj {
+    std::vector<std::vector<uint8_t>> sh, keep;
+    std::vector<uint8_t*> p;
+    std::vector<size_t> n;
+    uint64_t j = 0;
+  };
+  auto make_obj = [&](uint64_t seed) {
+    Obj o;
+    o.sh.assign(k + m, std::vector<uint8_t>(S));
+    uint64_t x = 0x9E3779B97F4A7C15ull * (seed + 1);
+    for (int i = 0; i < k; ++i)
+      for (auto& b : o.sh[i]) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        b = static_cast<uint8_t>(x);
+      }
+    o.p.resize(k + m);
+    o.n.assign(k + m, S);
+    for (int i = 0; i < k + m; ++i) o.p[i] = o.sh[i].data();
+    if (rs_encode(ctx, o.p.data(), o.n.data()) != RS_OK) ++bad;
+    o.keep = o.sh;
+    return o;
+  };
+  // Call j of an object: every 7th pair (an encode and a reconstruct
+  // each) scribbles the shards it must write and is checked byte-for-byte after;
+  // the others rewrite identical bytes unchecked (a full compare of every call
+  // would cost as much CPU as the codec itself at large objects).
+  auto verified = [&](const Obj& o) { return (o.j >> 1) % 7 == 0; };  // 7: every lost index in turn
+  // prepares call j: returns the lost shard (-1: encode), lens set
+  auto prep = [&](Obj& o) -> int {
+    o.n.assign(k + m, S);
+    const bool v = verified(o);
+    if (mix && (o.j & 1)) {
+      const int lost = static_cast<int>((o.j >> 1) % (k + m));
+      o.n[lost] = 0;
+      if (v) std::memset(o.sh[lost].data(), 0x5a, S);
+      return lost;
+    }
+    if (v)
+      for (int r = 0; r < m; ++r) std::memset(o.sh[k + r].data(), 0x5a, S);
+    return -1;
+  };
+  auto check = [&](Obj& o) -> uint64_t {
+    uint64_t e = 0;
+    if (verified(o))
+      for (int i = 0; i < k + m; ++i)
+        if (std::memcmp(o.sh[i].data(), o.keep[i].data(), S) != 0) {
+          ++e;
+          std::memcpy(o.sh[i].data(), o.keep[i].data(), S);
+        }
+    ++o.j;
+    return e;
+  };
   for (int t = 0; t < T; ++t)
     ts.emplace_back([&, t] {
-      std::vector<std::vector<uint8_t>> sh(k + m, std::vector<uint8_t>(S));
-      uint64_t x = 0x9E3779B97F4A7C15ull * (t + 1);
-      for (int i = 0; i < k; ++i)
-        for (auto& b : sh[i]) {
-          x ^= x << 13;
-          x ^= x >> 7;
-          x ^= x << 17;
-          b = static_cast<uint8_t>(x);
+      if (async_mode) {  // an event loop: `depth` calls in flight, reaped in bulk
+        std::vector<Obj> objs;
+        for (int d = 0; d < depth; ++d) objs.push_back(make_obj(static_cast<uint64_t>(t) * depth + d));
+        std::vector<int> idle;
+        for (int d = depth - 1; d >= 0; --d) idle.push_back(d);
+        std::vector<uint64_t> tags(depth);
+        std::vector<int> rcs(depth);
+        while (!start.load()) std::this_thread::yield();
+        uint64_t mine = 0, nb = 0, e = 0, inflight = 0;
+        while (!stop.load(std::memory_order_relaxed) || inflight) {
+          while (!idle.empty() && !stop.load(std::memory_order_relaxed)) {
+            const int d = idle.back();
+            Obj& o = objs[d];
+            const int lost = prep(o);
+            const int rc = lost < 0 ? rs_co_submit_encode(co, o.p.data(), o.n.data(), d)
+                                    : rs_co_submit_reconstruct(co, o.p.data(), o.n.data(), d);
+            if (rc == RS_ERR_BUSY) {
+              ++nb;
+              break;
+            }
+            if (rc != RS_OK) ++e;
+            idle.pop_back();
+            ++inflight;
+          }
+          if (!inflight) continue;
+          const int got = rs_co_reap(co, tags.data(), rcs.data(), depth, -1);
+          for (int g = 0; g < got; ++g) {
+            Obj& o = objs[static_cast<size_t>(tags[g])];
+            if (rcs[g] != RS_OK) ++e;
+            e += check(o);
+            idle.push_back(static_cast<int>(tags[g]));
+            --inflight;
+            ++mine;
+          }
         }
-      std::vector<uint8_t*> p(k + m);
-      std::vector<size_t> n(k + m, S);
-      for (int i = 0; i < k + m; ++i) p[i] = sh[i].data();
-      // reference parity from a direct call; every later call must reproduce all
-      // k+m shards byte for byte (data is never changed, so parity is constant)
-      if (rs_encode(ctx, p.data(), n.data()) != RS_OK) ++bad;
-      const std::vector<std::vector<uint8_t>> keep = sh;
+        ops += mine;
+        bad += e;
+        busy += nb;
+        return;
+      }
+      Obj o = make_obj(static_cast<uint64_t>(t));
       while (!start.load()) std::this_thread::yield();
-      uint64_t j = 0, mine = 0;
+      uint64_t mine = 0;
       while (!stop.load(std::memory_order_relaxed)) {
         int rc;
-        if (mix && (j & 1)) {
-          const int lost = static_cast<int>((j >> 1) % (k + m));
-          n.assign(k + m, S);
-          n[lost] = 0;
+        const int lost = prep(o);
+        if (lost >= 0) {
           if (cpu_mode) {
             const uint8_t* in[32];
-            for (int c = 0; c < k; ++c) in[c] = p[rec_in[lost][c]];
-            uint8_t* out[1] = {p[lost]};
+            for (int c = 0; c < k; ++c) in[c] = o.p[rec_in[lost][c]];
+            uint8_t* out[1] = {o.p[lost]};
             rc = rso_baseline_plan_apply(rec_plan[lost], in, out, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
           } else {
-            rc = co ? rs_co_reconstruct(co, p.data(), n.data()) : rs_reconstruct(ctx, p.data(), n.data());
+            rc = co ? rs_co_reconstruct(co, o.p.data(), o.n.data()) : rs_reconstruct(ctx, o.p.data(), o.n.data());
           }
         } else {
-          n.assign(k + m, S);
           if (cpu_mode)
-            rc = rso_baseline_plan_apply(enc_plan, p.data(), p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
+            rc = rso_baseline_plan_apply(enc_plan, o.p.data(), o.p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
           else
-            rc = co ? rs_co_encode(co, p.data(), n.data()) : rs_encode(ctx, p.data(), n.data());
+            rc = co ? rs_co_encode(co, o.p.data(), o.n.data()) : rs_encode(ctx, o.p.data(), o.n.data());
         }
         if (rc != RS_OK) ++bad;
-        for (int i = 0; i < k + m; ++i)
-          if (std::memcmp(sh[i].data(), keep[i].data(), S) != 0) {
-            ++bad;
-            std::memcpy(sh[i].data(), keep[i].data(), S);
-          }
-        ++j;
+        bad += check(o);
         ++mine;
       }
       ops += mine;
@@ -138,11 +217,13 @@ int main(int argc, char** argv) {
   std::printf(
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
-      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d}\n",
-      co ? "coalesced" : (cpu_mode ? "cpu" : "direct"), mix ? "mix" : "enc", T, obj, dt, n_ops / dt,
-      n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
+      "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d, "
+      "\"depth\": %d, \"busy\": %llu}\n",
+      async_mode ? "async" : (co ? "coalesced" : (cpu_mode ? "cpu" : "direct")), mix ? "mix" : "enc", T, obj, dt,
+      n_ops / dt, n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
-      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight);
+      static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
+      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()));
   if (co) rs_coalescer_destroy(co);
   if (enc_plan) rso_baseline_plan_free(enc_plan);
   for (void* pl : rec_plan)
