@@ -531,7 +531,7 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes):
     def put(name, ms, e):
         sec = ms * 1e-3
         res[name] = {"user_GiBps": round(N * k * S / sec / GiB, 1),
-                     "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4)}
+                     "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4), "kernel": eng.last_kernel()}
 
     put("rec1_per_stripe_out", sustained_kernel_ms(torch, lambda i: eng.reconstruct_out(
         split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one, max_missing=1))[0], 1)

@@ -31,6 +31,7 @@
 // over every GPU while a lone caller still sees one batch at a time.
 #include <hip/hip_runtime.h>
 #include <linux/futex.h>
+#include <sched.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -197,14 +198,32 @@ void advance_epoch(std::atomic<uint32_t>* w, uint32_t epoch) {
   }
 }
 
-// Waits until *w reaches `epoch`: a brief spin, then sleeps (callers may far
-// outnumber cores, so spinning long would steal the CPU the stragglers need to
-// stage their shards).
-void wait_epoch(std::atomic<uint32_t>* w, uint32_t epoch) {
-  for (int i = 0; i < 64; ++i) {
-    if (epoch_reached(w->load(std::memory_order_acquire), epoch)) return;
-    __builtin_ia32_pause();
+// Waits until *w reaches `epoch`.  A caller holding one of the `spin_slots`
+// spins (a batch turns around in tens of microseconds; a futex sleep and wake-up
+// costs a context switch each way); the others -- callers may far outnumber cores,
+// and spinning would steal the CPU the stragglers need to stage their shards --
+// sleep after a brief spin.
+void wait_epoch(std::atomic<uint32_t>* w, uint32_t epoch, std::atomic<int>* spinners, int spin_slots) {
+  if (spinners->fetch_add(1, std::memory_order_acq_rel) < spin_slots) {
+    const auto t0 = Clock::now();
+    for (uint32_t i = 0;; ++i) {
+      if (epoch_reached(w->load(std::memory_order_acquire), epoch)) {
+        spinners->fetch_sub(1, std::memory_order_acq_rel);
+        return;
+      }
+      __builtin_ia32_pause();
+      if ((i & 255u) == 255u && Clock::now() - t0 > std::chrono::microseconds(200)) break;
+    }
+  } else {
+    for (int i = 0; i < 64; ++i) {
+      if (epoch_reached(w->load(std::memory_order_acquire), epoch)) {
+        spinners->fetch_sub(1, std::memory_order_acq_rel);
+        return;
+      }
+      __builtin_ia32_pause();
+    }
   }
+  spinners->fetch_sub(1, std::memory_order_acq_rel);
   for (;;) {
     const uint32_t v = w->load(std::memory_order_acquire);
     if (epoch_reached(v, epoch)) return;
@@ -248,6 +267,26 @@ void poke(Dispatcher* d, bool from_caller = false) {
     futex_wake(&d->work, 1);
 }
 
+// CPUs this process may run on: the cgroup v2 quota (cpu.max "quota period") when
+// one is set, else the affinity mask (a container's quota is usually far below the
+// host CPUs its mask shows).
+int usable_cpus() {
+  int n = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const long long quota = std::atoll(q);
+      const int qc = static_cast<int>(std::max(1LL, quota / period));
+      if (n <= 0 || qc < n) n = qc;
+    }
+    std::fclose(f);
+  }
+  return n > 0 ? n : 1;
+}
+
 }  // namespace
 
 struct rs_coalescer {
@@ -261,6 +300,11 @@ struct rs_coalescer {
 
   int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
+  // callers that may spin-wait for their batch at once: the CPUs this process may
+  // use (its cgroup quota, else its affinity mask) minus room for the launcher,
+  // completer and staging threads
+  int spin_slots = 0;
+  std::atomic<int> spinners{0};
   std::atomic<bool> stop{false};
 
   std::mutex mu;
@@ -708,7 +752,7 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
     }
     if (staged) b->filled.fetch_add(staged, std::memory_order_release);
     poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
-    wait_epoch(&b->grp[grp], epoch);
+    wait_epoch(&b->grp[grp], epoch, &co->spinners, co->spin_slots);
     wake_more(b, epoch, 2);
     const int rc = b->rc;  // published by the group word (release / acquire), as n_final
     if (rc == RS_OK)
@@ -889,6 +933,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
+  co->spin_slots = std::max(0, usable_cpus() - 2 - 2 * ne);
   co->engine_load.assign(static_cast<size_t>(ne), 0);
   // the most slots a batch can hold: max_batch, bounded by the bytes budget at
   // the smallest slot (16-B shards) and by 2^20

@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -78,6 +79,8 @@ int main(int argc, char** argv) {
   const int depth = argc > 11 ? std::atoi(argv[11]) : 64;  // async: calls in flight per thread
   std::atomic<bool> stop{false}, start{false};
   std::atomic<uint64_t> ops{0}, bad{0}, busy{0};
+  std::unique_ptr<std::atomic<int>[]> done_word(new std::atomic<int>[static_cast<size_t>(T) * depth]);
+  for (size_t i = 0; i < static_cast<size_t>(T) * depth; ++i) done_word[i].store(0);
   std::vector<std::thread> ts;
   // One object's k+m shards; the reference parity comes from a direct call, and
   // before every call the shards it must write are scribbled, so a call that writes
@@ -138,13 +141,18 @@ int main(int argc, char** argv) {
   };
   for (int t = 0; t < T; ++t)
     ts.emplace_back([&, t] {
-      if (async_mode) {  // an event loop: `depth` calls in flight, reaped in bulk
+      if (async_mode) {
+        // An event loop with `depth` calls in flight.  Reaping is global (any thread
+        // may reap any call, as the Go shim's single reaper goroutine does), so a
+        // reaped tag = (thread << 32 | object) is routed to its owner through a
+        // completion word; each loop then handles its own completed objects.
         std::vector<Obj> objs;
         for (int d = 0; d < depth; ++d) objs.push_back(make_obj(static_cast<uint64_t>(t) * depth + d));
         std::vector<int> idle;
         for (int d = depth - 1; d >= 0; --d) idle.push_back(d);
-        std::vector<uint64_t> tags(depth);
-        std::vector<int> rcs(depth);
+        std::vector<uint64_t> tags(256);
+        std::vector<int> rcs(256);
+        std::atomic<int>* mine_done = &done_word[static_cast<size_t>(t) * depth];
         while (!start.load()) std::this_thread::yield();
         uint64_t mine = 0, nb = 0, e = 0, inflight = 0;
         while (!stop.load(std::memory_order_relaxed) || inflight) {
@@ -152,23 +160,32 @@ int main(int argc, char** argv) {
             const int d = idle.back();
             Obj& o = objs[d];
             const int lost = prep(o);
-            const int rc = lost < 0 ? rs_co_submit_encode(co, o.p.data(), o.n.data(), d)
-                                    : rs_co_submit_reconstruct(co, o.p.data(), o.n.data(), d);
+            const uint64_t tag = (static_cast<uint64_t>(t) << 32) | static_cast<uint64_t>(d);
+            const int rc = lost < 0 ? rs_co_submit_encode(co, o.p.data(), o.n.data(), tag)
+                                    : rs_co_submit_reconstruct(co, o.p.data(), o.n.data(), tag);
             if (rc == RS_ERR_BUSY) {
               ++nb;
               break;
             }
-            if (rc != RS_OK) ++e;
+            if (rc != RS_OK) {
+              ++e;
+              break;
+            }
             idle.pop_back();
             ++inflight;
           }
           if (!inflight) continue;
-          const int got = rs_co_reap(co, tags.data(), rcs.data(), depth, -1);
-          for (int g = 0; g < got; ++g) {
-            Obj& o = objs[static_cast<size_t>(tags[g])];
-            if (rcs[g] != RS_OK) ++e;
-            e += check(o);
-            idle.push_back(static_cast<int>(tags[g]));
+          const int got = rs_co_reap(co, tags.data(), rcs.data(), 256, 50);
+          for (int g = 0; g < got; ++g)
+            done_word[(tags[g] >> 32) * static_cast<uint64_t>(depth) + (tags[g] & 0xFFFFFFFFu)].store(
+                rcs[g] + 1, std::memory_order_release);
+          for (int d = 0; d < depth; ++d) {
+            const int v = mine_done[d].load(std::memory_order_acquire);
+            if (!v) continue;
+            mine_done[d].store(0, std::memory_order_relaxed);
+            if (v - 1 != RS_OK) ++e;
+            e += check(objs[d]);
+            idle.push_back(d);
             --inflight;
             ++mine;
           }

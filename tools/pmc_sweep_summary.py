@@ -6,6 +6,7 @@ tools/prof_summary.py) against the workload's algorithmic bytes (tools/ab_bench.
 Usage: python tools/pmc_sweep_summary.py gpurun_out/pmc_<tag> <tag>
 """
 import csv
+import json
 import os
 import statistics
 import sys
@@ -35,6 +36,7 @@ def main():
              "FETCH_SIZE x 1024 x 2, WRITE_SIZE x 1024 (MI355X_MICROARCH.md §HBM).", "",
              "| workload | kernel | n | avg us | alg MB | fetch MB | write MB | HBM / alg | alg GB/s | % of 8 TB/s |",
              "|---|---|---|---|---|---|---|---|---|---|"]
+    table = {}
     for w in sorted(os.listdir(src)):
         d = os.path.join(src, w)
         tr = os.path.join(d, "trace", "run_kernel_trace.csv")
@@ -64,9 +66,14 @@ def main():
         short = name.replace("void ", "").split("(")[0]
         lines.append(f"| {w} | `{short}` | {len(ds)} | {avg / 1e3:.1f} | {alg / 1e6:.1f} | {fb / 1e6:.1f} | "
                      f"{wb / 1e6:.1f} | {(fb + wb) / alg:.3f} | {alg / avg:.0f} | {alg / avg / 80:.1f} |")
+        table[w] = {"kernel": short, "dispatches": len(ds), "avg_ns": avg, "alg_bytes": alg,
+                    "hbm_bytes": (fb + wb) if f is not None and wr is not None else None,
+                    "hbm_frac": alg / avg / 8000.0}
     out = os.path.join(root, "profiles", f"{tag}_kmsweep_pmc.md")
     with open(out, "w") as fo:
         fo.write("\n".join(lines) + "\n")
+    with open(os.path.join(root, "profiles", f"{tag}_kmsweep_pmc.json"), "w") as fo:
+        json.dump({"tag": tag, "workloads": table}, fo, indent=1)
     print("\n".join(lines))
 
 

@@ -22,7 +22,7 @@ Q=$(awk '{if ($1 != "max") print int($1 / $2)}' /sys/fs/cgroup/cpu.max 2>/dev/nu
 Q=${Q:-16}
 PIN="taskset -c 0-$((Q - 1))"
 for OBJ in ${SIZES:-4096 10240 102400 819200 1536000}; do
-  run taskset -c 0 $B 1 $SECS mix cpu 0 0 $OBJ
+  run $B 1 $SECS mix cpu 0 0 $OBJ
   run $PIN $B $Q $SECS mix cpu 0 0 $OBJ
   for T in ${CALLERS:-16 64 256}; do
     run $PIN $B $T $SECS mix co 0 0 $OBJ
