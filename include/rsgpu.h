@@ -216,6 +216,9 @@ typedef struct {
   int max_exec;           /* batches executing at once (0 = 2; <= inflight) */
   int staged_dma;         /* 0: kernels read/write the pinned staging in place (zero-copy);
                              1: H2D / D2H copies around the kernel */
+  int spin_waiters;       /* callers that may spin-wait for their batch at once instead of
+                             sleeping on a futex: 0 = none (default), > 0 = that many, capped
+                             at the CPUs this process may use minus the coalescer's threads */
 } rs_coalescer_opts;
 int rs_coalescer_create(rs_ctx *ctx, const rs_coalescer_opts *opts /* NULL = defaults */,
                         rs_coalescer **out);

@@ -199,10 +199,9 @@ void advance_epoch(std::atomic<uint32_t>* w, uint32_t epoch) {
 }
 
 // Waits until *w reaches `epoch`.  A caller holding one of the `spin_slots`
-// spins (a batch turns around in tens of microseconds; a futex sleep and wake-up
-// costs a context switch each way); the others -- callers may far outnumber cores,
-// and spinning would steal the CPU the stragglers need to stage their shards --
-// sleep after a brief spin.
+// (rs_coalescer_opts.spin_waiters, default none) spins for up to 200 us before it
+// sleeps; the others sleep after a brief spin (callers may far outnumber cores, and
+// spinning steals the CPU the launcher, the completer and straggling callers need).
 void wait_epoch(std::atomic<uint32_t>* w, uint32_t epoch, std::atomic<int>* spinners, int spin_slots) {
   if (spinners->fetch_add(1, std::memory_order_acq_rel) < spin_slots) {
     const auto t0 = Clock::now();
@@ -300,9 +299,8 @@ struct rs_coalescer {
 
   int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
-  // callers that may spin-wait for their batch at once: the CPUs this process may
-  // use (its cgroup quota, else its affinity mask) minus room for the launcher,
-  // completer and staging threads
+  // callers that may spin-wait for their batch at once (opts.spin_waiters, capped at
+  // the CPUs this process may use minus the launcher and completer threads)
   int spin_slots = 0;
   std::atomic<int> spinners{0};
   std::atomic<bool> stop{false};
@@ -913,7 +911,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   if (!ctx || !out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
   const int ne = rs::ctx_engine_count(ctx);
-  rs_coalescer_opts o{4096, 0, std::max(16, 8 * ne), size_t(32) << 20, 2, 0};
+  rs_coalescer_opts o{4096, 0, std::max(16, 8 * ne), size_t(32) << 20, 2, 0, 0};
   if (opts) {
     if (opts->max_batch) o.max_batch = opts->max_batch;
     o.max_wait_us = opts->max_wait_us;
@@ -921,8 +919,9 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
     if (opts->max_batch_bytes) o.max_batch_bytes = opts->max_batch_bytes;
     if (opts->max_exec > 0) o.max_exec = opts->max_exec;
     o.staged_dma = opts->staged_dma;
+    o.spin_waiters = opts->spin_waiters;
   }
-  if (o.inflight > 256 || o.max_exec > o.inflight || o.inflight < ne) return RS_ERR_INVALID_ARG;
+  if (o.inflight > 256 || o.max_exec > o.inflight || o.inflight < ne || o.spin_waiters < 0) return RS_ERR_INVALID_ARG;
   auto co = std::make_unique<rs_coalescer>();
   co->ctx = ctx;
   co->k = rs_data_shards(ctx);
@@ -933,7 +932,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
-  co->spin_slots = std::max(0, usable_cpus() - 2 - 2 * ne);
+  co->spin_slots = std::min(o.spin_waiters, std::max(0, usable_cpus() - 2 - 2 * ne));
   co->engine_load.assign(static_cast<size_t>(ne), 0);
   // the most slots a batch can hold: max_batch, bounded by the bytes budget at
   // the smallest slot (16-B shards) and by 2^20

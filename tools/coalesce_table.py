@@ -1,0 +1,43 @@
+"""Markdown table of tools/run_coalesce_sizes.sh output: per object size, user
+GiB/s (and calls/s) of the CPU codec on 1 core and on the CPU quota, the coalesced
+GPU drop-in with blocking callers and with asynchronous calls.
+
+Usage: python tools/coalesce_table.py <run_coalesce_sizes log>
+"""
+import json
+import sys
+from collections import defaultdict
+
+
+def main():
+    rows = defaultdict(dict)
+    cols = []
+    for line in open(sys.argv[1]):
+        if not line.startswith("{"):
+            continue
+        r = json.loads(line)
+        mode = r["mode"]
+        if mode == "cpu":
+            key = f"CPU codec, {r['threads']} thread{'s' if r['threads'] > 1 else ''}"
+        elif mode == "coalesced":
+            key = f"GPU coalesced, {r['threads']} blocking callers"
+        elif mode == "async":
+            key = f"GPU async, {r['threads']} loops x {r['depth']} in flight"
+        else:
+            key = f"{mode} {r['threads']}"
+        if key not in cols:
+            cols.append(key)
+        rows[r["obj_bytes"]][key] = (r["user_GiBps"], r["calls_per_s"])
+    print("| object | " + " | ".join(cols) + " |")
+    print("|---|" + "---|" * len(cols))
+    for obj in sorted(rows):
+        cells = []
+        for c in cols:
+            v = rows[obj].get(c)
+            cells.append(f"{v[0]:.1f} GiB/s ({v[1] / 1e3:.0f} K/s)" if v else "")
+        size = f"{obj // 1024} KiB" if obj % 1024 == 0 else f"{obj / 1024:.0f} KiB"
+        print(f"| {size} | " + " | ".join(cells) + " |")
+
+
+if __name__ == "__main__":
+    main()
