@@ -56,6 +56,14 @@ WORKLOADS = {
     "rs104_S6656_rec1p_out": (10, 4, 6656, 16384, "rec1p_out"),
     "rs104_S6656_rec2p_out": (10, 4, 6656, 16384, "rec2p_out"),
     "rs104_S6144_enc": (10, 4, 6144, 16384, "enc"),
+    # RS(10+4) bounded per-stripe reconstruct at whole-task shard lengths (stripe-aligned
+    # apply_kernel: 384 / 512 columns) and a tail-free flat one (416 columns)
+    "rs104_S6144_rec1pb_out": (10, 4, 6144, 16384, "rec1pb_out"),
+    "rs104_S6144_rec2pb_out": (10, 4, 6144, 16384, "rec2pb_out"),
+    "rs104_S8192_rec1pb_out": (10, 4, 8192, 16384, "rec1pb_out"),
+    "rs104_S8192_rec2pb_out": (10, 4, 8192, 16384, "rec2pb_out"),
+    "rs104_S6656_rec1pb_out": (10, 4, 6656, 16384, "rec1pb_out"),
+    "rs104_S6656_rec2pb_out": (10, 4, 6656, 16384, "rec2pb_out"),
     # diagnostics: plan working set (one pattern for every stripe vs random), E
     "rs104_64K_rec01p_out": (10, 4, 6554, 16384, "rec01p_out"),    # devmask, all stripes miss {0,1}
     "rs104_64K_rec2u_out": (10, 4, 6554, 16384, "rec2u_out"),      # uniform host mask {0,1}

@@ -45,6 +45,7 @@ int main(int argc, char** argv) {
   const bool async_mode = std::strcmp(argv[4], "async") == 0;  // coalescer, rs_co_submit_* + rs_co_reap
   rs_coalescer_opts opts{0, 0, 0, 0, 0, 0, 0};
   if (const char* sw = std::getenv("SPIN")) opts.spin_waiters = std::atoi(sw);  // callers spin-waiting at once
+  if (const char* mb = std::getenv("BATCH_MB")) opts.max_batch_bytes = std::strtoull(mb, nullptr, 10) << 20;
   if (argc > 5) opts.max_batch = std::strtoull(argv[5], nullptr, 10);
   if (argc > 6) opts.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
   const size_t obj = argc > 7 ? std::strtoull(argv[7], nullptr, 10) : 4096;
