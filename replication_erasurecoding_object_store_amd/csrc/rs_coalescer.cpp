@@ -537,77 +537,111 @@ void complete(rs_coalescer* co, Dispatcher* d, Batch* b, int rc) {
   wake_more(b, epoch, 2);
 }
 
-// Waits until all n reserved slots of a closed batch are staged.  After a short
-// spin, slots whose callers published their FillReq but have not staged yet (a
-// descheduled caller, common with callers far outnumbering cores) are staged here;
-// only a caller preempted between its reservation and publishing (a few
-// instructions) is waited for.  Then the slot states are reset for the next run.
-void stage_stragglers(Batch* b, size_t n) {
-  for (int spin = 0; spin < 2048 && b->filled.load(std::memory_order_acquire) < n; ++spin) __builtin_ia32_pause();
-  while (b->filled.load(std::memory_order_acquire) < n) {
-    for (size_t s = 0; s < n; ++s) {
-      uint32_t st = b->slot_state[s].load(std::memory_order_acquire);
-      if (st != kSlotPublished) continue;
-      const FillReq* r = b->slot_req[s].load(std::memory_order_relaxed);
-      if (!b->slot_state[s].compare_exchange_strong(st, kSlotTaken, std::memory_order_acq_rel)) continue;
-      r->fn(r->ctx, b, s, r->item0 + (s - r->slot0));
-      b->filled.fetch_add(1, std::memory_order_release);
-    }
-    if (b->filled.load(std::memory_order_acquire) < n) std::this_thread::yield();
+// One pass over a closed batch's n slots: stages the slots whose callers published
+// their FillReq but have not started staging (a descheduled caller, common with
+// callers far outnumbering cores).  Slots a caller is copying are left to it.
+void stage_published(Batch* b, size_t n) {
+  for (size_t s = 0; s < n; ++s) {
+    uint32_t st = b->slot_state[s].load(std::memory_order_acquire);
+    if (st != kSlotPublished) continue;
+    const FillReq* r = b->slot_req[s].load(std::memory_order_relaxed);
+    if (!b->slot_state[s].compare_exchange_strong(st, kSlotTaken, std::memory_order_acq_rel)) continue;
+    r->fn(r->ctx, b, s, r->item0 + (s - r->slot0));
+    b->filled.fetch_add(1, std::memory_order_release);
   }
-  for (size_t s = 0; s < n; ++s) b->slot_state[s].store(kSlotReserved, std::memory_order_relaxed);
 }
 
-// Launcher: batching is group commit -- an open batch starts as soon as fewer than
-// max_exec batches of this GPU are executing and max_wait has passed since it
-// opened (default 0), or at once when full.  Callers arriving meanwhile pile into
-// it, so batches grow with the load and a lone caller waits for no timer.
+// A closed batch waiting for its callers' staging copies before it may launch.
+struct Closing {
+  Batch* b;
+  size_t n;
+  Clock::time_point closed;
+};
+
+// How long the launcher lets a closed batch's callers finish their own staging
+// copies before it stages published slots itself.
+constexpr auto kStraggleGrace = std::chrono::microseconds(100);
+
+// Launcher: batching is group commit -- an open batch closes when full, or when
+// max_wait has passed since it opened (default 0) and the device has room for it;
+// callers arriving meanwhile pile into it, so batches grow with the load and a lone
+// caller waits for no timer.  A closed batch launches once every reserved slot is
+// staged and fewer than max_exec batches of this GPU are executing.  Round 3: the
+// launcher no longer waits on a closed batch's staging copies before it can look
+// at other batches -- with 1.5 MB objects those copies took 41 % of its time while
+// the device idled between batches (RS_CO_DEBUG straggle_ms).  The last caller to
+// stage into a closed batch always wakes the launcher.
 void launcher_loop(rs_coalescer* co, Dispatcher* d) {
+  std::vector<Closing> closing;
   for (;;) {
     const uint32_t w = d->work.load(std::memory_order_acquire);
     if (co->stop.load(std::memory_order_acquire)) return;
-    Batch* pick = nullptr;
+    const auto now = Clock::now();
     Clock::time_point wake_at = Clock::time_point::max();
-    const bool slot = d->executing.load(std::memory_order_acquire) < co->max_exec;
+    // 1. launch fully staged closed batches, oldest first, while the device has room
+    for (size_t i = 0; i < closing.size() && d->executing.load(std::memory_order_acquire) < co->max_exec;) {
+      Closing& c = closing[i];
+      if (c.b->filled.load(std::memory_order_acquire) < c.n && now - c.closed >= kStraggleGrace) {
+        const auto ts0 = Clock::now();
+        stage_published(c.b, c.n);
+        co->straggle_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - ts0).count(),
+                                  std::memory_order_relaxed);
+      }
+      if (c.b->filled.load(std::memory_order_acquire) < c.n) {
+        // before the grace ends: wake then to stage published slots; after it, the
+        // slots left are being copied by their callers, and the last one wakes us
+        if (now - c.closed < kStraggleGrace) wake_at = std::min(wake_at, c.closed + kStraggleGrace);
+        ++i;
+        continue;
+      }
+      Batch* b = c.b;
+      const size_t n = c.n;
+      closing.erase(closing.begin() + static_cast<std::ptrdiff_t>(i));
+      for (size_t s = 0; s < n; ++s) b->slot_state[s].store(kSlotReserved, std::memory_order_relaxed);
+      b->n_final = n;
+      d->executing.fetch_add(1, std::memory_order_acq_rel);
+      const auto tl0 = Clock::now();
+      const int rc = launch_batch(co, b, n);
+      co->launch_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count(),
+                              std::memory_order_relaxed);
+      if (rc) {
+        complete(co, d, b, rc);
+        continue;
+      }
+      std::lock_guard<std::mutex> g(d->run_mu);
+      d->running.push_back(b);
+      d->run_cv.notify_one();
+    }
+    // 2. close open batches: a full one at once (it cannot grow), one past its
+    // linger only if the device would have room for it next to the closed ones
+    const int busy = d->executing.load(std::memory_order_acquire) + static_cast<int>(closing.size());
+    const bool slot = busy < co->max_exec;
+    Batch* pick = nullptr;
     for (Batch* b : d->mine) {
       const uint64_t t = b->ticket.load(std::memory_order_acquire);
       const size_t cnt = static_cast<size_t>(t & kCountMask);
       if ((t & kClosedBit) || cnt == 0) continue;  // free, closed, or nobody in it yet
       const bool full = cnt >= b->cap.load(std::memory_order_relaxed);
-      if (full || (slot && Clock::now() >= b->deadline)) {
+      if (full || (slot && now >= b->deadline)) {
         if (!pick || full) pick = b;
         if (full) break;
       } else if (slot) {
         wake_at = std::min(wake_at, b->deadline);
       }
     }
-    if (pick && (slot || d->executing.load(std::memory_order_acquire) < co->max_exec)) {
+    if (pick) {
       const uint64_t t = pick->ticket.fetch_or(kClosedBit, std::memory_order_acq_rel);
-      const size_t n = static_cast<size_t>(t & kCountMask);
       {
         std::lock_guard<std::mutex> g(co->mu);
         unpublish(co, pick, static_cast<uint32_t>(t >> kGenShift));
       }
-      const auto ts0 = Clock::now();
-      stage_stragglers(pick, n);
-      co->straggle_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - ts0).count(),
-                                std::memory_order_relaxed);
-      pick->n_final = n;
-      d->executing.fetch_add(1, std::memory_order_acq_rel);
-      const auto tl0 = Clock::now();
-      const int rc = launch_batch(co, pick, n);
-      co->launch_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count(),
-                              std::memory_order_relaxed);
-      if (rc) {
-        complete(co, d, pick, rc);
-        continue;
-      }
-      std::lock_guard<std::mutex> g(d->run_mu);
-      d->running.push_back(pick);
-      d->run_cv.notify_one();
-      continue;
+      closing.push_back(Closing{pick, static_cast<size_t>(t & kCountMask), Clock::now()});
+      continue;  // its callers may all have staged already
     }
-    // nothing to start: sleep until a caller stages, a slot frees or a linger ends
+    // nothing to do now: sleep until a caller stages, a slot frees, a linger or a
+    // straggler grace ends.  A staging caller wakes the launcher only if that can
+    // start something (a free slot for an open batch); the last stager of a closed
+    // batch and completions always wake it.
     d->launcher_wants_callers.store(slot, std::memory_order_seq_cst);
     d->launcher_idle.store(true, std::memory_order_seq_cst);
     if (d->work.load(std::memory_order_seq_cst) == w && !co->stop.load(std::memory_order_acquire)) {
@@ -748,8 +782,13 @@ int submit_many(rs_coalescer* co, Kind kind, size_t S, size_t count, bool parity
       fill(b, slot0 + j, done_items + j);
       if (b->slot_state[slot0 + j].compare_exchange_strong(st, kSlotStaged, std::memory_order_acq_rel)) ++staged;
     }
-    if (staged) b->filled.fetch_add(staged, std::memory_order_release);
-    poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
+    bool last = false;  // this caller completed the staging of a closed batch
+    if (staged) {
+      const size_t filled = b->filled.fetch_add(staged, std::memory_order_acq_rel) + staged;
+      const uint64_t t = b->ticket.load(std::memory_order_acquire);
+      last = (t & kClosedBit) && filled >= static_cast<size_t>(t & kCountMask);
+    }
+    poke(co->disp[static_cast<size_t>(b->engine)].get(), !last);
     wait_epoch(&b->grp[grp], epoch, &co->spinners, co->spin_slots);
     wake_more(b, epoch, 2);
     const int rc = b->rc;  // published by the group word (release / acquire), as n_final
@@ -780,8 +819,9 @@ int submit_async(rs_coalescer* co, Kind kind, size_t S, bool parity_in, Fill&& f
   const uint32_t ai = b->n_async.fetch_add(1, std::memory_order_relaxed);
   b->arec[ai] = rec;
   b->arec[ai].slot = static_cast<uint32_t>(slot);
-  b->filled.fetch_add(1, std::memory_order_release);  // publishes the slot and its record
-  poke(co->disp[static_cast<size_t>(b->engine)].get(), true);
+  const size_t filled = b->filled.fetch_add(1, std::memory_order_acq_rel) + 1;  // publishes the slot and its record
+  const uint64_t t = b->ticket.load(std::memory_order_acquire);
+  poke(co->disp[static_cast<size_t>(b->engine)].get(), !((t & kClosedBit) && filled >= (t & kCountMask)));
   return RS_OK;
 }
 

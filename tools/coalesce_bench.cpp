@@ -17,6 +17,9 @@
 // "async": the coalescer's asynchronous calls (rs_co_submit_* / rs_co_reap), each
 // thread an event loop with `depth` calls in flight (the Go shim's model: request
 // goroutines park on a channel while one poller reaps).
+// ROTATE_MB=<n>: each blocking thread cycles through its share of n MiB of objects
+// (DRAM-resident calls, as objects fresh off the network or a disk are) instead of
+// re-using one cache-resident object.
 // Usage: coalesce_bench <threads> <seconds> <enc|mix> <direct|co|cpu|async> [max_batch] [max_wait_us] [obj_bytes] [max_exec] [staged_dma] [inflight] [depth]
 #include <atomic>
 #include <chrono>
@@ -79,6 +82,7 @@ int main(int argc, char** argv) {
     }
   }
   const int depth = argc > 11 ? std::atoi(argv[11]) : 64;  // async: calls in flight per thread
+  const size_t rotate_bytes = std::getenv("ROTATE_MB") ? std::strtoull(std::getenv("ROTATE_MB"), nullptr, 10) << 20 : 0;
   std::atomic<bool> stop{false}, start{false};
   std::atomic<uint64_t> ops{0}, bad{0}, busy{0};
   std::unique_ptr<std::atomic<int>[]> done_word(new std::atomic<int>[static_cast<size_t>(T) * depth]);
@@ -197,10 +201,18 @@ int main(int argc, char** argv) {
         busy += nb;
         return;
       }
-      Obj o = make_obj(static_cast<uint64_t>(t));
+      // ROTATE_MB: the thread cycles through its share of that many MiB of objects,
+      // so calls find their object in DRAM instead of the cache (1 GiB >> the host's
+      // 256 MiB of L3); default one object, cache-resident after the first call
+      const size_t npool = std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
+      std::vector<Obj> pool;
+      for (size_t i = 0; i < npool; ++i) pool.push_back(make_obj(static_cast<uint64_t>(t) * npool + i));
+      size_t cur = 0;
       while (!start.load()) std::this_thread::yield();
       uint64_t mine = 0;
       while (!stop.load(std::memory_order_relaxed)) {
+        Obj& o = pool[cur];
+        cur = cur + 1 == npool ? 0 : cur + 1;
         int rc;
         const int lost = prep(o);
         if (lost >= 0) {
@@ -237,12 +249,12 @@ int main(int argc, char** argv) {
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
       "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d, "
-      "\"depth\": %d, \"busy\": %llu}\n",
+      "\"depth\": %d, \"busy\": %llu, \"rotate_mb\": %zu}\n",
       async_mode ? "async" : (co ? "coalesced" : (cpu_mode ? "cpu" : "direct")), mix ? "mix" : "enc", T, obj, dt,
       n_ops / dt, n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
-      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()));
+      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20);
   if (co) rs_coalescer_destroy(co);
   if (enc_plan) rso_baseline_plan_free(enc_plan);
   for (void* pl : rec_plan)

@@ -20,9 +20,14 @@ run() {
 SECS=${SECS:-2}
 Q=$(awk '{if ($1 != "max") print int($1 / $2)}' /sys/fs/cgroup/cpu.max 2>/dev/null || true)
 Q=${Q:-16}
-PIN="taskset -c 0-$((Q - 1))"
+# the quota's worth of cores on the GPU's NUMA node (where the pinned staging lives;
+# node-0 cores run the large objects 17-21 % slower, profiles/r03h_coalesce_numa.log)
+CPUS=$(tools/gpu_local_cpus.sh $Q)
+PIN="taskset -c $CPUS"
+ONE="taskset -c ${CPUS%%-*}"
+echo "# callers on cpus $CPUS" >&2
 for OBJ in ${SIZES:-4096 10240 102400 819200 1536000}; do
-  run $B 1 $SECS mix cpu 0 0 $OBJ
+  run $ONE $B 1 $SECS mix cpu 0 0 $OBJ
   run $PIN $B $Q $SECS mix cpu 0 0 $OBJ
   for T in ${CALLERS:-16 64 256}; do
     run $PIN $B $T $SECS mix co 0 0 $OBJ
