@@ -84,6 +84,7 @@ int main(int argc, char** argv) {
   const int depth = argc > 11 ? std::atoi(argv[11]) : 64;  // async: calls in flight per thread
   const size_t rotate_bytes = std::getenv("ROTATE_MB") ? std::strtoull(std::getenv("ROTATE_MB"), nullptr, 10) << 20 : 0;
   std::atomic<bool> stop{false}, start{false};
+  std::atomic<int> ready{0};  // threads done building their objects: the clock starts after all
   std::atomic<uint64_t> ops{0}, bad{0}, busy{0};
   std::unique_ptr<std::atomic<int>[]> done_word(new std::atomic<int>[static_cast<size_t>(T) * depth]);
   for (size_t i = 0; i < static_cast<size_t>(T) * depth; ++i) done_word[i].store(0);
@@ -159,6 +160,7 @@ int main(int argc, char** argv) {
         std::vector<uint64_t> tags(256);
         std::vector<int> rcs(256);
         std::atomic<int>* mine_done = &done_word[static_cast<size_t>(t) * depth];
+        ++ready;
         while (!start.load()) std::this_thread::yield();
         uint64_t mine = 0, nb = 0, e = 0, inflight = 0;
         while (!stop.load(std::memory_order_relaxed) || inflight) {
@@ -208,6 +210,7 @@ int main(int argc, char** argv) {
       std::vector<Obj> pool;
       for (size_t i = 0; i < npool; ++i) pool.push_back(make_obj(static_cast<uint64_t>(t) * npool + i));
       size_t cur = 0;
+      ++ready;
       while (!start.load()) std::this_thread::yield();
       uint64_t mine = 0;
       while (!stop.load(std::memory_order_relaxed)) {
@@ -236,6 +239,7 @@ int main(int argc, char** argv) {
       }
       ops += mine;
     });
+  while (ready.load() < T) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   start = true;
   const auto t0 = std::chrono::steady_clock::now();
   std::this_thread::sleep_for(std::chrono::duration<double>(secs));
