@@ -128,63 +128,83 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(uint8_t* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, 0x7FFFFFFF, 0x00020000);
 }
 
-// 16-B non-temporal store at base + off, or nothing at all when !live: a raw buffer
+// Cache policy of the output stores (the aux / cpol operand of the buffer store).
+// gfx950: bit 1 = NT (streaming), bit 4 = SC1 (device scope: the store writes
+// through the XCD's L2).  Measured by read:write mix (profiles/r03l_ab_store_*.log,
+// interleaved A/B, >= 100 ms per kernel): a launch that reads K >= 8 inputs per
+// output row it writes (1-erasure reconstruct of RS(8+4) / RS(10+4)) streams fastest
+// with device-scope write-through stores (RS(8+4) 72.0 -> 76.7 %, RS(10+4) 65.3 ->
+// 69.1 % of 8 TB/s); RS(10+4) with two rows per stripe with NT + SC1 (68.6 -> 70.0 %);
+// every other mix (RS(4+2), RS(8+4) 2-erasure, encodes) with NT alone, as before
+// (SC1 there costs 1.5-8 points).
+constexpr int kCpolNt = 2;
+constexpr int kCpolSc1 = 16;
+template <int K, int E>
+constexpr int out_cpol() {
+  return (E == 1 && K >= 8) ? kCpolSc1 : (E == 2 && K >= 10) ? (kCpolSc1 | kCpolNt) : kCpolNt;
+}
+
+// 16-B store at base + off, or nothing at all when !live: a raw buffer
 // store whose offset then fails the range check, so the hardware drops it -- no
 // branch around the store and no sink line to write back.  off < 2 GiB.
+template <int CPOL = kCpolNt>
 __device__ __forceinline__ void store16_or_drop(uint8_t* base, uint32_t off, bool live, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc(base), live ? off : kDropOffset, 0, 2 /* nt */);
+  __builtin_amdgcn_raw_buffer_store_b128(v, out_rsrc(base), live ? off : kDropOffset, 0, CPOL);
 }
 
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // The first nb (1..15, wave-uniform) bytes of v at base + off in at most four
 // naturally aligned buffer stores (8, 4, 2, 1 B), landing only for `live` lanes.
+// Same cache policy as the kernel's full-column stores (one line may get both).
+template <int CPOL = kCpolNt>
 __device__ __forceinline__ void store_part_or_drop(uint8_t* base, uint32_t off, bool live, u32x4 v, uint32_t nb) {
   const auto rsrc = out_rsrc(base);
   const uint32_t o = live ? off : kDropOffset;
   uint32_t q = 0;  // bytes stored so far
   if (nb & 8u) {
-    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, rsrc, o, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, rsrc, o, 0, CPOL);
     q = 8;
   }
   uint32_t w = q ? v[2] : v[0];  // dword holding byte q
   if (nb & 4u) {
-    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), rsrc, live ? off + q : kDropOffset, 0, CPOL);
     q += 4;
     w = q == 12u ? v[3] : v[1];
   }
   if (nb & 2u) {
-    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), rsrc, live ? off + q : kDropOffset, 0, CPOL);
     q += 2;
     w >>= 16;
   }
   if (nb & 1u)
-    __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), rsrc, live ? off + q : kDropOffset, 0, 2);
+    __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), rsrc, live ? off + q : kDropOffset, 0, CPOL);
 }
 
 // The first nb (1..15, wave-uniform) bytes of v at voff (+ soff) of descriptor r in at
 // most four naturally aligned buffer stores, landing only for `live` lanes (the
 // range check applies to voff: a dropped lane's offset is kDropOffset).
+template <int CPOL = kCpolNt>
 __device__ __forceinline__ void store_part_rsrc(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, bool live,
                                                 u32x4 v, uint32_t nb) {
   const uint32_t o = live ? voff : kDropOffset;
   uint32_t q = 0;  // bytes stored so far
   if (nb & 8u) {
-    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, r, o, soff, 2);
+    __builtin_amdgcn_raw_buffer_store_b64(i32x2{static_cast<int>(v[0]), static_cast<int>(v[1])}, r, o, soff, CPOL);
     q = 8;
   }
   uint32_t w = q ? v[2] : v[0];  // dword holding byte q
   if (nb & 4u) {
-    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), r, live ? voff + q : kDropOffset, soff, 2);
+    __builtin_amdgcn_raw_buffer_store_b32(static_cast<int>(w), r, live ? voff + q : kDropOffset, soff, CPOL);
     q += 4;
     w = q == 12u ? v[3] : v[1];
   }
   if (nb & 2u) {
-    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), r, live ? voff + q : kDropOffset, soff, 2);
+    __builtin_amdgcn_raw_buffer_store_b16(static_cast<short>(w), r, live ? voff + q : kDropOffset, soff, CPOL);
     q += 2;
     w >>= 16;
   }
-  if (nb & 1u) __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), r, live ? voff + q : kDropOffset, soff, 2);
+  if (nb & 1u) __builtin_amdgcn_raw_buffer_store_b8(static_cast<char>(w), r, live ? voff + q : kDropOffset, soff, CPOL);
 }
 
 // Shard slot s of stripe i (s < k: data region, else parity region).
@@ -389,14 +409,14 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t n_out = PER_STRIPE ? pv.n_out() : u_nout;
 #pragma unroll
     for (int r = 0; r < E; ++r)
-      store16_or_drop(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
-                      full && static_cast<uint32_t>(r) < n_out, y[r]);
+      store16_or_drop<out_cpol<K, E>()>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                                        full && static_cast<uint32_t>(r) < n_out, y[r]);
     if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
       const bool part = col == a.full_cols;
 #pragma unroll
       for (int r = 0; r < E; ++r)
-        store_part_or_drop(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
-                           part && static_cast<uint32_t>(r) < n_out, y[r], nb);
+        store_part_or_drop<out_cpol<K, E>()>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                                             part && static_cast<uint32_t>(r) < n_out, y[r], nb);
     }
   }
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, bad);
@@ -859,14 +879,15 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
     const uint32_t nl = inB ? nB : nA;
     const bool fullc = live && colr < a.full_cols;
+    const bool part = nb != 0u && live && colr == a.full_cols;
 #pragma unroll
     for (int r = 0; r < E; ++r)
       __builtin_amdgcn_raw_buffer_store_b128(y[r], oout, fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
-                                             r * pitch, 2 /* nt */);
-    const bool part = nb != 0u && live && colr == a.full_cols;
+                                             r * pitch, out_cpol<K, E>());
     if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
 #pragma unroll
-      for (int r = 0; r < E; ++r) store_part_rsrc(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, y[r], nb);
+      for (int r = 0; r < E; ++r)
+        store_part_rsrc<out_cpol<K, E>()>(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, y[r], nb);
     }
     c0 += step_c;
     s0 += step_s;

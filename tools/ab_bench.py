@@ -64,6 +64,10 @@ WORKLOADS = {
     "rs104_S8192_rec2pb_out": (10, 4, 8192, 16384, "rec2pb_out"),
     "rs104_S6656_rec1pb_out": (10, 4, 6656, 16384, "rec1pb_out"),
     "rs104_S6656_rec2pb_out": (10, 4, 6656, 16384, "rec2pb_out"),
+    # one erasure pattern for every stripe through the device-mask E = 1 kernel
+    # (no straddling task selects between two plans): data shard 0 / parity shard 13
+    "rs104_64K_rec1d0b_out": (10, 4, 6554, 16384, "rec1d0b_out"),
+    "rs104_64K_rec1p13b_out": (10, 4, 6554, 16384, "rec1p13b_out"),
     # diagnostics: plan working set (one pattern for every stripe vs random), E
     "rs104_64K_rec01p_out": (10, 4, 6554, 16384, "rec01p_out"),    # devmask, all stripes miss {0,1}
     "rs104_64K_rec2u_out": (10, 4, 6554, 16384, "rec2u_out"),      # uniform host mask {0,1}
@@ -77,7 +81,8 @@ WORKLOADS = {
 def alg_bytes(name):
     """Algorithmic HBM bytes of one launch of workload `name`."""
     k, m, S, N, mode = WORKLOADS[name]
-    e = {"enc": m, "ver": m, "encu_out": m, "rec1p_out": 1, "rec1pb_out": 1, "rec4p_out": min(4, m)}.get(mode, 2)
+    e = {"enc": m, "ver": m, "encu_out": m, "rec1p_out": 1, "rec1pb_out": 1, "rec1d0b_out": 1, "rec1p13b_out": 1,
+         "rec4p_out": min(4, m)}.get(mode, 2)
     return N * S * (k + e)
 
 
@@ -139,6 +144,8 @@ def main():
         masks4 = torch.from_numpy(four.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
+        md0 = torch.full((N,), ((1 << t) - 1) & ~1, dtype=torch.int32, device="cuda")
+        mp13 = torch.full((N,), ((1 << t) - 1) & ~(1 << (t - 1)), dtype=torch.int32, device="cuda")
         outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
         alg = alg_bytes(name.split("+")[0])
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
@@ -161,6 +168,10 @@ def main():
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks1)
             elif mode == "rec1pb_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks1, max_missing=1)
+            elif mode == "rec1d0b_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=md0, max_missing=1)
+            elif mode == "rec1p13b_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=mp13, max_missing=1)
             elif mode == "rec2pb_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb], max_missing=2)
             elif mode == "rec04u_out":
