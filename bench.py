@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--sustained-ms", type=float, default=150.0,
                    help="also time >= this many ms of steps (extras.sustained); 0 = off")
     p.add_argument("--no-extras", action="store_true")
+    p.add_argument("--sweep-only", action="store_true",
+                   help="only the K/M sweep and config 3's patterns (for tools/profile_sweep.sh: one process whose "
+                        "kernel trace holds exactly the windows the bench times)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--json-out", default="")
@@ -214,6 +217,10 @@ def sustained_kernel_ms(torch, fn, min_ms=100.0):
     launches), the same window tools/profile_kmsweep_pmc.sh profiles."""
     est = kernel_ms_events(torch, fn, 3)
     reps = max(10, int(np.ceil(min_ms / max(est, 1e-3))))
+    # a 3 ms idle gap before the timed pass marks its window in a kernel trace of this
+    # process (tools/sweep_trace_summary.py matches it by kernel name and reps + 2)
+    torch.cuda.synchronize()
+    time.sleep(0.003)
     return kernel_ms_events(torch, fn, reps), reps
 
 
@@ -528,18 +535,20 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes):
     dev_one = torch.from_numpy(one.astype(np.uint32).view(np.int32)).cuda()
     res = {}
 
-    def put(name, ms, e):
+    def put(name, timed, e):
+        ms, reps = timed
         sec = ms * 1e-3
         res[name] = {"user_GiBps": round(N * k * S / sec / GiB, 1),
-                     "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4), "kernel": eng.last_kernel()}
+                     "hbm_frac": round(N * S * (k + e) / sec / 1e9 / HBM_PEAK_GBS, 4), "kernel": eng.last_kernel(),
+                     "launches": reps}
 
     put("rec1_per_stripe_out", sustained_kernel_ms(torch, lambda i: eng.reconstruct_out(
-        split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one, max_missing=1))[0], 1)
+        split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, masks_dev=dev_one, max_missing=1)), 1)
     for name, pat in (("rec_0_1_uniform_out", (0, 1)), ("rec_0_4_uniform_out", (0, 4)),
                       ("rec_4_5_uniform_out", (4, 5))):
         mask = full & ~sum(1 << j for j in pat)
         put(name, sustained_kernel_ms(torch, lambda i: eng.reconstruct_out(
-            split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, present_masks=mask))[0], 2)
+            split[i % nb][0], split[i % nb][1], split[i % nb][2], S, N, present_masks=mask)), 2)
     del split
     torch.cuda.empty_cache()
     # SoA: shard s of every stripe in one plane
@@ -547,7 +556,7 @@ def layout_and_patterns(torch, eng, k, m, S, N, rotate_bytes):
             torch.empty((m, N, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
     put("soa_encode", sustained_kernel_ms(torch, lambda i: eng.encode(soa[i % nb][0], soa[i % nb][1], S, N,
                                                                       shard_pitch=N * P, data_stripe_pitch=P,
-                                                                      parity_stripe_pitch=P))[0], m)
+                                                                      parity_stripe_pitch=P)), m)
     del soa
     torch.cuda.empty_cache()
     return res
@@ -631,6 +640,19 @@ def main():
     N = args.stripes
     eng = BatchEngine(k, m, torch.cuda.current_device())
     rotate = int(args.rotate_gib * GiB)
+    if args.sweep_only:
+        res = {"kmsweep_64KiB_device": kmsweep(torch, rdist, rotate)}
+        if world == 1:
+            res["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
+        if rank == 0:
+            line = json.dumps(res)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+        eng.close()
+        rdist.shutdown()
+        return
 
     # weak scaling: every rank owns its own N-stripe batches (independent objects)
     w = RSWorkload(torch, eng, k, m, S, N, rotate, seed=0x5EED0002 + rank)
