@@ -165,3 +165,47 @@ def test_devmask_bound_flags_and_skips_excess(engines, k, m, S, bound):
     # the bound is checked against the out layout and m
     with pytest.raises(ECError):
         eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=-1)
+
+
+# Sporadic-corruption guard for the output stores: every kernel stores with one
+# cache policy (out_cpol); a per-lane mix of policies once returned wrong 64-B
+# halves of rows on a few stripes per run (profiles/r03n_ab_cpol.log).
+# Larger batches than the parity tests, two pattern draws each, every output row
+# and every unused output slot compared (vectorised).
+@pytest.mark.parametrize("k,m,S,bound", [(8, 4, 6554, 1), (10, 4, 6554, 2), (8, 4, 6554, 4), (8, 4, 8192, 1),
+                                         (10, 4, 6554, 1)])
+def test_out_of_place_stress(engines, k, m, S, bound):
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, N, P = k + m, 2049, shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 7 + bound)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    ref = torch.cat([data, parity], dim=1)[:, :, :S].cpu().numpy()  # [N, t, S], checked against the oracle above
+    for trial in range(2):
+        rng = np.random.default_rng(1000 * trial + S + bound)
+        masks = _masks(rng, N, t, 0, bound)
+        # expected out[i, r] = shard of the r-th missing index of stripe i
+        missing = [[j for j in range(t) if not (int(masks[i]) >> j) & 1] for i in range(N)]
+        for mode in ("host", "dev"):
+            out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+            if mode == "host":
+                eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
+            else:
+                eng.reconstruct_out(data, parity, out, S, N,
+                                    masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(), max_missing=bound)
+                eng.sync()
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            for r in range(m):
+                rows = np.array([i for i in range(N) if len(missing[i]) > r])
+                if len(rows):
+                    src = np.array([missing[i][r] for i in rows])
+                    bad = np.nonzero((got[rows, r, :S] != ref[rows, src]).any(axis=1))[0]
+                    assert len(bad) == 0, (mode, trial, r, rows[bad][:8].tolist())
+                unused = np.array([i for i in range(N) if len(missing[i]) <= r])
+                if len(unused):
+                    assert (got[unused, r] == 0xC3).all(), (mode, trial, r, "unused output slot written")
+            assert (got[:, :, S:] == 0xC3).all(), "output padding written"
