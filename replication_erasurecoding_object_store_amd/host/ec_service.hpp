@@ -199,6 +199,22 @@ class Service final : public IEcDriver {
   Error Reconstruct(Shards& shards) override { return reconstruct(shards, false); }
   Error ReconstructData(Shards& shards) { return reconstruct(shards, true); }
 
+  // Encode plus the write path's cold_hash (writeservice.go:222 and :267,
+  // computeSHA256Hex(value) :51-54) in one coalesced GPU batch: digest = SHA-256 of
+  // the first value_len bytes of data shards 0..K-1 (the Split input).  The Go
+  // shim's EncodeHash; needs the coalescing service (RS_ERR_NOT_SUPPORTED without).
+  Error EncodeHash(Shards& shards, size_t value_len, uint8_t digest[32]) {
+    if (!co_) return Error{RS_ERR_NOT_SUPPORTED};
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      p[i] = shards[i].empty() ? nullptr : shards[i].data();
+      n[i] = shards[i].size();
+    }
+    return Error{rs_co_encode_hash(co_, p.data(), n.data(), value_len, digest)};
+  }
+
   // [upstream Verify]
   Error Verify(const Shards& shards, bool* ok) {
     if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};

@@ -208,6 +208,27 @@ static void test_split_spare_capacity(ec::Service& svc) {
   }
 }
 
+// WriteEC with the cold_hash next to the encode (writeservice.go:218-222, :267):
+// parity = the oracle's, digest = SHA-256 of the value (oracle), for values whose
+// length is and is not a multiple of K; EncodeHash needs the coalescing service.
+static void test_encode_hash(ec::Service& co, ec::Service& plain) {
+  for (size_t n : {1ul, 10ul, 4096ul, 100001ul}) {
+    const std::vector<uint8_t> value = rand_bytes(n * 7 + 3, n);
+    ec::Shards sh;
+    CHECK(!co.Split(value.data(), value.size(), &sh));
+    uint8_t got[32], want[32];
+    CHECK(!co.EncodeHash(sh, value.size(), got));
+    rso_sha256(value.data(), value.size(), want);
+    CHECK(std::memcmp(got, want, 32) == 0);
+    CHECK(sh == oracle_encode(ec::K, ec::M, sh));
+  }
+  ec::Shards sh;
+  const std::vector<uint8_t> v = rand_bytes(1, 64);
+  CHECK(!plain.Split(v.data(), v.size(), &sh));
+  uint8_t d[32];
+  CHECK(plain.EncodeHash(sh, v.size(), d).code == RS_ERR_NOT_SUPPORTED);
+}
+
 int main() {
   ec::Error err;
   auto svc = ec::Service::NewService(ec::K, ec::M, 0, &err);
@@ -232,6 +253,7 @@ int main() {
     test_errors(*co);
     test_concurrent(*co);
     test_split_spare_capacity(*co);
+    test_encode_hash(*co, *svc);
     uint64_t calls = 0, batches = 0, stripes = 0, maxb = 0;
     CHECK(rs_co_stats(co->coalescer(), &calls, &batches, &stripes, &maxb) == RS_OK);
     std::printf("coalescer: %llu calls, %llu batches, %llu stripes, largest batch %llu\n",
