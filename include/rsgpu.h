@@ -292,7 +292,17 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
                         const uint64_t *lens, size_t n, uint8_t *digests, void *stream);
 
 /* ---- host memory helpers ------------------------------------------------ */
-int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);   /* pin for every GPU: DMA + zero-copy */
+/* Pins [ptr, ptr + bytes) for every GPU of the process (DMA + zero-copy) and
+ * remembers the range: a coalesced call (rs_co_encode / rs_co_reconstruct, their
+ * _submit_ and _many forms; not the _hash or _data forms) whose shards -- the ones
+ * it reads and the ones it fills -- all lie inside one registered range, 16-B
+ * aligned, runs in place: the kernel reads the caller's shards and writes the
+ * parity / missing shards straight into the caller's buffers over PCIe, with no
+ * staging copy either way (the request body and the HTTP send
+ * buffers, or a healer's shard buffers, in a registered arena).  Such a call writes
+ * nothing outside [0, S) of any shard.  Unregister only when no call is using the
+ * range. */
+int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);
 int rs_host_unregister(rs_ctx *ctx, void *ptr);
 
 /* ---- measurement helpers (bench.py) ------------------------------------- */

@@ -117,6 +117,8 @@ struct Batch {
   std::atomic<uint32_t> fill_err{0};   // a slot's plan could not be resolved (plan mode)
   std::atomic<uint32_t> max_missing{0};  // most shards any slot fills: the launch's erasure bound
   std::atomic<uint32_t> hash_in{0};      // some slot wants the SHA-256 of its value (cold_hash)
+  std::atomic<uint32_t> direct_in{0};    // some slot is addressed in the caller's registered buffers
+  uint8_t* host_dev = nullptr;           // zero-copy: GPU address of the pinned staging
   // asynchronous calls of the current run: their records, how many were made, how
   // many have been handed to reapers (under rs_coalescer::done_mu)
   std::unique_ptr<AsyncRec[]> arec;
@@ -160,7 +162,7 @@ struct Batch {
   rs::DevBuf dev;
   // region offsets (same in host staging and device slab)
   size_t o_data = 0, o_parity = 0, o_out = 0, o_masks = 0, o_plans = 0, o_bad = 0, o_hoff = 0, o_hlen = 0,
-         o_digest = 0, bytes = 0;
+         o_digest = 0, o_ptrs = 0, bytes = 0;
 };
 
 // Reserves up to `want` consecutive slots of batch b in generation gen.
@@ -299,6 +301,9 @@ struct rs_coalescer {
 
   int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
+  // objects whose shards lie in rs_host_register'ed memory run in place (zero-copy
+  // staging, k+m <= 16, a pointer-table kernel for (k, m))
+  bool direct_ok = false;
   // callers that may spin-wait for their batch at once (opts.spin_waiters, capped at
   // the CPUs this process may use minus the launcher and completer threads)
   int spin_slots = 0;
@@ -363,7 +368,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->S = S;
   b->P = round_up(S, 16);  // kernel contract: 16-B aligned slots
   rs::DeviceScope ds(rs::engine_device(rs::ctx_engine(co->ctx, b->engine)));
-  const size_t per = b->P * (k + 2 * m) + 64;  // shards + out + mask + plan + bad + hash args + digest
+  const size_t per = b->P * (k + 2 * m) + 64 + 8 * (k + m);  // shards + out + mask + plan + bad + hash + digest + ptrs
   const size_t cap = std::max<size_t>(
       1, std::min({co->max_batch, co->max_bytes / per, size_t(b->n_groups_alloc) * Batch::kGroup}));
   b->cap.store(cap, std::memory_order_relaxed);
@@ -376,10 +381,17 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->o_hoff = b->o_bad + round_up(cap * 4, 256);
   b->o_hlen = b->o_hoff + round_up(cap * 8, 256);
   b->o_digest = b->o_hlen + round_up(cap * 8, 256);
-  b->bytes = b->o_digest + round_up(cap * 32, 256);
+  b->o_ptrs = b->o_digest + round_up(cap * 32, 256);
+  b->bytes = b->o_ptrs + round_up(cap * 8 * (k + m), 256);
   if (!b->stream) RS_HIP(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
   if (!b->done_ev) RS_HIP(hipEventCreateWithFlags(&b->done_ev, hipEventDisableTiming));
   if (b->host.ensure(b->bytes) || b->dev.ensure(b->bytes)) return RS_ERR_DEVICE;
+  b->host_dev = nullptr;
+  if (co->direct_ok) {
+    void* hd = nullptr;
+    if (hipHostGetDevicePointer(&hd, b->host.p, 0) == hipSuccess) b->host_dev = static_cast<uint8_t*>(hd);
+    else (void)hipGetLastError();
+  }
   b->epoch += 1;
   // Words of groups unused for ~2^30 runs would read as "reached" once the epoch
   // wraps half-way round: pull them along (loads only, almost always).
@@ -393,6 +405,7 @@ int prepare(rs_coalescer* co, Batch* b, Kind kind, size_t S) {
   b->fill_err.store(0, std::memory_order_relaxed);
   b->max_missing.store(0, std::memory_order_relaxed);
   b->hash_in.store(0, std::memory_order_relaxed);
+  b->direct_in.store(0, std::memory_order_relaxed);
   b->n_async.store(0, std::memory_order_relaxed);
   b->async_cursor = 0;
   if (b->arec_cap < cap) {  // the batch is free: nobody reads the old records
@@ -446,7 +459,14 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
     RS_HIP(hipMemcpyAsync(host_at(b, b->o_bad), dev_at(b, b->o_bad), n * 4, hipMemcpyDeviceToHost, st));
   } else {
     if (b->fill_err.load(std::memory_order_acquire)) return RS_ERR_DEVICE;
-    if (co->per_stripe) {
+    if (co->per_stripe && b->direct_in.load(std::memory_order_acquire)) {
+      // some slot is addressed in the caller's registered buffers: every slot
+      // through its row of the pointer table (staged slots point into the staging)
+      if (!zc || !b->host_dev || at(0) != b->host_dev) return RS_ERR_DEVICE;
+      const int bound = static_cast<int>(b->max_missing.load(std::memory_order_acquire));
+      rc = rs::engine_apply_batch_ptrs(eng, reinterpret_cast<const uint64_t*>(at(b->o_ptrs)),
+                                       reinterpret_cast<const uint32_t*>(at(b->o_masks)), b->S, n, bound, st);
+    } else if (co->per_stripe) {
       // erasure bound = the most any slot misses (an encode slot: m): a batch of
       // 1-2 erasure repairs runs the E = 1 / 2 kernels
       const int bound = static_cast<int>(b->max_missing.load(std::memory_order_acquire));
@@ -842,6 +862,8 @@ struct RecItem {
   size_t S = 0;
   uint32_t present = 0;
   bool parity_used = false;  // a parity shard is among the k survivors
+  bool direct = false;       // every shard it reads or writes is registered: addressed in place
+  uint64_t dev[32] = {};     // direct: GPU address of every shard (rs_host_register'ed)
 };
 
 // Checks one object; *need = false when there is nothing to do (rc RS_OK).
@@ -901,9 +923,85 @@ void set_hash(Batch* b, int k, size_t slot, uint64_t value_len) {
   if (value_len != rs::kSha256Skip) b->hash_in.store(1, std::memory_order_relaxed);
 }
 
+// A slot's row of the pointer table (GPU addresses of its k+m shards), used when
+// the batch runs the pointer-table kernel (some slot is direct).
+uint64_t* ptr_row(const rs_coalescer* co, Batch* b, size_t slot) {
+  return reinterpret_cast<uint64_t*>(host_at(b, b->o_ptrs)) + slot * static_cast<size_t>(co->k + co->m);
+}
+
+// Row of a staged slot: present shards at their staging copies, missing ones at the
+// slot's output rows (the r-th missing shard -> out row r), all in the staging's
+// GPU mapping.  Written for every staged slot, so a direct slot may join any batch.
+void stage_ptrs(const rs_coalescer* co, Batch* b, size_t slot, uint32_t present) {
+  if (!co->direct_ok || !b->host_dev) return;
+  const size_t k = co->k, m = co->m, P = b->P;
+  uint64_t* row = ptr_row(co, b, slot);
+  auto at = [&](size_t off) { return reinterpret_cast<uint64_t>(b->host_dev + off); };
+  for (size_t s = 0, r = 0; s < k + m; ++s) {
+    if ((present >> s) & 1u)
+      row[s] = s < k ? at(b->o_data + (slot * k + s) * P) : at(b->o_parity + (slot * m + (s - k)) * P);
+    else
+      row[s] = at(b->o_out + (slot * m + r++) * P);
+  }
+}
+
+// GPU addresses of a call's shards when every one the kernel touches lies in
+// rs_host_register'ed memory, 16-B aligned: `touched` bit s = shard s is read (one of
+// the first k present) or written (an output).  Other entries repeat the first
+// touched address (never dereferenced).  False: the call is staged.
+bool direct_ptrs(rs_coalescer* co, uint8_t* const* shards, size_t S, uint32_t touched, uint64_t* dev) {
+  if (!co->direct_ok) return false;
+  const int t = co->k + co->m;
+  uint64_t first = 0;
+  for (int s = 0; s < t; ++s) {
+    dev[s] = 0;
+    if (!((touched >> s) & 1u)) continue;
+    if (!shards[s] || reinterpret_cast<uintptr_t>(shards[s]) % 16) return false;
+    uint8_t* d = rs::ctx_registered(co->ctx, shards[s], S);
+    if (!d || reinterpret_cast<uintptr_t>(d) % 16) return false;
+    dev[s] = reinterpret_cast<uint64_t>(d);
+    if (!first) first = dev[s];
+  }
+  for (int s = 0; s < t; ++s)
+    if (!dev[s]) dev[s] = first;
+  return first != 0;
+}
+
+// A direct slot: its row = the caller's buffers; nothing is copied.
+void direct_fill(const rs_coalescer* co, Batch* b, size_t slot, const uint64_t* dev, uint32_t present) {
+  const int t = co->k + co->m;
+  std::memcpy(ptr_row(co, b, slot), dev, static_cast<size_t>(t) * 8);
+  set_hash(b, co->k, slot, rs::kSha256Skip);
+  reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = present;
+  note_missing(b, static_cast<uint32_t>(t - __builtin_popcount(present)));
+  b->direct_in.store(1, std::memory_order_relaxed);
+}
+
+// Decides whether a reconstruct runs in place (Reconstruct only: ReconstructData
+// leaves missing parity unwritten and may pass no buffer for it).
+void rec_direct(rs_coalescer* co, RecItem* it, bool data_only) {
+  it->direct = false;
+  if (data_only) return;
+  const int k = co->k, t = k + co->m;
+  uint32_t touched = 0;
+  for (int i = 0, used = 0; i < t; ++i) {
+    if (it->lens[i] && used < k) {
+      touched |= 1u << i;
+      ++used;
+    } else if (!it->lens[i]) {
+      touched |= 1u << i;
+    }
+  }
+  it->direct = direct_ptrs(co, it->shards, it->S, touched, it->dev);
+}
+
 void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, bool data_only) {
   const int k = co->k, m = co->m, t = k + m;
   const size_t P = b->P;
+  if (it.direct) {
+    direct_fill(co, b, slot, it.dev, it.present);
+    return;
+  }
   set_hash(b, k, slot, rs::kSha256Skip);
   for (int i = 0, staged = 0; i < t && staged < k; ++i) {  // the k survivors only
     if (!it.lens[i]) continue;
@@ -914,6 +1012,7 @@ void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, 
   if (co->per_stripe) {
     reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
     note_missing(b, static_cast<uint32_t>(t - __builtin_popcount(it.present)));
+    stage_ptrs(co, b, slot, it.present);
   } else {
     set_plan(co, b, slot, it.present, data_only, false);
   }
@@ -925,8 +1024,8 @@ void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it,
   for (int i = 0; i < t; ++i) {
     if (it.lens[i]) continue;
     if (!data_only || i < k) {
-      std::memcpy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
-      it.lens[i] = it.S;
+      if (!it.direct) std::memcpy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
+      it.lens[i] = it.S;  // direct: the kernel wrote the caller's buffer
     }
     ++r;
   }
@@ -938,6 +1037,7 @@ int co_reconstruct(rs_coalescer* co, uint8_t* const* shards, size_t* lens, bool 
   bool need = false;
   const int rc = rec_check(co, shards, lens, data_only, &it, &need);
   if (rc || !need) return rc;
+  rec_direct(co, &it, data_only);
   return submit(
       co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it, data_only); },
       [&](Batch* b, size_t slot) { rec_drain(co, b, slot, it, data_only); });
@@ -972,6 +1072,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
+  co->direct_ok = co->zero_copy && co->k + co->m <= 16 && rs::apply_ptrs_supported(co->k, co->m);
   co->spin_slots = std::min(o.spin_waiters, std::max(0, usable_cpus() - 2 - 2 * ne));
   co->engine_load.assign(static_cast<size_t>(ne), 0);
   // the most slots a batch can hold: max_batch, bounded by the bytes budget at
@@ -1033,18 +1134,28 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
+  // every shard in registered memory (and no cold_hash, which reads the staging):
+  // the kernel reads the data and writes the parity in place
+  uint64_t dev[32];
+  const bool direct = !hash && direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev);
   auto fill = [&](Batch* b, size_t slot) {
+    if (direct) {
+      direct_fill(co, b, slot, dev, data_mask);
+      return;
+    }
     for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
     set_hash(b, k, slot, value_len);
     if (co->per_stripe) {
       reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
       note_missing(b, static_cast<uint32_t>(m));
+      stage_ptrs(co, b, slot, data_mask);
     } else {
       set_plan(co, b, slot, data_mask, false, true);
     }
   };
   auto drain = [&](Batch* b, size_t slot) {
-    for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+    if (!direct)
+      for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
     if (hash) std::memcpy(digest, host_at(b, b->o_digest + slot * 32), 32);
   };
   return submit(co, Kind::kApply, S, false, fill, drain);
@@ -1098,16 +1209,23 @@ int rs_co_submit_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* 
   if (m == 0) return RS_ERR_NOT_SUPPORTED;  // nothing to compute, nothing would be reaped
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   const uint32_t data_mask = (1u << k) - 1u;
+  uint64_t dev[32];
+  const bool direct = direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev);  // in place: nothing to copy back
   AsyncRec rec;
   rec.tag = tag;
-  rec.n_out = static_cast<uint32_t>(m);
+  rec.n_out = direct ? 0u : static_cast<uint32_t>(m);
   for (int r = 0; r < m; ++r) rec.out[r] = shards[k + r];
   auto fill = [&](Batch* b, size_t slot) {
+    if (direct) {
+      direct_fill(co, b, slot, dev, data_mask);
+      return;
+    }
     for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
     set_hash(b, k, slot, rs::kSha256Skip);
     if (co->per_stripe) {
       reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
       note_missing(b, static_cast<uint32_t>(m));
+      stage_ptrs(co, b, slot, data_mask);
     } else {
       set_plan(co, b, slot, data_mask, false, true);
     }
@@ -1122,10 +1240,12 @@ int rs_co_submit_reconstruct(rs_coalescer* co, uint8_t* const* shards, const siz
   const int rc = rec_check(co, shards, const_cast<size_t*>(lens), false, &it, &need);
   if (rc) return rc;
   if (!need) return RS_ERR_NOT_SUPPORTED;  // nothing missing: nothing would be reaped
+  rec_direct(co, &it, false);
   AsyncRec rec;
   rec.tag = tag;
-  for (int i = 0; i < co->k + co->m; ++i)
-    if (!lens[i]) rec.out[rec.n_out++] = shards[i];
+  if (!it.direct)  // in place: the kernel writes the missing shards' buffers itself
+    for (int i = 0; i < co->k + co->m; ++i)
+      if (!lens[i]) rec.out[rec.n_out++] = shards[i];
   return submit_async(
       co, Kind::kApply, it.S, it.parity_used, [&](Batch* b, size_t slot) { rec_fill(co, b, slot, it, false); }, rec);
 }
@@ -1181,7 +1301,10 @@ int rs_co_reconstruct_many(rs_coalescer* co, size_t n_objects, uint8_t* const* s
   for (size_t i = 0; i < n_objects; ++i) {
     bool need = false;
     rcs[i] = rec_check(co, shards + i * t, lens + i * t, false, &items[i], &need);
-    if (need) by_len[items[i].S].push_back(i);
+    if (need) {
+      rec_direct(co, &items[i], false);
+      by_len[items[i].S].push_back(i);
+    }
   }
   for (auto& g : by_len) {
     const std::vector<size_t>& idx = g.second;

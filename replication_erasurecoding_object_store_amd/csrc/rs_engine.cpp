@@ -37,6 +37,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -362,9 +363,20 @@ struct Engine {
 
 using rs::Engine;
 
+// A host range pinned and GPU-mapped through rs_host_register.
+struct RegRange {
+  uintptr_t lo = 0, hi = 0;  // [lo, hi)
+  uint8_t* dev = nullptr;     // GPU address of lo (portable mapping: every device)
+};
+
 struct rs_ctx {
   int k = 0, m = 0;
   Matrix enc;
+  // rs_host_register'ed ranges, sorted by lo (the coalescer addresses buffers that
+  // lie inside one in place instead of staging them)
+  std::shared_mutex reg_mu;
+  std::vector<RegRange> reg;
+  std::atomic<uint32_t> n_reg{0};
   std::vector<uint32_t> h_lut;            // missing mask -> plan index (k+m <= 16)
   std::vector<std::unique_ptr<Engine>> engines;
   Shared shared;
@@ -1032,6 +1044,18 @@ PlanSet build_plans(rs_ctx* c) {
 namespace rs {
 
 int ctx_engine_count(const rs_ctx* c) { return c ? static_cast<int>(c->engines.size()) : 0; }
+
+uint8_t* ctx_registered(rs_ctx* c, const void* p, size_t bytes) {
+  if (!c || !p || c->n_reg.load(std::memory_order_acquire) == 0) return nullptr;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  std::shared_lock<std::shared_mutex> g(c->reg_mu);
+  auto it = std::upper_bound(c->reg.begin(), c->reg.end(), lo,
+                             [](uintptr_t x, const RegRange& r) { return x < r.lo; });
+  if (it == c->reg.begin()) return nullptr;
+  --it;  // the last range starting at or before p
+  if (lo >= it->hi || bytes > it->hi - lo) return nullptr;
+  return it->dev + (lo - it->lo);
+}
 Engine* ctx_engine(rs_ctx* c, int i) { return c->engines[static_cast<size_t>(i)].get(); }
 int engine_device(const Engine* e) { return e->device; }
 
@@ -1118,6 +1142,27 @@ int engine_apply_batch_plans(Engine* e, const uint8_t* data, size_t data_sp, con
   a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);  // unused: every stripe has its own
   a.stripe_plans = plans_dev;
   return launch(e, a, e->m, true, s);
+}
+
+int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uint32_t* masks_dev, size_t S,
+                            size_t N, int max_missing, hipStream_t s) {
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!e->have_lut || S > 0xFFFFFFF0u || N * ((round_up(S, 16) / 16 + 63) / 64) >= (1ull << 32))
+    return RS_ERR_NOT_SUPPORTED;
+  const int bound = max_missing > 0 ? std::min(max_missing, e->m) : e->m;
+  const Layout L{nullptr, 0, nullptr, 0, round_up(S, 16)};
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+  a.present_masks = masks_dev;
+  a.shard_ptrs = shard_ptrs_dev;
+  if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, bound);
+  const char* name = rs::launch_apply_ptrs(a, bound, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
+  if (!name) return RS_ERR_NOT_SUPPORTED;
+  e->shared->last_kernel.store(name);
+  RS_HIP(hipGetLastError());
+  return RS_OK;
 }
 
 int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
@@ -1500,16 +1545,37 @@ static int sync_stream(rs_ctx* c, void* stream, bool release) {
 int rs_sync(rs_ctx* c, void* stream) { return sync_stream(c, stream, false); }
 int rs_stream_release(rs_ctx* c, void* stream) { return sync_stream(c, stream, true); }
 
-// Pins for every GPU of the process (portable) and maps into their address spaces.
+// Pins for every GPU of the process (portable) and maps into their address spaces;
+// the range is remembered so coalesced calls on buffers inside it run in place.
 int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
-  if (!c || !ptr) return RS_ERR_INVALID_ARG;
+  if (!c || !ptr || bytes == 0) return RS_ERR_INVALID_ARG;
   DeviceScope ds(c->engines[0]->device);
   RS_HIP(hipHostRegister(ptr, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(ptr);
+    return RS_ERR_DEVICE;
+  }
+  const RegRange r{reinterpret_cast<uintptr_t>(ptr), reinterpret_cast<uintptr_t>(ptr) + bytes,
+                   static_cast<uint8_t*>(dev)};
+  std::unique_lock<std::shared_mutex> g(c->reg_mu);
+  auto it = std::lower_bound(c->reg.begin(), c->reg.end(), r.lo,
+                             [](const RegRange& a, uintptr_t lo) { return a.lo < lo; });
+  c->reg.insert(it, r);
+  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
   return RS_OK;
 }
 
 int rs_host_unregister(rs_ctx* c, void* ptr) {
   if (!c || !ptr) return RS_ERR_INVALID_ARG;
+  {
+    std::unique_lock<std::shared_mutex> g(c->reg_mu);
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+    auto it = std::find_if(c->reg.begin(), c->reg.end(), [&](const RegRange& r) { return r.lo == lo; });
+    if (it != c->reg.end()) c->reg.erase(it);
+    c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+  }
   DeviceScope ds(c->engines[0]->device);
   RS_HIP(hipHostUnregister(ptr));
   return RS_OK;

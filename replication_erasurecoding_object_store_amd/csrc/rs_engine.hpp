@@ -70,5 +70,17 @@ const uint8_t* engine_encode_plan(Engine* e);
 int engine_apply_batch_plans(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
                              size_t parity_sp, size_t pitch, size_t S, size_t N, const uint64_t* plans_dev,
                              uint8_t* out, size_t out_sp, hipStream_t s);
+// Per-stripe masks (k+m <= 16) over a table of shard addresses: stripe i's shard s
+// at shard_ptrs_dev[i*(k+m) + s], every shard S bytes and 16-B aligned, inputs the
+// first k present, outputs the missing shards' buffers; nothing outside [0, S) of
+// any shard is written (apply_ptr_kernel).  RS_ERR_NOT_SUPPORTED for (k, m) without
+// a specialised kernel (the caller then stages).  The status word of s collects
+// deferred errors as for device masks.
+int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uint32_t* masks_dev, size_t S,
+                            size_t N, int max_missing, hipStream_t s);
+// GPU address of [p, p + bytes) when it lies inside one rs_host_register'ed range of
+// the context, else nullptr.  Cheap when nothing is registered.
+uint8_t* ctx_registered(rs_ctx* c, const void* p, size_t bytes);
+bool apply_ptrs_supported(int k, int m);  // engine_apply_batch_ptrs has a kernel for (k, m)
 
 }  // namespace rs

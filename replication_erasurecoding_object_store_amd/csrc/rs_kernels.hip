@@ -900,6 +900,91 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
 }
 
 // ---------------------------------------------------------------------------
+// Per-stripe plans over a table of shard addresses (round 3): the coalescer's
+// batches whose objects lie in the caller's registered (pinned, GPU-mapped) buffers
+// are read and written in place -- no staging copy of the request body, no copy of
+// the parity back.  A slot staged as usual simply points
+// into the staging.  Every shard is its own buffer of exactly S bytes, so each is
+// addressed through a buffer descriptor whose range ends with the shard: loads stop
+// at the dword holding byte S-1 (out-of-range dwords are not fetched and read as
+// zero), stores at byte S-1 (the partial last column in byte-exact pieces).
+// Stripe-aligned 64-column tasks: per-object shards are large (the objects that
+// gain from skipping the copy), so the idle lanes of a stripe's last task are few.
+template <int K, int M, int E>
+__global__ __launch_bounds__(256) void apply_ptr_kernel(const KernelArgs a) {
+  constexpr int T = K + M;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_index();
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t bps = a.blocks_per_stripe;
+  const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
+  const uint32_t S = a.shard_len;
+  const uint32_t cols = (S + 15u) >> 4;
+  const uint32_t nb = S & 15u;
+  const uint32_t in_range = (S + 3u) & ~3u;  // whole dwords: the last one holds byte S-1
+  const uint32_t full = a.full_mask;
+  uint32_t bad = 0u;
+  for (uint32_t t = wave; t < ntasks; t += nwaves) {
+    const uint32_t stripe = t / bps;
+    const uint32_t blk = t - stripe * bps;
+    const uint32_t present = as_const<uint32_t>(a.present_masks)[stripe] & full;
+    uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
+    bool skip = pid == kPlanInvalid;
+    bad |= skip ? 1u : 0u;
+    if constexpr (E < M) {  // more erasures than this launch's bound: skip, flag
+      const bool over = static_cast<uint32_t>(__builtin_popcount((~present) & full)) > static_cast<uint32_t>(E);
+      bad |= over ? 2u : 0u;
+      skip = skip || over;
+    }
+    pid = skip ? 0u : pid;  // plan 0 = nothing missing: every store dropped
+    const uint8_t* plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+    if constexpr (K * E * 5 > 48) asm volatile("" : "+s"(plan));  // tables per trip (as apply_kernel)
+    const PlanView pv(plan, K, M);
+    const uint64_t* sp = as_const<uint64_t>(a.shard_ptrs) + static_cast<uint64_t>(stripe) * T;
+    const uint32_t col = blk * 64u + lane;
+    const uint32_t off = (col < cols ? col : cols - 1u) * 16u;  // past the end: re-read the last column
+    u32x4 x[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      const uint32_t s = skip ? static_cast<uint32_t>(c) : pv.in_idx(c);
+      uint8_t* base = reinterpret_cast<uint8_t*>(as_const<uint64_t>(sp)[s]);
+      const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, in_range,
+                                                       0x00020000);
+      x[c] = bload16(r, off, 0);
+    }
+    u32x4 y[E];
+    const uint32_t n_out = pv.n_out();
+    if constexpr (E > 2) {
+      Idx3 ix[K][4];
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+      y[0] = gf_row_ix<K, M>(plan, ix, 0);
+#pragma unroll
+      for (int r = 1; r < E; ++r) {
+        y[r] = y[0];  // dropped unless computed
+        if (static_cast<uint32_t>(r) < n_out) y[r] = gf_row_ix<K, M>(plan, ix, r);
+      }
+    } else {
+      gf_rows<K, M, 0, E>(plan, x, y);
+    }
+    const bool fullc = col < a.full_cols;
+    const bool part = nb != 0u && col == a.full_cols;
+    const bool last = nb != 0u && blk + 1u == bps;  // wave-uniform: the task holds the partial column
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      const bool row = static_cast<uint32_t>(r) < n_out;
+      uint8_t* base = reinterpret_cast<uint8_t*>(as_const<uint64_t>(sp)[row ? pv.out_idx(r) : 0u]);
+      const auto ro = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(uniform_ptr(base)), 0, S, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(y[r], ro, fullc && row ? off : kDropOffset, 0, out_cpol<K, E>());
+      if (last) store_part_rsrc<out_cpol<K, E>()>(ro, off, 0, part && row, y[r], nb);
+    }
+  }
+  if (bad && lane == 0u) atomicOr(a.status, bad);
+}
+
+// ---------------------------------------------------------------------------
 // Verify / scrub ([upstream reedsolomon.go Verify]: re-encode and compare; the
 // reference lists bit-rot detection as missing, docs/ARCHITECTURE.md:175-178).
 // Same lookup arithmetic as apply_kernel, but the M stored parity columns are
@@ -1271,6 +1356,35 @@ const char* launch_apply(const KernelArgs& args, int e, bool per_stripe, uint32_
     name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s);
     if (!name) return nullptr;
   }
+  return name;
+}
+
+bool apply_ptrs_supported(int k, int m) {
+  return (k == 4 && m == 2) || (k == 8 && m == 4) || (k == 10 && m == 4) || (k == 6 && m == 3);
+}
+
+const char* launch_apply_ptrs(const KernelArgs& a, int e_bound, uint32_t blocks_per_cu, uint32_t cu_count,
+                              hipStream_t s) {
+  const void* fn = nullptr;
+  const char* name = nullptr;
+  const int e = e_bound <= 2 ? e_bound : a.m;  // E = 1, 2 or m
+#define RS_PTRS(KK, MM, EE)                                                 \
+  if (!fn && a.k == KK && a.m == MM && e == EE) {                           \
+    fn = reinterpret_cast<const void*>(&apply_ptr_kernel<KK, MM, EE>);     \
+    name = "apply_ptr_kernel<" #KK "," #MM "," #EE ">";                     \
+  }
+  RS_PTRS(4, 2, 1) RS_PTRS(4, 2, 2)
+  RS_PTRS(8, 4, 1) RS_PTRS(8, 4, 2) RS_PTRS(8, 4, 4)
+  RS_PTRS(10, 4, 1) RS_PTRS(10, 4, 2) RS_PTRS(10, 4, 4)
+  RS_PTRS(6, 3, 1) RS_PTRS(6, 3, 2) RS_PTRS(6, 3, 3)
+#undef RS_PTRS
+  if (!fn) return nullptr;  // shapes without a specialisation stage their slots instead
+  KernelArgs b = a;
+  b.max_out = static_cast<uint32_t>(e);
+  void* args[] = {&b};
+  const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
+  if (waves == 0) return name;
+  if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
 }
 

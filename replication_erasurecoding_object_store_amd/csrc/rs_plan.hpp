@@ -99,6 +99,9 @@ struct KernelArgs {
   uint32_t encode_net;             // 1: uniform plan is the encode matrix and the generated
                                    //    bitsliced XOR program for (k, m) matches it
   uint32_t data_inputs;            // 1: uniform plan reads data shards 0..k-1 (encode)
+  const uint64_t* shard_ptrs;      // pointer-table launches: stripe i's shard s at device address
+                                   //   shard_ptrs[i*(k+m) + s] (inputs: present shards; outputs:
+                                   //   the missing shards' buffers), each S bytes, 16-B aligned
 };
 
 // Parity rows the generated bitsliced encode program of (k, m) was derived from
@@ -116,6 +119,12 @@ const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t b
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.
+// Per-stripe plans (masks -> LUT) over a table of shard addresses instead of a
+// strided layout: every shard its own buffer of exactly S bytes (caller memory the
+// coalescer addresses in place).  Loads never touch a byte past the dword holding a
+// shard's byte S-1, stores never past byte S-1.  e = the launch's erasure bound.
+const char* launch_apply_ptrs(const KernelArgs& a, int e, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
+bool apply_ptrs_supported(int k, int m);  // a specialised pointer-table kernel exists
 // a.bad must be zeroed first (launch_verify does it on s).
 const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
 

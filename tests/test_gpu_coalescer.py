@@ -439,3 +439,117 @@ def test_async_submit_reap_matches_oracle(gpu, k, m):
         assert L.rs_co_reap(svc._co, tags, rcs, 64, 0) == 0
     finally:
         svc.close()
+
+
+@pytest.mark.parametrize("k,m,S", [(4, 2, 100000), (10, 4, 6554), (4, 2, 1001), (8, 4, 384000), (6, 3, 777)])
+def test_registered_buffers_run_in_place(gpu, k, m, S):
+    """Objects whose shards lie in rs_host_register'ed memory (request bodies and
+    storage-node reads in a pinned arena) are encoded and
+    reconstructed by the coalescer in place -- the pointer-table kernel reads and
+    writes the caller's buffers, nothing is staged -- with the oracle's bytes and no
+    byte outside [0, S) of any shard written; pageable objects join the same
+    batches (staged); after rs_host_unregister the same calls are staged again.
+    Asynchronous calls run in place too (nothing left to copy at reap)."""
+    import ctypes
+    import mmap
+
+    from replication_erasurecoding_object_store_amd import _lib
+
+    L = _lib.lib()
+    t = k + m
+    n_obj = 24
+    P = (S + 15) // 16 * 16 + 48  # 16-B aligned shards, guard bytes between them
+    region = mmap.mmap(-1, n_obj * t * P + 4096)
+    arr = np.frombuffer(region, np.uint8)
+    arr[:] = 0xA5
+    base = ctypes.addressof(ctypes.c_uint8.from_buffer(region))
+    rng = np.random.default_rng(k * 1000 + S)
+    data = rng.integers(0, 256, (n_obj, k, S), dtype=np.uint8)
+    want = np.zeros((n_obj, t, S), np.uint8)
+    for i in range(n_obj):
+        sh = [bytearray(data[i, c].tobytes()) for c in range(k)] + [bytearray(S) for _ in range(m)]
+        assert rs_oracle.encode(k, m, sh) == 0
+        want[i] = np.frombuffer(b"".join(sh), np.uint8).reshape(t, S)
+
+    def view(i, s):
+        return arr[(i * t + s) * P:(i * t + s) * P + S]
+
+    def ptrs(i):
+        return (_lib._u8p * t)(*[ctypes.cast(base + (i * t + s) * P, _lib._u8p) for s in range(t)])
+
+    svc = CoalescingService(k, m, max_wait_us=3000)
+    registered = False
+    try:
+        assert L.rs_host_register(svc._ctx, base, len(region)) == 0
+        registered = True
+        for i in range(n_obj):
+            for c in range(k):
+                view(i, c)[:] = data[i, c]
+        # encode: 24 registered objects and 8 pageable ones from 32 threads (batches mix both)
+        pageable = [[bytearray(data[i, c].tobytes()) for c in range(k)] + [bytearray(S) for _ in range(m)]
+                    for i in range(8)]
+
+        def enc(tid):
+            if tid < n_obj:
+                lens = (ctypes.c_size_t * t)(*([S] * t))
+                assert L.rs_co_encode(svc._co, ptrs(tid), lens) == _lib.RS_OK
+            else:
+                svc.Encode(pageable[tid - n_obj])
+
+        _run_threads(n_obj + 8, enc)
+        for i in range(n_obj):
+            for s in range(t):
+                assert np.array_equal(view(i, s), want[i, s]), ("encode", i, s)
+        for i in range(8):
+            assert [bytes(x) for x in pageable[i]] == [want[i, s].tobytes() for s in range(t)]
+        # reconstruct: 1..m erased per object, their buffers scribbled; odd objects
+        # blocking from threads, even ones asynchronous from this thread
+        lost = [sorted(rng.choice(t, size=int(rng.integers(1, m + 1)), replace=False).tolist()) for _ in range(n_obj)]
+        for i in range(n_obj):
+            for s in lost[i]:
+                view(i, s)[:] = 0x3C
+        keep = []
+        for i in range(0, n_obj, 2):
+            p, lens = ptrs(i), (ctypes.c_size_t * t)(*[0 if s in lost[i] else S for s in range(t)])
+            keep.append((p, lens))
+            assert L.rs_co_submit_reconstruct(svc._co, p, lens, i) == _lib.RS_OK
+
+        def rec(tid):
+            i = 2 * tid + 1
+            lens = (ctypes.c_size_t * t)(*[0 if s in lost[i] else S for s in range(t)])
+            assert L.rs_co_reconstruct(svc._co, ptrs(i), lens) == _lib.RS_OK
+            assert all(lens[s] == S for s in range(t))
+
+        _run_threads(n_obj // 2, rec)
+        tags = (ctypes.c_uint64 * 64)()
+        rcs = (ctypes.c_int * 64)()
+        reaped = set()
+        while len(reaped) < n_obj // 2:
+            n = L.rs_co_reap(svc._co, tags, rcs, 64, 1000000)
+            assert n > 0
+            for j in range(n):
+                assert rcs[j] == _lib.RS_OK
+                reaped.add(tags[j])
+        assert reaped == set(range(0, n_obj, 2))
+        assert "apply_ptr_kernel" in L.rs_last_kernel(svc._ctx).decode()
+        for i in range(n_obj):
+            for s in range(t):
+                assert np.array_equal(view(i, s), want[i, s]), ("reconstruct", i, s, lost[i])
+        # nothing outside the shards was written
+        for i in range(n_obj * t):
+            assert (arr[i * P + S:(i + 1) * P] == 0xA5).all(), ("guard", i)
+        assert (arr[n_obj * t * P:] == 0xA5).all()
+        # unregistered: the same memory is staged, same bytes
+        assert L.rs_host_unregister(svc._ctx, base) == 0
+        registered = False
+        for s in range(m):
+            view(0, k + s)[:] = 0
+        lens = (ctypes.c_size_t * t)(*([S] * t))
+        assert L.rs_co_encode(svc._co, ptrs(0), lens) == _lib.RS_OK
+        assert "apply_ptr_kernel" not in L.rs_last_kernel(svc._ctx).decode()
+        for s in range(t):
+            assert np.array_equal(view(0, s), want[0, s])
+    finally:
+        if registered:
+            L.rs_host_unregister(svc._ctx, base)
+        svc.close()

@@ -17,6 +17,8 @@
 // "async": the coalescer's asynchronous calls (rs_co_submit_* / rs_co_reap), each
 // thread an event loop with `depth` calls in flight (the Go shim's model: request
 // goroutines park on a channel while one poller reaps).
+// REGISTER=1: the objects live in one rs_host_register'ed arena: coalesced calls on
+// them run in place (pointer-table kernel, no staging copies).
 // ROTATE_MB=<n>: each blocking thread cycles through its share of n MiB of objects
 // (DRAM-resident calls, as objects fresh off the network or a disk are) instead of
 // re-using one cache-resident object.
@@ -98,7 +100,24 @@ int main(int argc, char** argv) {
     std::vector<size_t> n;
     uint64_t j = 0;
   };
-  auto make_obj = [&](uint64_t seed) {
+  // REGISTER=1: every object's shards live in one rs_host_register'ed arena (the
+  // gateway's request bodies / the healer's shard buffers in a pinned arena), so
+  // coalesced calls run in place (no staging copies); else per-shard heap vectors.
+  const bool reg = std::getenv("REGISTER") && std::atoi(std::getenv("REGISTER")) != 0;
+  const size_t SP = (S + 63) / 64 * 64;
+  const size_t per_thread = async_mode ? static_cast<size_t>(depth)
+                                       : std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
+  uint8_t* arena = nullptr;
+  size_t arena_bytes = 0;
+  if (reg) {
+    arena_bytes = static_cast<size_t>(T) * per_thread * (k + m) * SP;
+    arena = static_cast<uint8_t*>(std::aligned_alloc(4096, (arena_bytes + 4095) / 4096 * 4096));
+    if (!arena || rs_host_register(ctx, arena, arena_bytes) != RS_OK) {
+      std::fprintf(stderr, "REGISTER: arena of %zu bytes failed\n", arena_bytes);
+      return 1;
+    }
+  }
+  auto make_obj = [&](uint64_t seed, size_t place) {
     Obj o;
     o.sh.assign(k + m, std::vector<uint8_t>(S));
     uint64_t x = 0x9E3779B97F4A7C15ull * (seed + 1);
@@ -111,9 +130,18 @@ int main(int argc, char** argv) {
       }
     o.p.resize(k + m);
     o.n.assign(k + m, S);
-    for (int i = 0; i < k + m; ++i) o.p[i] = o.sh[i].data();
+    for (int i = 0; i < k + m; ++i) {
+      if (arena) {
+        o.p[i] = arena + (place * (k + m) + i) * SP;
+        std::memcpy(o.p[i], o.sh[i].data(), S);
+      } else {
+        o.p[i] = o.sh[i].data();
+      }
+    }
     if (rs_encode(ctx, o.p.data(), o.n.data()) != RS_OK) ++bad;
-    o.keep = o.sh;
+    o.keep.assign(k + m, std::vector<uint8_t>(S));
+    for (int i = 0; i < k + m; ++i) std::memcpy(o.keep[i].data(), o.p[i], S);
+    if (arena) o.sh.clear();  // the arena holds the shards
     return o;
   };
   // Call j of an object: every 7th pair (an encode and a reconstruct
@@ -128,20 +156,20 @@ int main(int argc, char** argv) {
     if (mix && (o.j & 1)) {
       const int lost = static_cast<int>((o.j >> 1) % (k + m));
       o.n[lost] = 0;
-      if (v) std::memset(o.sh[lost].data(), 0x5a, S);
+      if (v) std::memset(o.p[lost], 0x5a, S);
       return lost;
     }
     if (v)
-      for (int r = 0; r < m; ++r) std::memset(o.sh[k + r].data(), 0x5a, S);
+      for (int r = 0; r < m; ++r) std::memset(o.p[k + r], 0x5a, S);
     return -1;
   };
   auto check = [&](Obj& o) -> uint64_t {
     uint64_t e = 0;
     if (verified(o))
       for (int i = 0; i < k + m; ++i)
-        if (std::memcmp(o.sh[i].data(), o.keep[i].data(), S) != 0) {
+        if (std::memcmp(o.p[i], o.keep[i].data(), S) != 0) {
           ++e;
-          std::memcpy(o.sh[i].data(), o.keep[i].data(), S);
+          std::memcpy(o.p[i], o.keep[i].data(), S);
         }
     ++o.j;
     return e;
@@ -154,7 +182,7 @@ int main(int argc, char** argv) {
         // reaped tag = (thread << 32 | object) is routed to its owner through a
         // completion word; each loop then handles its own completed objects.
         std::vector<Obj> objs;
-        for (int d = 0; d < depth; ++d) objs.push_back(make_obj(static_cast<uint64_t>(t) * depth + d));
+        for (int d = 0; d < depth; ++d) objs.push_back(make_obj(static_cast<uint64_t>(t) * depth + d, static_cast<size_t>(t) * per_thread + d));
         std::vector<int> idle;
         for (int d = depth - 1; d >= 0; --d) idle.push_back(d);
         std::vector<uint64_t> tags(256);
@@ -206,9 +234,10 @@ int main(int argc, char** argv) {
       // ROTATE_MB: the thread cycles through its share of that many MiB of objects,
       // so calls find their object in DRAM instead of the cache (1 GiB >> the host's
       // 256 MiB of L3); default one object, cache-resident after the first call
-      const size_t npool = std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
+      const size_t npool = per_thread;
       std::vector<Obj> pool;
-      for (size_t i = 0; i < npool; ++i) pool.push_back(make_obj(static_cast<uint64_t>(t) * npool + i));
+      for (size_t i = 0; i < npool; ++i)
+        pool.push_back(make_obj(static_cast<uint64_t>(t) * npool + i, static_cast<size_t>(t) * npool + i));
       size_t cur = 0;
       ++ready;
       while (!start.load()) std::this_thread::yield();
@@ -253,13 +282,17 @@ int main(int argc, char** argv) {
       "{\"mode\": \"%s\", \"workload\": \"%s\", \"threads\": %d, \"obj_bytes\": %zu, \"seconds\": %.2f, "
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
       "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d, "
-      "\"depth\": %d, \"busy\": %llu, \"rotate_mb\": %zu}\n",
+      "\"depth\": %d, \"busy\": %llu, \"rotate_mb\": %zu, \"registered\": %d}\n",
       async_mode ? "async" : (co ? "coalesced" : (cpu_mode ? "cpu" : "direct")), mix ? "mix" : "enc", T, obj, dt,
       n_ops / dt, n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
-      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20);
+      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20, reg ? 1 : 0);
   if (co) rs_coalescer_destroy(co);
+  if (arena) {
+    rs_host_unregister(ctx, arena);
+    std::free(arena);
+  }
   if (enc_plan) rso_baseline_plan_free(enc_plan);
   for (void* pl : rec_plan)
     if (pl) rso_baseline_plan_free(pl);
