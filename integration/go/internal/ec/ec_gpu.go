@@ -403,3 +403,70 @@ func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 	}
 	return errs
 }
+
+// Arena hands out []byte backed by C memory the engine has registered
+// (rs_host_register): a call whose shards -- those it reads and those it fills --
+// all come from an arena runs in place on the GPU, with no staging copy of the
+// request body and the parity written straight into the caller's slices
+// (DESIGN.md §6, "In place on registered buffers").  Meant for buffers the service
+// owns end to end: the gateway reading a request body into Alloc'd memory before
+// Split, parity slices for the storage-node uploads, the healer's shard fetches.
+// A bump allocator: Alloc until full, Reset when none of its slices is in use.
+// Nil on a GPU-less host (the CPU codec needs no arena).
+type Arena struct {
+	ctx  *C.rs_ctx
+	base unsafe.Pointer
+	size int
+	mu   sync.Mutex
+	off  int
+}
+
+// NewArena registers `size` bytes of C memory for in-place calls.
+func (s *Service) NewArena(size int) (*Arena, error) {
+	if s.cpu != nil || size <= 0 {
+		return nil, nil
+	}
+	n := (size + 4095) &^ 4095
+	p := C.aligned_alloc(4096, C.size_t(n))
+	if p == nil {
+		return nil, errors.New("rsgpu: arena allocation failed")
+	}
+	if rc := C.rs_host_register(s.ctx, p, C.size_t(n)); rc != C.RS_OK {
+		C.free(p)
+		return nil, toErr(rc)
+	}
+	return &Arena{ctx: s.ctx, base: p, size: n}, nil
+}
+
+// Alloc returns n bytes (16-B aligned, len = cap = n) or nil when the arena is full.
+func (a *Arena) Alloc(n int) []byte {
+	if a == nil || n <= 0 {
+		return nil
+	}
+	a.mu.Lock()
+	defer a.mu.Unlock()
+	off := (a.off + 15) &^ 15
+	if off+n > a.size {
+		return nil
+	}
+	a.off = off + n
+	return unsafe.Slice((*byte)(unsafe.Add(a.base, off)), n)
+}
+
+// Reset makes the whole arena available again (no slice of it may be in use).
+func (a *Arena) Reset() {
+	if a != nil {
+		a.mu.Lock()
+		a.off = 0
+		a.mu.Unlock()
+	}
+}
+
+// Close unregisters and frees the arena (no call may be using it).
+func (a *Arena) Close() {
+	if a != nil && a.base != nil {
+		C.rs_host_unregister(a.ctx, a.base)
+		C.free(a.base)
+		a.base = nil
+	}
+}

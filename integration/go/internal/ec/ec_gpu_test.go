@@ -173,3 +173,65 @@ func TestEncodeHashMatchesSha256(t *testing.T) {
 		}
 	}
 }
+
+// Shards allocated from an Arena (registered C memory) are encoded and
+// reconstructed in place; the bytes equal klauspost's.
+func TestArenaInPlaceMatchesKlauspost(t *testing.T) {
+	svc := NewService().(*Service)
+	if svc.cpu != nil {
+		t.Skip("no MI355X visible")
+	}
+	ref, err := reedsolomon.New(config.K, config.M, reedsolomon.WithAutoGoroutines(runtime.NumCPU()))
+	if err != nil {
+		t.Fatal(err)
+	}
+	total := config.K + config.M
+	for _, n := range []int{1, 1001, 100 << 10, 1500 << 10} {
+		per := (n + config.K - 1) / config.K
+		arena, err := svc.NewArena(2 * total * (per + 16))
+		if err != nil {
+			t.Fatal(err)
+		}
+		value := make([]byte, n)
+		rand.New(rand.NewSource(int64(n))).Read(value)
+		shards := make([][]byte, total)
+		for i := range shards {
+			shards[i] = arena.Alloc(per)
+			if shards[i] == nil {
+				t.Fatal("arena full")
+			}
+			for j := range shards[i] {
+				shards[i][j] = 0
+			}
+			if lo := i * per; lo < n && i < config.K {
+				hi := lo + per
+				if hi > n {
+					hi = n
+				}
+				copy(shards[i], value[lo:hi])
+			}
+		}
+		want, _ := ref.Split(append([]byte(nil), value...))
+		if err := ref.Encode(want); err != nil {
+			t.Fatal(err)
+		}
+		if err := svc.Encode(shards); err != nil {
+			t.Fatal(err)
+		}
+		for i := range shards {
+			if !bytes.Equal(shards[i], want[i]) {
+				t.Fatalf("n=%d: shard %d differs from klauspost", n, i)
+			}
+		}
+		shards[0], shards[total-1] = shards[0][:0], shards[total-1][:0] // lost: capacity (arena) reused
+		if err := svc.Reconstruct(shards); err != nil {
+			t.Fatal(err)
+		}
+		for i := range shards {
+			if !bytes.Equal(shards[i], want[i]) {
+				t.Fatalf("n=%d: reconstructed shard %d differs", n, i)
+			}
+		}
+		arena.Close()
+	}
+}
