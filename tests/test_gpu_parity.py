@@ -35,6 +35,28 @@ def eng_for(engines, k, m):
     return engines[(k, m)]
 
 
+def _host_diff(got, want):
+    """'' when equal, else where a host-resident result differs (stripe / shard / byte
+    ranges, how many differing bytes are zero) and whether it still differs 20 ms
+    later: in-place zero-copy writes that land late vs bytes that are wrong."""
+    import time
+
+    def where():
+        bad = np.argwhere(got != want)
+        if bad.size == 0:
+            return ""
+        z = int((got[got != want] == 0).sum())
+        return (f"{len(bad)} bytes differ ({z} zero) in {np.unique(bad[:, 0]).size} stripes, "
+                f"shards {sorted(set(bad[:, 1].tolist()))}, bytes {bad[:, 2].min()}..{bad[:, 2].max()}, "
+                f"first {bad[:4].tolist()}")
+
+    d = where()
+    if d:
+        time.sleep(0.02)
+        d += " | after 20 ms: " + (where() or "equal")
+    return d
+
+
 # ---- per-object IEcDriver surface ------------------------------------------------
 @pytest.mark.parametrize("k,m", KM)
 @pytest.mark.parametrize("length", [1, 2, 3, 10, 410, 4096, 6554 * 4 + 3, 65536])
@@ -309,7 +331,7 @@ def test_batch_host_paths_match_device(engines, zero_copy):
         host[:, 0, :S] = 0
         host[:, 3, :S] = 0
         eng.reconstruct_host_unified(host, S, P, N, 0b110110)
-        assert np.array_equal(host[:, :, :S], orig[:, :, :S])
+        assert not _host_diff(host[:, :, :S], orig[:, :, :S]), _host_diff(host[:, :, :S], orig[:, :, :S])
         rng = np.random.default_rng(5)
         masks = np.array([0b111111 & ~(1 << rng.integers(0, 6)) for _ in range(N)], np.uint32)
         for i in range(N):
@@ -317,7 +339,7 @@ def test_batch_host_paths_match_device(engines, zero_copy):
                 if not (masks[i] >> j) & 1:
                     host[i, j, :S] = 0
         eng.reconstruct_host_unified(host, S, P, N, masks)
-        assert np.array_equal(host[:, :, :S], orig[:, :, :S])
+        assert not _host_diff(host[:, :, :S], orig[:, :, :S]), _host_diff(host[:, :, :S], orig[:, :, :S])
         assert eng.last_host_path() == ("zero-copy" if zero_copy else "staged")
     finally:
         eng.set_host_zero_copy(True)
@@ -525,13 +547,13 @@ def test_split_layout_host(engines, S, zero_copy):
         data[:, 1] = 0
         parity[:, 0] = 0
         eng.reconstruct_host(data, parity, S, N, 0b101101)
-        assert np.array_equal(data, d0) and np.array_equal(parity, p0)
+        assert not _host_diff(data, d0) and not _host_diff(parity, p0), (_host_diff(data, d0), _host_diff(parity, p0))
         masks = _masks_upto(rng, N, 6, 2)
         lost = ((masks[:, None] >> np.arange(6)[None, :]) & 1) == 0
         data[lost[:, :4]] = 0
         parity[lost[:, 4:]] = 0
         eng.reconstruct_host(data, parity, S, N, masks)
-        assert np.array_equal(data, d0) and np.array_equal(parity, p0)
+        assert not _host_diff(data, d0) and not _host_diff(parity, p0), (_host_diff(data, d0), _host_diff(parity, p0))
         # scrub, zero-copy or staged alike
         assert not eng.verify_host(data, parity, S, N).any()
         parity[17, 1, 3] ^= 4
