@@ -16,7 +16,10 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -138,6 +141,26 @@ class Service final : public IEcDriver {
       if (data_len > i * per)  // the payload's tail did not fill a whole shard
         std::copy(data.begin() + static_cast<std::ptrdiff_t>(i * per),
                   data.begin() + static_cast<std::ptrdiff_t>(data_len), pad->begin());
+      for (size_t j = 0; i + j < total; ++j) out->at(i + j) = Slice{pad->data() + j * per, per, per, pad};
+    }
+    return Error{};
+  }
+
+  // The same on a Go-style slice (e.g. a request body read into an Arena
+  // allocation): bytes [len, min(cap, (K+M)*perShard)) are zeroed and used for the
+  // shards that fit, exactly as Split(vector&) uses a vector's capacity.
+  Error Split(const Slice& data, Slices* out) {
+    if (data.empty()) return Error{RS_ERR_SHORT_DATA};
+    const size_t total = static_cast<size_t>(k_ + m_);
+    const size_t per = rs_shard_size(ctx_, data.len);
+    const size_t used = std::max(data.len, std::min(data.cap, total * per));
+    std::memset(data.p + data.len, 0, used - data.len);
+    out->assign(total, Slice{});
+    size_t i = 0;
+    for (; i < total && (i + 1) * per <= used; ++i) out->at(i) = Slice{data.p + i * per, per, per, data.owner};
+    if (i < total) {
+      auto pad = std::make_shared<std::vector<uint8_t>>((total - i) * per, 0);
+      if (data.len > i * per) std::copy(data.p + i * per, data.p + data.len, pad->begin());
       for (size_t j = 0; i + j < total; ++j) out->at(i + j) = Slice{pad->data() + j * per, per, per, pad};
     }
     return Error{};
@@ -272,6 +295,54 @@ class Service final : public IEcDriver {
   rs_ctx* ctx_;
   rs_coalescer* co_ = nullptr;
   int k_, m_;
+};
+
+// The Go shim's Arena (ec_gpu.go): slices backed by memory the context has
+// registered (rs_host_register), so a coalesced call whose shards -- read and
+// filled -- all come from an arena runs in place on the GPU: no staging copy of the
+// request body, parity written straight into the caller's slices.  Allocations are
+// 16-B aligned (the in-place kernel's condition); anything else is staged as usual.
+class Arena {
+ public:
+  static std::unique_ptr<Arena> New(const Service& svc, size_t size, Error* err = nullptr) {
+    const size_t n = (size + 4095) & ~size_t(4095);
+    void* p = n ? std::aligned_alloc(4096, n) : nullptr;
+    int rc = p ? rs_host_register(svc.ctx(), p, n) : RS_ERR_INVALID_ARG;
+    if (err) err->code = rc;
+    if (rc != RS_OK) {
+      std::free(p);
+      return nullptr;
+    }
+    return std::unique_ptr<Arena>(new Arena(svc.ctx(), static_cast<uint8_t*>(p), n));
+  }
+  ~Arena() {
+    rs_host_unregister(ctx_, base_);
+    std::free(base_);
+  }
+  Arena(const Arena&) = delete;
+  Arena& operator=(const Arena&) = delete;
+
+  // n bytes (len = cap = n), 16-B aligned; an empty slice when the arena is full.
+  Slice Alloc(size_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (n == 0 || n > size_ - off_) return Slice{};
+    Slice s{base_ + off_, n, n, nullptr};
+    off_ = std::min(size_, off_ + ((n + 15) & ~size_t(15)));
+    return s;
+  }
+  // Every earlier Alloc is invalid afterwards.
+  void Reset() {
+    std::lock_guard<std::mutex> g(mu_);
+    off_ = 0;
+  }
+  size_t Size() const { return size_; }
+
+ private:
+  Arena(rs_ctx* c, uint8_t* b, size_t n) : ctx_(c), base_(b), size_(n) {}
+  rs_ctx* ctx_;
+  uint8_t* base_;
+  size_t size_, off_ = 0;
+  std::mutex mu_;
 };
 
 }  // namespace ec

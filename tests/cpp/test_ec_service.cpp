@@ -229,6 +229,55 @@ static void test_encode_hash(ec::Service& co, ec::Service& plain) {
   CHECK(plain.EncodeHash(sh, v.size(), d).code == RS_ERR_NOT_SUPPORTED);
 }
 
+// The gateway's write and read paths on Arena memory (the Go shim's Arena): the
+// request body is read into an arena allocation with room for K+M shards, Split
+// carves every shard out of it, Encode writes the parity in place; a degraded read
+// refills two lost shards in their arena slots.  Shards 16-B aligned (shard sizes
+// that are multiples of 16) run on the in-place pointer-table kernel; others are
+// staged.  Bytes = the oracle's either way.
+static void test_arena_in_place(ec::Service& co) {
+  const size_t total = ec::K + ec::M;
+  ec::Error err;
+  auto arena = ec::Arena::New(co, 16u << 20, &err);
+  CHECK(arena != nullptr);
+  if (!arena) return;
+  for (size_t n : {4096ul, 102400ul, 1536000ul, 1001ul, 6ul}) {
+    arena->Reset();
+    const size_t per = (n + ec::K - 1) / ec::K;
+    const std::vector<uint8_t> value = rand_bytes(n * 17 + 5, n);
+    ec::Slice body = arena->Alloc(total * per);
+    CHECK(!body.empty());
+    if (body.empty()) return;
+    std::memset(body.p, 0xEE, body.cap);  // stale bytes past len: Split zeroes them
+    std::memcpy(body.p, value.data(), n);
+    body.len = n;
+    ec::Slices sh;
+    CHECK(!co.Split(body, &sh));
+    for (size_t i = 0; i < total; ++i) CHECK(sh[i].p == body.p + i * per && sh[i].len == per);
+    CHECK(!co.Encode(sh));
+    const bool in_place = per % 16 == 0;
+    const std::string k1 = rs_last_kernel(co.ctx());
+    CHECK((k1.find("apply_ptr_kernel") != std::string::npos) == in_place);
+    ec::Shards want;
+    CHECK(!co.Split(value.data(), value.size(), &want));
+    want = oracle_encode(ec::K, ec::M, want);
+    for (size_t i = 0; i < total; ++i) CHECK(std::equal(sh[i].p, sh[i].p + per, want[i].begin()));
+    ec::Slices got = sh;  // nodes 1 and 4 down: their arena slots are refilled in place
+    std::memset(got[1].p, 0x3C, per);
+    std::memset(got[4].p, 0x3C, per);
+    got[1].len = 0;
+    got[4].len = 0;
+    CHECK(!co.Reconstruct(got));
+    const std::string k2 = rs_last_kernel(co.ctx());
+    CHECK((k2.find("apply_ptr_kernel") != std::string::npos) == in_place);
+    for (size_t i = 0; i < total; ++i) {
+      CHECK(got[i].p == sh[i].p && got[i].len == per);
+      CHECK(std::equal(got[i].p, got[i].p + per, want[i].begin()));
+    }
+  }
+  CHECK(arena->Alloc(arena->Size() + 1).empty());
+}
+
 int main() {
   ec::Error err;
   auto svc = ec::Service::NewService(ec::K, ec::M, 0, &err);
@@ -254,6 +303,7 @@ int main() {
     test_concurrent(*co);
     test_split_spare_capacity(*co);
     test_encode_hash(*co, *svc);
+    test_arena_in_place(*co);
     uint64_t calls = 0, batches = 0, stripes = 0, maxb = 0;
     CHECK(rs_co_stats(co->coalescer(), &calls, &batches, &stripes, &maxb) == RS_OK);
     std::printf("coalescer: %llu calls, %llu batches, %llu stripes, largest batch %llu\n",
