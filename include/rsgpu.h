@@ -304,6 +304,16 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
  * range. */
 int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);
 int rs_host_unregister(rs_ctx *ctx, void *ptr);
+/* The same in-place eligibility on memory the context allocates itself:
+ * page-locked (hipHostMalloc, portable, on the first GPU's NUMA node when the
+ * runtime allows), GPU-mapped, page aligned.  Unlike a registered range of
+ * malloc'ed memory, whose pages the OS may still migrate or compact (amdgpu maps
+ * registered user memory without pinning it for life), these pages stay put, so an
+ * arena of long-lived request / shard buffers is best taken from here (the Go
+ * shim's and the C++ mirror's Arena do).  rs_host_free only pointers rs_host_alloc
+ * returned, when no call is using them; rs_destroy frees any left. */
+int rs_host_alloc(rs_ctx *ctx, size_t bytes, void **out);
+int rs_host_free(rs_ctx *ctx, void *ptr);
 
 /* ---- measurement helpers (bench.py) ------------------------------------- */
 /* Name of the kernel the last batched call on this context launched. */

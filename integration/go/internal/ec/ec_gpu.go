@@ -404,8 +404,9 @@ func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 	return errs
 }
 
-// Arena hands out []byte backed by C memory the engine has registered
-// (rs_host_register): a call whose shards -- those it reads and those it fills --
+// Arena hands out []byte backed by page-locked C memory the engine owns
+// (rs_host_alloc; registered for in-place calls like rs_host_register'ed memory,
+// but pinned for life, so the OS cannot migrate its pages under a call): a call whose shards -- those it reads and those it fills --
 // all come from an arena runs in place on the GPU, with no staging copy of the
 // request body and the parity written straight into the caller's slices
 // (DESIGN.md §6, "In place on registered buffers").  Meant for buffers the service
@@ -421,18 +422,14 @@ type Arena struct {
 	off  int
 }
 
-// NewArena registers `size` bytes of C memory for in-place calls.
+// NewArena allocates `size` bytes of page-locked memory for in-place calls.
 func (s *Service) NewArena(size int) (*Arena, error) {
 	if s.cpu != nil || size <= 0 {
 		return nil, nil
 	}
 	n := (size + 4095) &^ 4095
-	p := C.aligned_alloc(4096, C.size_t(n))
-	if p == nil {
-		return nil, errors.New("rsgpu: arena allocation failed")
-	}
-	if rc := C.rs_host_register(s.ctx, p, C.size_t(n)); rc != C.RS_OK {
-		C.free(p)
+	var p unsafe.Pointer
+	if rc := C.rs_host_alloc(s.ctx, C.size_t(n), &p); rc != C.RS_OK {
 		return nil, toErr(rc)
 	}
 	return &Arena{ctx: s.ctx, base: p, size: n}, nil
@@ -462,11 +459,10 @@ func (a *Arena) Reset() {
 	}
 }
 
-// Close unregisters and frees the arena (no call may be using it).
+// Close frees the arena (no call may be using it).
 func (a *Arena) Close() {
 	if a != nil && a.base != nil {
-		C.rs_host_unregister(a.ctx, a.base)
-		C.free(a.base)
+		C.rs_host_free(a.ctx, a.base)
 		a.base = nil
 	}
 }

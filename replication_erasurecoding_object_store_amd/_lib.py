@@ -84,6 +84,8 @@ SIGNATURES = {
     "rs_co_encode_hash_many": (_i, [_vp, _sz, _u8pp, _szp, _szp, _u8p, ctypes.POINTER(_i)]),
     "rs_host_register": (_i, [_vp, _vp, _sz]),
     "rs_host_unregister": (_i, [_vp, _vp]),
+    "rs_host_alloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
+    "rs_host_free": (_i, [_vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
     "rs_device_copy": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "rs_set_blocks_per_cu": (_i, [_vp, _i]),

@@ -213,6 +213,16 @@ class BatchEngine(Service):
     def host_unregister(self, arr: np.ndarray) -> None:
         _check(_lib.lib().rs_host_unregister(self.ctx, arr.ctypes.data))
 
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """Page-locked host memory owned by the context (rs_host_alloc) as a uint8
+        array; free with host_free before the engine closes (or let close free it)."""
+        p = ctypes.c_void_p()
+        _check(_lib.lib().rs_host_alloc(self.ctx, nbytes, ctypes.byref(p)))
+        return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
+
+    def host_free(self, arr: np.ndarray) -> None:
+        _check(_lib.lib().rs_host_free(self.ctx, arr.ctypes.data))
+
     # ---- measurement helpers ----------------------------------------------------------
     def device_copy(self, dst, src, nbytes: Optional[int] = None, stream=None) -> None:
         n = nbytes if nbytes is not None else src.numel() * src.element_size()

@@ -367,6 +367,7 @@ using rs::Engine;
 struct RegRange {
   uintptr_t lo = 0, hi = 0;  // [lo, hi)
   uint8_t* dev = nullptr;     // GPU address of lo (portable mapping: every device)
+  bool owned = false;         // rs_host_alloc'ed (freed by rs_host_free / rs_destroy)
 };
 
 struct rs_ctx {
@@ -1272,7 +1273,15 @@ int rs_create_multi(int k, int m, uint64_t device_mask, int flags, rs_ctx** out)
   return rs_create_devices(k, m, devs.data(), static_cast<int>(devs.size()), flags, out);
 }
 
-void rs_destroy(rs_ctx* ctx) { delete ctx; }
+void rs_destroy(rs_ctx* ctx) {
+  if (!ctx) return;
+  if (!ctx->engines.empty()) {
+    DeviceScope ds(ctx->engines[0]->device);
+    for (const RegRange& r : ctx->reg)  // rs_host_alloc'ed memory never freed by the caller
+      if (r.owned) rs::pinned_free(reinterpret_cast<void*>(r.lo));
+  }
+  delete ctx;
+}
 
 int rs_data_shards(const rs_ctx* c) { return c ? c->k : 0; }
 int rs_parity_shards(const rs_ctx* c) { return c ? c->m : 0; }
@@ -1545,6 +1554,27 @@ static int sync_stream(rs_ctx* c, void* stream, bool release) {
 int rs_sync(rs_ctx* c, void* stream) { return sync_stream(c, stream, false); }
 int rs_stream_release(rs_ctx* c, void* stream) { return sync_stream(c, stream, true); }
 
+namespace {
+void reg_insert(rs_ctx* c, const RegRange& r) {
+  std::unique_lock<std::shared_mutex> g(c->reg_mu);
+  auto it = std::lower_bound(c->reg.begin(), c->reg.end(), r.lo,
+                             [](const RegRange& a, uintptr_t lo) { return a.lo < lo; });
+  c->reg.insert(it, r);
+  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+}
+
+// Removes the range starting at ptr if its ownership matches; false if none does.
+bool reg_erase(rs_ctx* c, void* ptr, bool owned) {
+  std::unique_lock<std::shared_mutex> g(c->reg_mu);
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+  auto it = std::find_if(c->reg.begin(), c->reg.end(), [&](const RegRange& r) { return r.lo == lo; });
+  if (it == c->reg.end() || it->owned != owned) return false;
+  c->reg.erase(it);
+  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+  return true;
+}
+}  // namespace
+
 // Pins for every GPU of the process (portable) and maps into their address spaces;
 // the range is remembered so coalesced calls on buffers inside it run in place.
 int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
@@ -1557,27 +1587,51 @@ int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
     (void)hipHostUnregister(ptr);
     return RS_ERR_DEVICE;
   }
-  const RegRange r{reinterpret_cast<uintptr_t>(ptr), reinterpret_cast<uintptr_t>(ptr) + bytes,
-                   static_cast<uint8_t*>(dev)};
-  std::unique_lock<std::shared_mutex> g(c->reg_mu);
-  auto it = std::lower_bound(c->reg.begin(), c->reg.end(), r.lo,
-                             [](const RegRange& a, uintptr_t lo) { return a.lo < lo; });
-  c->reg.insert(it, r);
-  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+  reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(ptr), reinterpret_cast<uintptr_t>(ptr) + bytes,
+                         static_cast<uint8_t*>(dev), false});
   return RS_OK;
 }
+
 
 int rs_host_unregister(rs_ctx* c, void* ptr) {
   if (!c || !ptr) return RS_ERR_INVALID_ARG;
   {
-    std::unique_lock<std::shared_mutex> g(c->reg_mu);
-    const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
-    auto it = std::find_if(c->reg.begin(), c->reg.end(), [&](const RegRange& r) { return r.lo == lo; });
-    if (it != c->reg.end()) c->reg.erase(it);
-    c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+    std::shared_lock<std::shared_mutex> g(c->reg_mu);
+    for (const RegRange& r : c->reg)
+      if (r.lo == reinterpret_cast<uintptr_t>(ptr) && r.owned) return RS_ERR_INVALID_ARG;  // rs_host_free's
   }
+  (void)reg_erase(c, ptr, false);
   DeviceScope ds(c->engines[0]->device);
   RS_HIP(hipHostUnregister(ptr));
+  return RS_OK;
+}
+
+int rs_host_alloc(rs_ctx* c, size_t bytes, void** out) {
+  if (!c || !out || bytes == 0) return RS_ERR_INVALID_ARG;
+  *out = nullptr;
+  Engine* e = c->engines[0].get();
+  DeviceScope ds(e->device);
+  if (!ds.ok()) return RS_ERR_DEVICE;
+  const size_t n = round_up(bytes, 4096);
+  void* p = rs::pinned_alloc(n, e->numa);
+  if (!p) return RS_ERR_DEVICE;
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+    (void)hipGetLastError();
+    rs::pinned_free(p);
+    return RS_ERR_DEVICE;
+  }
+  reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + n,
+                         static_cast<uint8_t*>(dev), true});
+  *out = p;
+  return RS_OK;
+}
+
+int rs_host_free(rs_ctx* c, void* ptr) {
+  if (!c || !ptr) return RS_ERR_INVALID_ARG;
+  if (!reg_erase(c, ptr, true)) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(c->engines[0]->device);
+  rs::pinned_free(ptr);
   return RS_OK;
 }
 

@@ -297,8 +297,9 @@ class Service final : public IEcDriver {
   int k_, m_;
 };
 
-// The Go shim's Arena (ec_gpu.go): slices backed by memory the context has
-// registered (rs_host_register), so a coalesced call whose shards -- read and
+// The Go shim's Arena (ec_gpu.go): slices backed by page-locked memory the
+// context owns (rs_host_alloc, eligible for in-place calls like rs_host_register'ed
+// memory and pinned for life), so a coalesced call whose shards -- read and
 // filled -- all come from an arena runs in place on the GPU: no staging copy of the
 // request body, parity written straight into the caller's slices.  Allocations are
 // 16-B aligned (the in-place kernel's condition); anything else is staged as usual.
@@ -306,19 +307,13 @@ class Arena {
  public:
   static std::unique_ptr<Arena> New(const Service& svc, size_t size, Error* err = nullptr) {
     const size_t n = (size + 4095) & ~size_t(4095);
-    void* p = n ? std::aligned_alloc(4096, n) : nullptr;
-    int rc = p ? rs_host_register(svc.ctx(), p, n) : RS_ERR_INVALID_ARG;
+    void* p = nullptr;
+    const int rc = n ? rs_host_alloc(svc.ctx(), n, &p) : RS_ERR_INVALID_ARG;
     if (err) err->code = rc;
-    if (rc != RS_OK) {
-      std::free(p);
-      return nullptr;
-    }
+    if (rc != RS_OK) return nullptr;
     return std::unique_ptr<Arena>(new Arena(svc.ctx(), static_cast<uint8_t*>(p), n));
   }
-  ~Arena() {
-    rs_host_unregister(ctx_, base_);
-    std::free(base_);
-  }
+  ~Arena() { rs_host_free(ctx_, base_); }
   Arena(const Arena&) = delete;
   Arena& operator=(const Arena&) = delete;
 

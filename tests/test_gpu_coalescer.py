@@ -441,15 +441,18 @@ def test_async_submit_reap_matches_oracle(gpu, k, m):
         svc.close()
 
 
-@pytest.mark.parametrize("k,m,S", [(4, 2, 100000), (10, 4, 6554), (4, 2, 1001), (8, 4, 384000), (6, 3, 777)])
-def test_registered_buffers_run_in_place(gpu, k, m, S):
+@pytest.mark.parametrize("k,m,S,mem", [(4, 2, 100000, "register"), (10, 4, 6554, "register"), (4, 2, 1001, "register"),
+                                       (8, 4, 384000, "register"), (6, 3, 777, "register"),
+                                       (4, 2, 100000, "alloc"), (10, 4, 6554, "alloc")])
+def test_registered_buffers_run_in_place(gpu, k, m, S, mem):
     """Objects whose shards lie in rs_host_register'ed memory (request bodies and
     storage-node reads in a pinned arena) are encoded and
     reconstructed by the coalescer in place -- the pointer-table kernel reads and
     writes the caller's buffers, nothing is staged -- with the oracle's bytes and no
     byte outside [0, S) of any shard written; pageable objects join the same
     batches (staged); after rs_host_unregister the same calls are staged again.
-    Asynchronous calls run in place too (nothing left to copy at reap)."""
+    Asynchronous calls run in place too (nothing left to copy at reap).  mem="alloc":
+    the same on context-owned page-locked memory (rs_host_alloc)."""
     import ctypes
     import mmap
 
@@ -459,10 +462,18 @@ def test_registered_buffers_run_in_place(gpu, k, m, S):
     t = k + m
     n_obj = 24
     P = (S + 15) // 16 * 16 + 48  # 16-B aligned shards, guard bytes between them
-    region = mmap.mmap(-1, n_obj * t * P + 4096)
-    arr = np.frombuffer(region, np.uint8)
+    nbytes = n_obj * t * P + 4096
+    svc = CoalescingService(k, m, max_wait_us=3000)
+    if mem == "alloc":
+        p = ctypes.c_void_p()
+        assert L.rs_host_alloc(svc._ctx, nbytes, ctypes.byref(p)) == 0
+        base = p.value
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(base))
+    else:
+        region = mmap.mmap(-1, nbytes)
+        arr = np.frombuffer(region, np.uint8)
+        base = ctypes.addressof(ctypes.c_uint8.from_buffer(region))
     arr[:] = 0xA5
-    base = ctypes.addressof(ctypes.c_uint8.from_buffer(region))
     rng = np.random.default_rng(k * 1000 + S)
     data = rng.integers(0, 256, (n_obj, k, S), dtype=np.uint8)
     want = np.zeros((n_obj, t, S), np.uint8)
@@ -477,11 +488,11 @@ def test_registered_buffers_run_in_place(gpu, k, m, S):
     def ptrs(i):
         return (_lib._u8p * t)(*[ctypes.cast(base + (i * t + s) * P, _lib._u8p) for s in range(t)])
 
-    svc = CoalescingService(k, m, max_wait_us=3000)
     registered = False
     try:
-        assert L.rs_host_register(svc._ctx, base, len(region)) == 0
-        registered = True
+        if mem == "register":
+            assert L.rs_host_register(svc._ctx, base, nbytes) == 0
+            registered = True
         for i in range(n_obj):
             for c in range(k):
                 view(i, c)[:] = data[i, c]
@@ -539,6 +550,11 @@ def test_registered_buffers_run_in_place(gpu, k, m, S):
         for i in range(n_obj * t):
             assert (arr[i * P + S:(i + 1) * P] == 0xA5).all(), ("guard", i)
         assert (arr[n_obj * t * P:] == 0xA5).all()
+        if mem == "alloc":
+            assert L.rs_host_unregister(svc._ctx, base) == _lib.RS_ERR_INVALID_ARG  # rs_host_free's
+            assert L.rs_host_free(svc._ctx, base + 16) == _lib.RS_ERR_INVALID_ARG  # not an allocation
+            assert L.rs_host_free(svc._ctx, base) == 0
+            return
         # unregistered: the same memory is staged, same bytes
         assert L.rs_host_unregister(svc._ctx, base) == 0
         registered = False

@@ -523,6 +523,42 @@ def test_split_layout_device(engines, k, m, S):
         assert torch.equal(p2[:, :, :S], parity[:, :, :S])
 
 
+def test_host_alloc_batches_zero_copy(engines):
+    """Host batches in context-owned page-locked memory (rs_host_alloc): zero-copy,
+    oracle bytes for encode, a uniform and a per-stripe reconstruct; the pointer is
+    rs_host_free's alone (rs_host_unregister refuses it)."""
+    from replication_erasurecoding_object_store_amd import _lib
+
+    k, m, S, N = 4, 2, 1024, 3000
+    eng = eng_for(engines, k, m)
+    buf = eng.host_alloc(N * (k + m) * S)
+    try:
+        data = buf[:N * k * S].reshape(N, k, S)
+        parity = buf[N * k * S:].reshape(N, m, S)
+        data[:] = np.random.default_rng(77).integers(0, 256, (N, k, S), dtype=np.uint8)
+        parity[:] = 0
+        eng.encode_host(data, parity, S, N)
+        assert eng.last_host_path() == "zero-copy"
+        uni = np.concatenate([data, np.zeros_like(parity)], axis=1).copy()
+        rs_oracle.encode_batch_scalar(k, m, uni.reshape(-1), (k + m) * S, S, S, N)
+        assert not _host_diff(parity, uni[:, k:]), _host_diff(parity, uni[:, k:])
+        d0, p0 = data.copy(), parity.copy()
+        data[:, 2] = 0
+        parity[:, 1] = 0
+        eng.reconstruct_host(data, parity, S, N, 0b011011)
+        assert not _host_diff(data, d0) and not _host_diff(parity, p0), (_host_diff(data, d0), _host_diff(parity, p0))
+        masks = _masks_upto(np.random.default_rng(78), N, 6, 2)
+        lost = ((masks[:, None] >> np.arange(6)[None, :]) & 1) == 0
+        data[lost[:, :4]] = 0
+        parity[lost[:, 4:]] = 0
+        eng.reconstruct_host(data, parity, S, N, masks)
+        assert eng.last_host_path() == "zero-copy"
+        assert not _host_diff(data, d0) and not _host_diff(parity, p0), (_host_diff(data, d0), _host_diff(parity, p0))
+        assert _lib.lib().rs_host_unregister(eng.ctx, buf.ctypes.data) == _lib.RS_ERR_INVALID_ARG
+    finally:
+        eng.host_free(buf)
+
+
 @pytest.mark.parametrize("zero_copy", [True, False])
 @pytest.mark.parametrize("S", [1024, 1000])
 def test_split_layout_host(engines, S, zero_copy):

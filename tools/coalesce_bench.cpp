@@ -103,7 +103,9 @@ int main(int argc, char** argv) {
   // REGISTER=1: every object's shards live in one rs_host_register'ed arena (the
   // gateway's request bodies / the healer's shard buffers in a pinned arena), so
   // coalesced calls run in place (no staging copies); else per-shard heap vectors.
-  const bool reg = std::getenv("REGISTER") && std::atoi(std::getenv("REGISTER")) != 0;
+  // REGISTER=2: the arena comes from rs_host_alloc (context-owned page-locked memory).
+  const int reg_mode = std::getenv("REGISTER") ? std::atoi(std::getenv("REGISTER")) : 0;
+  const bool reg = reg_mode != 0;
   const size_t SP = (S + 63) / 64 * 64;
   const size_t per_thread = async_mode ? static_cast<size_t>(depth)
                                        : std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
@@ -111,8 +113,15 @@ int main(int argc, char** argv) {
   size_t arena_bytes = 0;
   if (reg) {
     arena_bytes = static_cast<size_t>(T) * per_thread * (k + m) * SP;
-    arena = static_cast<uint8_t*>(std::aligned_alloc(4096, (arena_bytes + 4095) / 4096 * 4096));
-    if (!arena || rs_host_register(ctx, arena, arena_bytes) != RS_OK) {
+    void* p = nullptr;
+    if (reg_mode == 2) {
+      if (rs_host_alloc(ctx, arena_bytes, &p) != RS_OK) p = nullptr;
+      arena = static_cast<uint8_t*>(p);
+    } else {
+      arena = static_cast<uint8_t*>(std::aligned_alloc(4096, (arena_bytes + 4095) / 4096 * 4096));
+      if (arena && rs_host_register(ctx, arena, arena_bytes) != RS_OK) arena = nullptr;  // (leaks: exits)
+    }
+    if (!arena) {
       std::fprintf(stderr, "REGISTER: arena of %zu bytes failed\n", arena_bytes);
       return 1;
     }
@@ -287,11 +296,15 @@ int main(int argc, char** argv) {
       n_ops / dt, n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
-      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20, reg ? 1 : 0);
+      async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20, reg_mode);
   if (co) rs_coalescer_destroy(co);
   if (arena) {
-    rs_host_unregister(ctx, arena);
-    std::free(arena);
+    if (reg_mode == 2) {
+      rs_host_free(ctx, arena);
+    } else {
+      rs_host_unregister(ctx, arena);
+      std::free(arena);
+    }
   }
   if (enc_plan) rso_baseline_plan_free(enc_plan);
   for (void* pl : rec_plan)
