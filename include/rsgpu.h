@@ -294,9 +294,10 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
 /* ---- host memory helpers ------------------------------------------------ */
 /* Pins [ptr, ptr + bytes) for every GPU of the process (DMA + zero-copy) and
  * remembers the range: a coalesced call (rs_co_encode / rs_co_reconstruct, their
- * _submit_ and _many forms; not the _hash or _data forms) whose shards -- the ones
- * it reads and the ones it fills -- all lie inside one registered range, 16-B
- * aligned, runs in place: the kernel reads the caller's shards and writes the
+ * _submit_ and _many forms, and the _hash forms when the data shards holding the
+ * value are contiguous -- shard c at shard 0 + c*S, as Split carves them; not the
+ * _data form) whose shards -- the ones it reads and the ones it fills -- all lie
+ * inside one registered range, 16-B aligned, runs in place: the kernel reads the caller's shards and writes the
  * parity / missing shards straight into the caller's buffers over PCIe, with no
  * staging copy either way (the request body and the HTTP send
  * buffers, or a healer's shard buffers, in a registered arena).  Such a call writes

@@ -967,6 +967,25 @@ bool direct_ptrs(rs_coalescer* co, uint8_t* const* shards, size_t S, uint32_t to
   return first != 0;
 }
 
+// cold_hash of a direct encode reads the value in place: possible when the data
+// shards holding its first value_len bytes are contiguous (shard c at shard 0 + c*S,
+// as Split carves them from one body; with 16-B aligned shards S is then a multiple
+// of 16, so the hash kernel's shard pitch b->P equals S).
+bool hash_in_place_ok(uint8_t* const* shards, size_t S, uint64_t value_len) {
+  const uint64_t n = (value_len + S - 1) / S;
+  for (uint64_t c = 1; c < n; ++c)
+    if (shards[c] != shards[0] + c * S) return false;
+  return true;
+}
+
+// The hash request of a direct slot: its value starts at the GPU address dev0 (the
+// kernel adds the offset to the batch's data base in 64-bit wrap-around arithmetic).
+void set_hash_direct(Batch* b, size_t slot, uint64_t value_len, uint64_t dev0) {
+  reinterpret_cast<uint64_t*>(host_at(b, b->o_hlen))[slot] = value_len;
+  reinterpret_cast<uint64_t*>(host_at(b, b->o_hoff))[slot] = dev0 - reinterpret_cast<uint64_t>(b->host_dev + b->o_data);
+  b->hash_in.store(1, std::memory_order_relaxed);
+}
+
 // A direct slot: its row = the caller's buffers; nothing is copied.
 void direct_fill(const rs_coalescer* co, Batch* b, size_t slot, const uint64_t* dev, uint32_t present) {
   const int t = co->k + co->m;
@@ -1134,13 +1153,15 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
-  // every shard in registered memory (and no cold_hash, which reads the staging):
-  // the kernel reads the data and writes the parity in place
+  // every shard in registered memory (a cold_hash's value contiguous in it): the
+  // kernels read the data and write the parity in place
   uint64_t dev[32];
-  const bool direct = !hash && direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev);
+  const bool direct =
+      direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev) && (!hash || hash_in_place_ok(shards, S, value_len));
   auto fill = [&](Batch* b, size_t slot) {
     if (direct) {
       direct_fill(co, b, slot, dev, data_mask);
+      if (hash) set_hash_direct(b, slot, value_len, dev[0]);
       return;
     }
     for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
@@ -1347,26 +1368,42 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
     if (rc == RS_OK && m > 0) by_len[S].push_back(i);
   }
   const uint32_t data_mask = (1u << k) - 1u;
+  // objects whose shards are all registered run in place (as rs_co_encode's)
+  std::vector<uint64_t> devs(co->direct_ok ? n_objects * t : 0);
+  std::vector<uint8_t> direct(n_objects, 0);
+  for (auto& g : by_len)
+    for (size_t i : g.second)
+      direct[i] = co->direct_ok && direct_ptrs(co, shards + i * t, g.first, (1u << t) - 1u, &devs[i * t]) &&
+                  (!hash || hash_in_place_ok(shards + i * t, g.first, value_lens[i]));
   for (auto& g : by_len) {
     const std::vector<size_t>& idx = g.second;
     const size_t S = g.first;
     const int rc = submit_many(
         co, Kind::kApply, S, idx.size(), false,
         [&](Batch* b, size_t slot, size_t j) {
-          uint8_t* const* sh = shards + idx[j] * t;
+          const size_t i = idx[j];
+          if (direct[i]) {
+            direct_fill(co, b, slot, &devs[i * t], data_mask);
+            if (hash) set_hash_direct(b, slot, value_lens[i], devs[i * t]);
+            return;
+          }
+          uint8_t* const* sh = shards + i * t;
           for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
-          set_hash(b, k, slot, hash ? value_lens[idx[j]] : rs::kSha256Skip);
+          set_hash(b, k, slot, hash ? value_lens[i] : rs::kSha256Skip);
           if (co->per_stripe) {
             reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
             note_missing(b, static_cast<uint32_t>(m));
+            stage_ptrs(co, b, slot, data_mask);  // a direct slot may share the batch
           } else {
             set_plan(co, b, slot, data_mask, false, true);
           }
         },
         [&](Batch* b, size_t slot, size_t j) {
-          uint8_t* const* sh = shards + idx[j] * t;
-          for (int r = 0; r < m; ++r) std::memcpy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
-          if (hash) std::memcpy(digests + idx[j] * 32, host_at(b, b->o_digest + slot * 32), 32);
+          const size_t i = idx[j];
+          uint8_t* const* sh = shards + i * t;
+          if (!direct[i])
+            for (int r = 0; r < m; ++r) std::memcpy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+          if (hash) std::memcpy(digests + i * 32, host_at(b, b->o_digest + slot * 32), 32);
         });
     if (rc) {
       for (size_t i : idx) rcs[i] = rc;

@@ -569,3 +569,100 @@ def test_registered_buffers_run_in_place(gpu, k, m, S, mem):
         if registered:
             L.rs_host_unregister(svc._ctx, base)
         svc.close()
+
+
+@pytest.mark.parametrize("k,m,S", [(4, 2, 25600), (10, 4, 1024)])
+def test_in_place_calls_share_batches_with_staged_many_forms(gpu, k, m, S):
+    """In-place objects (context-owned pinned memory, each object's K+M shards
+    contiguous as Split carves them from one body) and staged objects of the same
+    shard length in the same device batches: rs_co_encode_hash (in place, cold_hash
+    read where the value lies) and rs_co_encode_hash_many / rs_co_encode_many on
+    pageable objects from concurrent threads.  Every staged slot of a batch that runs
+    the pointer-table kernel must carry its own pointer row; parity = the oracle's,
+    digests = hashlib's, for every object."""
+    import ctypes
+    import hashlib
+
+    from replication_erasurecoding_object_store_amd import _lib
+
+    L = _lib.lib()
+    t = k + m
+    n_obj = 48
+    svc = CoalescingService(k, m, max_wait_us=2000)
+    p = ctypes.c_void_p()
+    assert L.rs_host_alloc(svc._ctx, n_obj * t * S, ctypes.byref(p)) == 0
+    base = p.value
+    arena = np.ctypeslib.as_array((ctypes.c_uint8 * (n_obj * t * S)).from_address(base))
+    try:
+        rng = np.random.default_rng(k * 7 + S)
+        vlen = [int(rng.integers(1, k * S + 1)) for _ in range(n_obj)]
+        values = [rng.integers(0, 256, v, dtype=np.uint8).tobytes() for v in vlen]
+        want = []
+        for i in range(n_obj):  # Split into the arena: body = object i's region
+            body = arena[i * t * S:(i + 1) * t * S]
+            body[:] = 0
+            body[:vlen[i]] = np.frombuffer(values[i], np.uint8)
+            sh = [bytearray(body[c * S:(c + 1) * S].tobytes()) for c in range(k)] + [bytearray(S) for _ in range(m)]
+            assert rs_oracle.encode(k, m, sh) == 0
+            want.append([bytes(x) for x in sh])
+
+        def ptrs(i):
+            return (_lib._u8p * t)(*[ctypes.cast(base + (i * t + s) * S, _lib._u8p) for s in range(t)])
+
+        lens = (ctypes.c_size_t * t)(*([S] * t))
+
+        def in_place(tid):
+            for i in range(tid, n_obj, 16):
+                dig = (ctypes.c_uint8 * 32)()
+                assert L.rs_co_encode_hash(svc._co, ptrs(i), lens, vlen[i], dig) == 0
+                assert bytes(dig) == hashlib.sha256(values[i]).digest(), ("in place digest", i)
+
+        def staged_many(tid):
+            objs = [[bytearray(want[i][c]) if c < k else bytearray(S) for c in range(t)]
+                    for i in range(tid, n_obj, 4)]
+            idx = list(range(tid, n_obj, 4))
+            keep = [(ctypes.c_uint8 * S).from_buffer(b) for o in objs for b in o]
+            sp = (_lib._u8p * (len(objs) * t))(*[ctypes.cast(x, _lib._u8p) for x in keep])
+            ls = (ctypes.c_size_t * (len(objs) * t))(*([S] * (len(objs) * t)))
+            rcs = (ctypes.c_int * len(objs))()
+            if tid % 2:
+                assert L.rs_co_encode_many(svc._co, len(objs), sp, ls, rcs) == 0
+            else:
+                vl = (ctypes.c_size_t * len(objs))(*[vlen[i] for i in idx])
+                digs = (ctypes.c_uint8 * (32 * len(objs)))()
+                assert L.rs_co_encode_hash_many(svc._co, len(objs), sp, ls, vl, digs, rcs) == 0
+                for j, i in enumerate(idx):
+                    assert bytes(digs[32 * j:32 * j + 32]) == hashlib.sha256(values[i]).digest(), ("many digest", i)
+            assert list(rcs) == [0] * len(objs)
+            for j, i in enumerate(idx):
+                assert [bytes(x) for x in objs[j]] == want[i], ("staged many parity", i)
+
+        _run_threads(20, lambda tid: in_place(tid) if tid < 16 else staged_many(tid - 16))
+        for i in range(n_obj):
+            for s in range(t):
+                got = arena[(i * t + s) * S:(i * t + s + 1) * S].tobytes()
+                assert got == want[i][s], ("in place parity", i, s)
+        # the in-place forms of the _many calls too: every object in the arena
+        for i in range(n_obj):
+            arena[(i * t + k) * S:(i + 1) * t * S] = 0
+        sp = (_lib._u8p * (n_obj * t))(*[ctypes.cast(base + j * S, _lib._u8p) for j in range(n_obj * t)])
+        ls = (ctypes.c_size_t * (n_obj * t))(*([S] * (n_obj * t)))
+        vl = (ctypes.c_size_t * n_obj)(*vlen)
+        digs = (ctypes.c_uint8 * (32 * n_obj))()
+        rcs = (ctypes.c_int * n_obj)()
+        assert L.rs_co_encode_hash_many(svc._co, n_obj, sp, ls, vl, digs, rcs) == 0
+        assert "apply_ptr_kernel" in L.rs_last_kernel(svc._ctx).decode()
+        for i in range(n_obj):
+            assert bytes(digs[32 * i:32 * i + 32]) == hashlib.sha256(values[i]).digest()
+            for s in range(t):
+                assert arena[(i * t + s) * S:(i * t + s + 1) * S].tobytes() == want[i][s]
+        # a value whose data shards are not contiguous is hashed from the staging
+        dig = (ctypes.c_uint8 * 32)()
+        order = [1, 0] + list(range(2, t))  # (a ctypes pointer-array swap would alias)
+        swapped = (_lib._u8p * t)(*[ctypes.cast(base + order[s] * S, _lib._u8p) for s in range(t)])
+        v2 = arena[S:2 * S].tobytes() + arena[0:S].tobytes()
+        assert L.rs_co_encode_hash(svc._co, swapped, lens, 2 * S, dig) == 0
+        assert bytes(dig) == hashlib.sha256(v2).digest()
+    finally:
+        assert L.rs_host_free(svc._ctx, base) == 0
+        svc.close()
