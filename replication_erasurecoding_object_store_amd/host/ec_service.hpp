@@ -238,6 +238,20 @@ class Service final : public IEcDriver {
     return Error{rs_co_encode_hash(co_, p.data(), n.data(), value_len, digest)};
   }
 
+  // The same on Go-style slices: Split(const Slice&) of an Arena body gives
+  // contiguous data shards, so the batch hashes the value where it lies (in place).
+  Error EncodeHash(Slices& shards, size_t value_len, uint8_t digest[32]) {
+    if (!co_) return Error{RS_ERR_NOT_SUPPORTED};
+    if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};
+    std::vector<uint8_t*> p(shards.size());
+    std::vector<size_t> n(shards.size());
+    for (size_t i = 0; i < shards.size(); ++i) {
+      p[i] = shards[i].p;
+      n[i] = shards[i].len;
+    }
+    return Error{rs_co_encode_hash(co_, p.data(), n.data(), value_len, digest)};
+  }
+
   // [upstream Verify]
   Error Verify(const Shards& shards, bool* ok) {
     if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};

@@ -254,7 +254,10 @@ static void test_arena_in_place(ec::Service& co) {
     ec::Slices sh;
     CHECK(!co.Split(body, &sh));
     for (size_t i = 0; i < total; ++i) CHECK(sh[i].p == body.p + i * per && sh[i].len == per);
-    CHECK(!co.Encode(sh));
+    uint8_t digest[32], want_digest[32];
+    CHECK(!co.EncodeHash(sh, n, digest));  // writeservice.go:222 + :267 in one batch
+    rso_sha256(value.data(), n, want_digest);
+    CHECK(std::memcmp(digest, want_digest, 32) == 0);
     const bool in_place = per % 16 == 0;
     const std::string k1 = rs_last_kernel(co.ctx());
     CHECK((k1.find("apply_ptr_kernel") != std::string::npos) == in_place);
