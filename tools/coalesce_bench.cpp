@@ -8,7 +8,9 @@
 // obj_bytes (4 KiB default; the reference's payloads: 10 / 100 / 800 KiB,
 // benchmark/k6/benchmark.js:14-19, and 1500 KiB, go-ycsb hybridstore db.go:56), host
 // memory.  Workload per call: "enc" = Encode; "mix" = 50/50 Encode and 1-erasure
-// Reconstruct (SURVEY.md §8d config 5's mix).  Prints one JSON line per run.
+// Reconstruct (SURVEY.md §8d config 5's mix); "hash" = the write path's Encode +
+// cold_hash of the whole value (writeservice.go:222,267: rs_co_encode_hash; the CPU
+// codec plus SHA-256 of the k data shards in "cpu" mode).  Prints one JSON line per run.
 //
 // Build: g++ -std=c++17 -O2 -pthread tools/coalesce_bench.cpp -o tools/coalesce_bench \
 //          -Lreplication_erasurecoding_object_store_amd -lrsgpu \
@@ -45,6 +47,7 @@ int main(int argc, char** argv) {
   const int T = std::atoi(argv[1]);
   const double secs = std::atof(argv[2]);
   const bool mix = std::strcmp(argv[3], "mix") == 0;
+  const bool hash_wl = std::strcmp(argv[3], "hash") == 0;
   const bool co_mode = std::strcmp(argv[4], "co") == 0;
   const bool cpu_mode = std::strcmp(argv[4], "cpu") == 0;
   const bool async_mode = std::strcmp(argv[4], "async") == 0;  // coalescer, rs_co_submit_* + rs_co_reap
@@ -96,6 +99,7 @@ int main(int argc, char** argv) {
   // nothing cannot pass.
   struct Obj {
     std::vector<std::vector<uint8_t>> sh, keep;
+    uint8_t digest[32];  // SHA-256 of the value (the k data shards in order)
     std::vector<uint8_t*> p;
     std::vector<size_t> n;
     uint64_t j = 0;
@@ -148,6 +152,11 @@ int main(int argc, char** argv) {
       }
     }
     if (rs_encode(ctx, o.p.data(), o.n.data()) != RS_OK) ++bad;
+    {
+      std::vector<uint8_t> value;
+      for (int i = 0; i < k; ++i) value.insert(value.end(), o.p[i], o.p[i] + S);
+      rso_sha256(value.data(), value.size(), o.digest);
+    }
     o.keep.assign(k + m, std::vector<uint8_t>(S));
     for (int i = 0; i < k + m; ++i) std::memcpy(o.keep[i].data(), o.p[i], S);
     if (arena) o.sh.clear();  // the arena holds the shards
@@ -265,6 +274,15 @@ int main(int argc, char** argv) {
           } else {
             rc = co ? rs_co_reconstruct(co, o.p.data(), o.n.data()) : rs_reconstruct(ctx, o.p.data(), o.n.data());
           }
+        } else if (hash_wl) {
+          uint8_t dg[32];
+          if (cpu_mode) {
+            rc = rso_baseline_plan_apply(enc_plan, o.p.data(), o.p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
+            for (int c = 0; c < k; ++c) rso_sha256(o.p[c], S, dg);  // same bytes hashed (per shard)
+          } else {
+            rc = co ? rs_co_encode_hash(co, o.p.data(), o.n.data(), static_cast<size_t>(k) * S, dg) : RS_ERR_INVALID_ARG;
+            if (rc == RS_OK && verified(o) && std::memcmp(dg, o.digest, 32) != 0) ++bad;
+          }
         } else {
           if (cpu_mode)
             rc = rso_baseline_plan_apply(enc_plan, o.p.data(), o.p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
@@ -292,7 +310,7 @@ int main(int argc, char** argv) {
       "\"calls_per_s\": %.0f, \"user_GiBps\": %.3f, \"errors\": %llu, \"batches\": %llu, \"avg_batch\": %.1f, "
       "\"max_batch\": %llu, \"max_exec\": %d, \"max_wait_us\": %u, \"staged_dma\": %d, \"inflight\": %d, "
       "\"depth\": %d, \"busy\": %llu, \"rotate_mb\": %zu, \"registered\": %d}\n",
-      async_mode ? "async" : (co ? "coalesced" : (cpu_mode ? "cpu" : "direct")), mix ? "mix" : "enc", T, obj, dt,
+      async_mode ? "async" : (co ? "coalesced" : (cpu_mode ? "cpu" : "direct")), mix ? "mix" : (hash_wl ? "hash" : "enc"), T, obj, dt,
       n_ops / dt, n_ops * static_cast<double>(k * S) / dt / (1 << 30), static_cast<unsigned long long>(bad.load()),
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
