@@ -291,47 +291,46 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 	return nil
 }
 
-// EncodeHash is Encode plus the write path's cold_hash in the same GPU batch:
-// WriteEC splits and encodes `value` (writeservice.go:218-222) and later stores
-// computeSHA256Hex(value) (:267; hybrid writes :326, :382-386).  The data shards of
-// Split(value) are the value followed by zero padding, so the SHA-256 of their
-// first valueLen = len(value) bytes is that hash; the engine computes it over the
-// shards it has already staged for the encode (rs_co_encode_hash).  Not part of
-// IEcDriver: a caller type-asserts for
+// EncodeHash is Encode plus the write path's cold_hash: WriteEC splits and encodes
+// `value` (writeservice.go:218-222) and later stores computeSHA256Hex(value) (:267;
+// hybrid writes :326, :382-386).  The data shards of Split(value) are the value
+// followed by zero padding, so the SHA-256 of their first valueLen = len(value)
+// bytes is that hash.  It is computed here with Go's crypto/sha256 (SHA-NI on amd64,
+// the reference's own code) while the GPU encodes.  SHA-256 is sequential within a
+// message: one GPU lane hashes ~30-40 MB/s against ~2 GB/s for a SHA-NI core, so
+// the engine's digest (rs_co_encode_hash) pays only with thousands of values per
+// launch (rs_co_encode_hash_many, rs_sha256_batch); per object it cut this path
+// from 4-40 GiB/s to 0.5 GiB/s (DESIGN.md §6).  Not part of IEcDriver: a caller
+// type-asserts for
 //   interface{ EncodeHash([][]byte, int) ([32]byte, error) }
 // and keeps Encode + computeSHA256Hex otherwise.
 func (s *Service) EncodeHash(shards [][]byte, valueLen int) (sum [32]byte, err error) {
-	if s.cpu != nil {
-		if err = s.cpu.Encode(shards); err != nil {
-			return sum, err
-		}
-		h := sha256.New()
-		rem := valueLen
-		for i := 0; i < config.K && rem > 0; i++ {
-			n := min(rem, len(shards[i]))
-			h.Write(shards[i][:n])
-			rem -= n
-		}
-		if rem > 0 {
-			return sum, errors.New(C.GoString(C.rs_strerror(C.RS_ERR_INVALID_ARG)))
-		}
-		copy(sum[:], h.Sum(nil))
-		return sum, nil
-	}
-	if len(shards) != config.K+config.M {
+	if len(shards) < config.K {
 		return sum, reedsolomon.ErrTooFewShards
 	}
-	var pin runtime.Pinner
-	defer pin.Unpin()
-	p, l, free := shardArgs(shards, &pin)
-	defer free()
-	d := (*[32]C.uint8_t)(C.malloc(32))
-	defer C.free(unsafe.Pointer(d))
-	if err = toErr(C.rs_co_encode_hash(s.co, p, l, C.size_t(valueLen), &d[0])); err != nil {
-		return sum, err
+	rem := valueLen
+	for i := 0; i < config.K && rem > 0; i++ {
+		rem -= min(rem, len(shards[i]))
 	}
-	for i := range sum {
-		sum[i] = byte(d[i])
+	if rem > 0 {
+		return sum, errors.New(C.GoString(C.rs_strerror(C.RS_ERR_INVALID_ARG)))
+	}
+	done := make(chan struct{})
+	go func() { // reads the data shards only, as the encode does
+		h := sha256.New()
+		left := valueLen
+		for i := 0; i < config.K && left > 0; i++ {
+			n := min(left, len(shards[i]))
+			h.Write(shards[i][:n])
+			left -= n
+		}
+		copy(sum[:], h.Sum(nil))
+		close(done)
+	}()
+	err = s.Encode(shards) // the GPU (klauspost on a GPU-less host)
+	<-done
+	if err != nil {
+		return [32]byte{}, err
 	}
 	return sum, nil
 }

@@ -224,8 +224,11 @@ class Service final : public IEcDriver {
 
   // Encode plus the write path's cold_hash (writeservice.go:222 and :267,
   // computeSHA256Hex(value) :51-54) in one coalesced GPU batch: digest = SHA-256 of
-  // the first value_len bytes of data shards 0..K-1 (the Split input).  The Go
-  // shim's EncodeHash; needs the coalescing service (RS_ERR_NOT_SUPPORTED without).
+  // the first value_len bytes of data shards 0..K-1 (the Split input); needs the
+  // coalescing service (RS_ERR_NOT_SUPPORTED without).  The GPU digest is one lane
+  // per object (rs_co_encode_hash): it pays for bulk loads of many small values, not
+  // per request -- the Go shim's EncodeHash hashes on the CPU while the GPU encodes
+  // (rsgpu.h).
   Error EncodeHash(Shards& shards, size_t value_len, uint8_t digest[32]) {
     if (!co_) return Error{RS_ERR_NOT_SUPPORTED};
     if (static_cast<int>(shards.size()) != k_ + m_) return Error{RS_ERR_TOO_FEW_SHARDS};

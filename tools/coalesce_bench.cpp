@@ -278,7 +278,9 @@ int main(int argc, char** argv) {
           uint8_t dg[32];
           if (cpu_mode) {
             rc = rso_baseline_plan_apply(enc_plan, o.p.data(), o.p.data() + k, S) >= 0 ? RS_OK : RS_ERR_DEVICE;
-            for (int c = 0; c < k; ++c) rso_sha256(o.p[c], S, dg);  // same bytes hashed (per shard)
+            // SHA-NI on this thread (Go's crypto/sha256 class of code), the same bytes
+            // hashed shard by shard
+            for (int c = 0; c < k; ++c) rso_baseline_sha256_batch(o.p[c], 0, S, 1, dg, 1);
           } else {
             rc = co ? rs_co_encode_hash(co, o.p.data(), o.n.data(), static_cast<size_t>(k) * S, dg) : RS_ERR_INVALID_ARG;
             if (rc == RS_OK && verified(o) && std::memcmp(dg, o.digest, 32) != 0) ++bad;

@@ -16,9 +16,10 @@ Q=${Q:-16}
 CPUS=$(tools/gpu_local_cpus.sh $Q)
 PIN="taskset -c $CPUS"
 export ROTATE_MB=1024
-for OBJ in ${SIZES:-102400 819200 1536000}; do
+for OBJ in ${SIZES:-4096 10240 102400 819200 1536000}; do
   run taskset -c ${CPUS%%-*} $B 1 2 hash cpu 0 0 $OBJ
   for R in 0 2; do
     REGISTER=$R run $PIN $B 64 2 hash co 0 0 $OBJ
+    REGISTER=$R run $PIN $B 64 2 enc co 0 0 $OBJ
   done
 done
