@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--workloads", default="all")
     ap.add_argument("--pads", default="0", help="comma-separated extra bytes added to the shard pitch "
                                                 "(multiples of 16), each its own workload line")
+    ap.add_argument("--out-rows", default="full", choices=["full", "dense", "both"],
+                    help="out-of-place outputs: m rows per stripe (full), or only the launch's erasure "
+                         "bound (dense: a bounded 1-erasure launch writes stripe after stripe back to back)")
     ap.add_argument("--parity-pad", action="store_true",
                     help="rs_set_parity_pad_writes(1): encode writes parity padding to the next 128-B line")
     args = ap.parse_args()
@@ -116,6 +119,14 @@ def main():
         workloads = {(f"{n}+{pad}" if pad else n): (*w, pad) for n, w in workloads.items() for pad in pads}
     else:
         workloads = {n: (*w, 0) for n, w in workloads.items()}
+    bounded_rows = {"rec1pb_out": 1, "rec1d0b_out": 1, "rec1p13b_out": 1, "rec2pb_out": 2}
+    if args.out_rows != "full":
+        dense = {f"{n}+dense": w for n, w in workloads.items() if w[4] in bounded_rows}
+        if args.out_rows == "dense":
+            workloads = dense
+        else:
+            workloads = {kk: vv for n, w in workloads.items() for kk, vv in
+                         ([(n, w)] + ([(f"{n}+dense", w)] if w[4] in bounded_rows else []))}
     for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
@@ -146,8 +157,9 @@ def main():
         m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
         md0 = torch.full((N,), ((1 << t) - 1) & ~1, dtype=torch.int32, device="cuda")
         mp13 = torch.full((N,), ((1 << t) - 1) & ~(1 << (t - 1)), dtype=torch.int32, device="cuda")
-        outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
-        alg = alg_bytes(name.split("+")[0])
+        rows = bounded_rows[mode] if name.endswith("+dense") else m
+        outs = [torch.empty((N, rows, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
+        alg = alg_bytes(name.split("+")[0])  # "+<pad>" / "+dense" variants move the same bytes
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
         def run(i):
