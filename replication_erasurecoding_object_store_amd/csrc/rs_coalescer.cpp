@@ -1026,7 +1026,7 @@ void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, 
     if (!it.lens[i]) continue;
     ++staged;
     uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P) : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
-    std::memcpy(dst, it.shards[i], it.S);
+    rs::stage_copy(dst, it.shards[i], it.S);
   }
   if (co->per_stripe) {
     reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
@@ -1043,7 +1043,7 @@ void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it,
   for (int i = 0; i < t; ++i) {
     if (it.lens[i]) continue;
     if (!data_only || i < k) {
-      if (!it.direct) std::memcpy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
+      if (!it.direct) rs::stage_copy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
       it.lens[i] = it.S;  // direct: the kernel wrote the caller's buffer
     }
     ++r;
@@ -1164,7 +1164,7 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
       if (hash) set_hash_direct(b, slot, value_len, dev[0]);
       return;
     }
-    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
     set_hash(b, k, slot, value_len);
     if (co->per_stripe) {
       reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
@@ -1176,7 +1176,7 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
   };
   auto drain = [&](Batch* b, size_t slot) {
     if (!direct)
-      for (int r = 0; r < m; ++r) std::memcpy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+      for (int r = 0; r < m; ++r) rs::stage_copy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
     if (hash) std::memcpy(digest, host_at(b, b->o_digest + slot * 32), 32);
   };
   return submit(co, Kind::kApply, S, false, fill, drain);
@@ -1211,8 +1211,8 @@ int rs_co_verify(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, i
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   auto fill = [&](Batch* b, size_t slot) {
-    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    for (int r = 0; r < m; ++r) std::memcpy(host_at(b, b->o_parity + (slot * m + r) * b->P), shards[k + r], S);
+    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    for (int r = 0; r < m; ++r) rs::stage_copy(host_at(b, b->o_parity + (slot * m + r) * b->P), shards[k + r], S);
   };
   auto drain = [&](Batch* b, size_t slot) { *ok = reinterpret_cast<uint32_t*>(host_at(b, b->o_bad))[slot] == 0; };
   return submit(co, Kind::kVerify, S, true, fill, drain);
@@ -1241,7 +1241,7 @@ int rs_co_submit_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* 
       direct_fill(co, b, slot, dev, data_mask);
       return;
     }
-    for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
     set_hash(b, k, slot, rs::kSha256Skip);
     if (co->per_stripe) {
       reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
@@ -1290,7 +1290,7 @@ int rs_co_reap(rs_coalescer* co, uint64_t* tags, int* rcs, int max, int timeout_
         const AsyncRec& r = b->arec[j];
         if (brc == RS_OK) {
           for (uint32_t o = 0; o < r.n_out; ++o)
-            std::memcpy(r.out[o], host_at(b, b->o_out + (static_cast<size_t>(r.slot) * m + o) * b->P), b->S);
+            rs::stage_copy(r.out[o], host_at(b, b->o_out + (static_cast<size_t>(r.slot) * m + o) * b->P), b->S);
         }
         tags[got] = r.tag;
         rcs[got] = brc;
@@ -1388,7 +1388,7 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
             return;
           }
           uint8_t* const* sh = shards + i * t;
-          for (int c = 0; c < k; ++c) std::memcpy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
+          for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
           set_hash(b, k, slot, hash ? value_lens[i] : rs::kSha256Skip);
           if (co->per_stripe) {
             reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
@@ -1402,7 +1402,7 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
           const size_t i = idx[j];
           uint8_t* const* sh = shards + i * t;
           if (!direct[i])
-            for (int r = 0; r < m; ++r) std::memcpy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+            for (int r = 0; r < m; ++r) rs::stage_copy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
           if (hash) std::memcpy(digests + i * 32, host_at(b, b->o_digest + slot * 32), 32);
         });
     if (rc) {
