@@ -634,7 +634,12 @@ def test_reconstruct_out_of_place(engines, k, m, S):
         else:
             eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
             eng.sync()
-        torch.cuda.synchronize()
+        # a device fault is reported asynchronously: name the mode whose launch preceded it
+        try:
+            torch.cuda.synchronize()
+            _ = out[0, 0, 0].item()
+        except Exception as exc:
+            raise AssertionError(f"device error after mode {mode} ({eng.last_kernel()}): {exc}") from exc
         assert torch.equal(data, d0) and torch.equal(parity, p0), "inputs must be read-only"
         got = out.cpu().numpy()
         ref = full.cpu().numpy()
