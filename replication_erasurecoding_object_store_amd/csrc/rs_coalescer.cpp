@@ -996,6 +996,31 @@ void direct_fill(const rs_coalescer* co, Batch* b, size_t slot, const uint64_t* 
   b->direct_in.store(1, std::memory_order_relaxed);
 }
 
+// One encode slot (rs_co_encode / _hash / _submit_encode / _many): in place through
+// the caller's addresses when `dev` is set, else its data shards staged, its mask
+// (or plan) and pointer row written -- every staged slot needs the row, since an
+// in-place slot may make the batch run the pointer-table kernel.  value_len:
+// kSha256Skip for no cold_hash.
+void encode_fill(const rs_coalescer* co, Batch* b, size_t slot, uint8_t* const* shards, size_t S,
+                 const uint64_t* dev, uint64_t value_len) {
+  const int k = co->k, m = co->m;
+  const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
+  if (dev) {
+    direct_fill(co, b, slot, dev, data_mask);
+    if (value_len != rs::kSha256Skip) set_hash_direct(b, slot, value_len, dev[0]);
+    return;
+  }
+  for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+  set_hash(b, k, slot, value_len);
+  if (co->per_stripe) {
+    reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
+    note_missing(b, static_cast<uint32_t>(m));
+    stage_ptrs(co, b, slot, data_mask);
+  } else {
+    set_plan(co, b, slot, data_mask, false, true);
+  }
+}
+
 // Decides whether a reconstruct runs in place (Reconstruct only: ReconstructData
 // leaves missing parity unwritten and may pass no buffer for it).
 void rec_direct(rs_coalescer* co, RecItem* it, bool data_only) {
@@ -1152,28 +1177,12 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
   for (int i = 0; i < k + m; ++i)
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
-  const uint32_t data_mask = (1u << k) - 1u;  // parity all missing -> encode rows
   // every shard in registered memory (a cold_hash's value contiguous in it): the
   // kernels read the data and write the parity in place
   uint64_t dev[32];
   const bool direct =
       direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev) && (!hash || hash_in_place_ok(shards, S, value_len));
-  auto fill = [&](Batch* b, size_t slot) {
-    if (direct) {
-      direct_fill(co, b, slot, dev, data_mask);
-      if (hash) set_hash_direct(b, slot, value_len, dev[0]);
-      return;
-    }
-    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    set_hash(b, k, slot, value_len);
-    if (co->per_stripe) {
-      reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
-      note_missing(b, static_cast<uint32_t>(m));
-      stage_ptrs(co, b, slot, data_mask);
-    } else {
-      set_plan(co, b, slot, data_mask, false, true);
-    }
-  };
+  auto fill = [&](Batch* b, size_t slot) { encode_fill(co, b, slot, shards, S, direct ? dev : nullptr, value_len); };
   auto drain = [&](Batch* b, size_t slot) {
     if (!direct)
       for (int r = 0; r < m; ++r) rs::stage_copy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
@@ -1229,7 +1238,6 @@ int rs_co_submit_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* 
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (m == 0) return RS_ERR_NOT_SUPPORTED;  // nothing to compute, nothing would be reaped
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
-  const uint32_t data_mask = (1u << k) - 1u;
   uint64_t dev[32];
   const bool direct = direct_ptrs(co, shards, S, (1u << (k + m)) - 1u, dev);  // in place: nothing to copy back
   AsyncRec rec;
@@ -1237,19 +1245,7 @@ int rs_co_submit_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* 
   rec.n_out = direct ? 0u : static_cast<uint32_t>(m);
   for (int r = 0; r < m; ++r) rec.out[r] = shards[k + r];
   auto fill = [&](Batch* b, size_t slot) {
-    if (direct) {
-      direct_fill(co, b, slot, dev, data_mask);
-      return;
-    }
-    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    set_hash(b, k, slot, rs::kSha256Skip);
-    if (co->per_stripe) {
-      reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
-      note_missing(b, static_cast<uint32_t>(m));
-      stage_ptrs(co, b, slot, data_mask);
-    } else {
-      set_plan(co, b, slot, data_mask, false, true);
-    }
+    encode_fill(co, b, slot, shards, S, direct ? dev : nullptr, rs::kSha256Skip);
   };
   return submit_async(co, Kind::kApply, S, false, fill, rec);
 }
@@ -1367,7 +1363,6 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
     rcs[i] = rc;
     if (rc == RS_OK && m > 0) by_len[S].push_back(i);
   }
-  const uint32_t data_mask = (1u << k) - 1u;
   // objects whose shards are all registered run in place (as rs_co_encode's)
   std::vector<uint64_t> devs(co->direct_ok ? n_objects * t : 0);
   std::vector<uint8_t> direct(n_objects, 0);
@@ -1382,21 +1377,8 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
         co, Kind::kApply, S, idx.size(), false,
         [&](Batch* b, size_t slot, size_t j) {
           const size_t i = idx[j];
-          if (direct[i]) {
-            direct_fill(co, b, slot, &devs[i * t], data_mask);
-            if (hash) set_hash_direct(b, slot, value_lens[i], devs[i * t]);
-            return;
-          }
-          uint8_t* const* sh = shards + i * t;
-          for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), sh[c], S);
-          set_hash(b, k, slot, hash ? value_lens[i] : rs::kSha256Skip);
-          if (co->per_stripe) {
-            reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
-            note_missing(b, static_cast<uint32_t>(m));
-            stage_ptrs(co, b, slot, data_mask);  // a direct slot may share the batch
-          } else {
-            set_plan(co, b, slot, data_mask, false, true);
-          }
+          encode_fill(co, b, slot, shards + i * t, S, direct[i] ? &devs[i * t] : nullptr,
+                      hash ? value_lens[i] : rs::kSha256Skip);
         },
         [&](Batch* b, size_t slot, size_t j) {
           const size_t i = idx[j];
