@@ -12,5 +12,6 @@ cp "$SRC" $C/_ab_kernels.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result "$@" -c $C/_ab_kernels.hip -o /tmp/_ab_$NAME.o
 rm -f $C/_ab_kernels.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -o abx/$NAME.so /tmp/_ab_$NAME.o \
-  $C/build/rs_sha256.hip.o $C/build/rs_engine.cpp.o $C/build/rs_coalescer.cpp.o $C/build/gf256.cpp.o
+  $C/build/rs_sha256.hip.o $C/build/rs_engine.cpp.o $C/build/rs_coalescer.cpp.o $C/build/gf256.cpp.o \
+  $C/build/rs_host_copy.cpp.o
 echo "abx/$NAME.so"
