@@ -59,8 +59,8 @@ def _shard_array(shards: Sequence[Optional[bytearray]], S: int, fill_missing: bo
                 keep.append(buf)
                 ptrs[i] = ctypes.cast(buf, _lib._u8p)
             continue
-        if not isinstance(sh, bytearray):
-            raise TypeError("shards must be bytearray (mutable, like Go []byte) or None")
+        if not isinstance(sh, (bytearray, memoryview)) or (isinstance(sh, memoryview) and sh.readonly):
+            raise TypeError("shards must be bytearray or a writable memoryview (mutable, like Go []byte) or None")
         buf = (ctypes.c_uint8 * len(sh)).from_buffer(sh)
         keep.append(buf)
         ptrs[i] = ctypes.cast(buf, _lib._u8p)
@@ -164,6 +164,10 @@ class Service:
     def ReconstructData(self, shards: List[Optional[bytearray]]) -> None:
         self._reconstruct(shards, data_only=True)
 
+    def NewArena(self, size: int) -> "Arena":
+        """Page-locked memory for in-place calls (the Go shim's NewArena)."""
+        return Arena(self, size)
+
     def Verify(self, shards: List[bytearray]) -> bool:
         if len(shards) != self.k + self.m:
             raise ECError(ErrTooFewShards)
@@ -172,6 +176,38 @@ class Service:
         _check(self._call("verify", ptrs, lens, ctypes.byref(ok)))
         del keep
         return bool(ok.value)
+
+
+class Arena:
+    """The Go shim's Arena (ec_gpu.go): page-locked memory the context owns
+    (rs_host_alloc).  Alloc(n) hands out writable memoryviews, 16-B aligned; a
+    coalesced call whose shards all come from an arena runs in place on the GPU (no
+    staging copies, parity written straight into the views).  A bump allocator:
+    Alloc until full, Reset when no view is in use, Close to free."""
+
+    def __init__(self, svc: "Service", size: int):
+        n = (size + 4095) // 4096 * 4096
+        p = ctypes.c_void_p()
+        _check(_lib.lib().rs_host_alloc(svc.ctx, n, ctypes.byref(p)))
+        self._svc, self._base, self._size, self._off = svc, p.value, n, 0
+        self._mem = (ctypes.c_uint8 * n).from_address(p.value)
+
+    def Alloc(self, n: int) -> Optional[memoryview]:
+        off = (self._off + 15) // 16 * 16
+        if n <= 0 or self._base is None or off + n > self._size:
+            return None
+        self._off = off + n
+        return memoryview(self._mem).cast("B")[off:off + n]
+
+    def Reset(self) -> None:
+        self._off = 0
+
+    def Close(self) -> None:
+        """Frees the memory (no view may be in use); after the service closed,
+        rs_destroy has freed it already."""
+        if self._base is not None and self._svc.ctx:
+            _check(_lib.lib().rs_host_free(self._svc.ctx, self._base))
+        self._base, self._mem = None, None
 
 
 def NewService(k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0) -> Service:

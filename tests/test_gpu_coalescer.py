@@ -666,3 +666,40 @@ def test_in_place_calls_share_batches_with_staged_many_forms(gpu, k, m, S):
     finally:
         assert L.rs_host_free(svc._ctx, base) == 0
         svc.close()
+
+
+def test_python_arena_encode_in_place(gpu):
+    """The Python mirror's Arena (Service.NewArena, rs_host_alloc): Split's shards
+    copied into arena views, Encode runs in place (pointer-table kernel), parity
+    lands in the views; a degraded read with the survivors in the arena repairs the
+    lost shards; oracle bytes throughout."""
+    from replication_erasurecoding_object_store_amd import _lib
+
+    k, m = 4, 2
+    svc = CoalescingService(k, m, max_wait_us=200)
+    arena = svc.NewArena(8 << 20)
+    try:
+        for n in (4096, 102400, 1001):
+            arena.Reset()
+            value = xoshiro_bytes(n, n)
+            ref = rs_oracle.split(k, m, value)
+            assert rs_oracle.encode(k, m, ref) == 0
+            S = len(ref[0])
+            views = [arena.Alloc(S) for _ in range(k + m)]
+            for i in range(k):
+                views[i][:] = ref[i]
+            svc.Encode(views)
+            # every view starts 16-B aligned: in place whatever S is (S = 251 for 1001 B)
+            assert "apply_ptr_kernel" in _lib.lib().rs_last_kernel(svc.ctx).decode()
+            assert [bytes(v) for v in views] == [bytes(r) for r in ref]
+            got = list(views)
+            got[1] = None
+            got[5] = None
+            svc.Reconstruct(got)
+            assert [bytes(g) for g in got] == [bytes(r) for r in ref]
+        assert arena.Alloc(16 << 20) is None
+        with pytest.raises(TypeError):
+            svc.Encode([bytes(8)] * (k + m))  # read-only buffers are refused
+    finally:
+        arena.Close()
+        svc.close()
