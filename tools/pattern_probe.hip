@@ -155,6 +155,25 @@ __global__ __launch_bounds__(256) void pD(Geo g) {
   }
 }
 
+// G: 1 KiB tasks over PAIRS of stripes -- lane l owns column c of stripe 2p and
+// the same column of stripe 2p+1 (32 B per lane, as a bitsliced encode needs,
+// without C's 2 KiB-wide rows: the encode matrix is the same for every stripe).
+template <int K, int M>
+__global__ __launch_bounds__(256) void pG(Geo g) {
+  const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4, bps = (g.cols + 63) / 64, pairs = (g.N + 1) / 2, tasks = pairs * bps;
+  for (uint32_t t = wave; t < tasks; t += nw) {
+    const uint32_t sp = t / bps, b = t - sp * bps, col = b * 64 + lane;
+    const uint32_t sa = 2 * sp, sb = 2 * sp + 1 < g.N ? 2 * sp + 1 : 2 * sp;
+    u32x4 xa[K], xb[K];
+    uint32_t oa, ob;
+    task_load<K, M>(g, sa, col, xa, &oa);
+    task_load<K, M>(g, sb, col, xb, &ob);
+    task_store<K, M>(g, sa, col, oa, xa);
+    task_store<K, M>(g, sb, col, ob, xb);
+  }
+}
+
 template <int K, int M>
 __global__ __launch_bounds__(256) void pE(Geo g) {
   const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
@@ -575,6 +594,42 @@ static void launch_run(void* a) {
   CHECK(hipLaunchKernel(r->fn, dim3(r->grid), dim3(256), args, 0, nullptr));
 }
 
+// B (1 KiB tasks), C (2 KiB-wide tasks) and G (1 KiB tasks over stripe pairs), two
+// passes in alternating order.
+template <int K, int M>
+static void geometry_pairs(int cus, uint32_t S, uint32_t N) {
+  const uint32_t P = (S + 255) / 256 * 256;
+  Geo g[2];
+  for (auto& x : g) {
+    uint8_t *d, *p;
+    CHECK(hipMalloc(&d, (size_t)N * K * P));
+    CHECK(hipMalloc(&p, (size_t)N * M * P));
+    fill(d, (size_t)N * K * P);
+    x = Geo{d, p, N, S, P, (S + 15) / 16, S / 16, S / 16};
+  }
+  const double alg = (double)N * S * (K + M);
+  struct V {
+    const char* name;
+    const void* fn;
+  } vs[] = {{"B bufdrop 1KiB", (const void*)&pB<K, M>},
+            {"C bufdrop 2KiB", (const void*)&pC<K, M>},
+            {"G stripe-pair 1KiB", (const void*)&pG<K, M>}};
+  for (int pass = 0; pass < 2; ++pass)
+    for (int i = 0; i < 3; ++i) {
+      const V& v = vs[pass ? 2 - i : i];
+      for (int bpc : {2, 4}) {
+        Run r{v.fn, {g[0], g[1]}, (uint32_t)(cus * bpc), 0};
+        const float ms = time_it(launch_run, &r, 20);
+        std::printf("RS(%d+%d) S=%u P=%u  %-18s bpc=%d  %7.1f GB/s  (%.1f%% of 8 TB/s)\n", K, M, S, P, v.name, bpc,
+                    alg / ms / 1e6, alg / ms / 1e6 / 80.0);
+      }
+    }
+  for (auto& x : g) {
+    CHECK(hipFree(const_cast<uint8_t*>(x.d)));
+    CHECK(hipFree(x.p));
+  }
+}
+
 template <int K, int M>
 static void geometry(int cus, uint32_t S, uint32_t N, uint32_t pitch = 0, bool only_b = false) {
   const uint32_t P = pitch ? pitch : (S + 255) / 256 * 256;
@@ -659,6 +714,13 @@ int main(int argc, char** argv) {
       compute_geometry<10, 4, 4>(cus, 6554, 16384);
     }
     geometry<10, 4>(cus, 6656, 16384, 0, true);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'P') {  // stripe-pair tasks vs 1 KiB and 2 KiB tasks
+    geometry_pairs<8, 4>(cus, 8192, 16384);
+    geometry_pairs<10, 4>(cus, 6656, 16384);
+    geometry_pairs<10, 4>(cus, 6554, 16384);
+    geometry_pairs<4, 2>(cus, 16384, 16384);
     return 0;
   }
   if (argc > 1 && argv[1][0] == 'g') {
