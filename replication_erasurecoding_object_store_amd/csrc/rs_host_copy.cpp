@@ -8,7 +8,6 @@
 #include <cstdlib>
 #include <cstring>
 
-
 namespace rs {
 
 void stage_copy(void* dst, const void* src, size_t n);  // rs_host_util.hpp
@@ -63,4 +62,5 @@ void stage_copy(void* dst, const void* src, size_t n) {
   else
     std::memcpy(dst, src, n);
 }
+
 }  // namespace rs
