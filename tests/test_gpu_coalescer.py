@@ -443,7 +443,9 @@ def test_async_submit_reap_matches_oracle(gpu, k, m):
 
 @pytest.mark.parametrize("k,m,S,mem", [(4, 2, 100000, "register"), (10, 4, 6554, "register"), (4, 2, 1001, "register"),
                                        (8, 4, 384000, "register"), (6, 3, 777, "register"),
-                                       (4, 2, 100000, "alloc"), (10, 4, 6554, "alloc")])
+                                       (4, 2, 100000, "alloc"), (10, 4, 6554, "alloc"),
+                                       # tiny shards: partial first column, byte-exact stores
+                                       (4, 2, 1, "alloc"), (4, 2, 3, "alloc"), (10, 4, 17, "register")])
 def test_registered_buffers_run_in_place(gpu, k, m, S, mem):
     """Objects whose shards lie in rs_host_register'ed memory (request bodies and
     storage-node reads in a pinned arena) are encoded and
