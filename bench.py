@@ -469,6 +469,13 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             e2.set_parity_pad_writes(False)
         timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"])
         timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+        if SS % 128:
+            # rs_set_out_pad_writes: output rows end on whole 128-B lines (the outputs
+            # are the bench's own, full-pitch rows); bytes counted stay N*S*(K+e)
+            e2.set_out_pad_writes(True)
+            timed("reconstruct2_out_pad", lambda i: w.rec(i, bound=2), alg["reconstruct"])
+            timed("reconstruct1_out_pad", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+            e2.set_out_pad_writes(False)
         if mm > 2:
             timed("reconstruct2_unbounded", w.rec, alg["reconstruct"])
             timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])

@@ -337,6 +337,13 @@ int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
  * [0, S) are unchanged; the padding then holds the code of the data padding.
  * 0 (the default): no byte past S of any slot is ever written. */
 int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
+/* The same for the out-of-place reconstructs (rs_reconstruct_batch_out and its
+ * _devmask form): each output row written gets its padding up to the next 128-B
+ * line, bytes [S, min(pitch, round_up(S, 128))) of the row at out + i*out_sp +
+ * r*pitch (the caller's output allocation must cover them), and the inputs' padding
+ * is read over the same range.  Bytes [0, S) are unchanged.  0 (the default): no
+ * byte past S of an output row is written. */
+int rs_set_out_pad_writes(rs_ctx *ctx, int enable);
 /* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or
  * rs_host_register) and 16-B aligned run zero-copy by default: the kernel reads
  * the survivors and writes the missing shards across PCIe in place.  0 forces

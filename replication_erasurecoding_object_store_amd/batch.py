@@ -240,6 +240,11 @@ class BatchEngine(Service):
     def set_blocks_per_cu(self, n: int) -> None:
         _check(_lib.lib().rs_set_blocks_per_cu(self.ctx, n))
 
+    def set_out_pad_writes(self, enable: bool) -> None:
+        """Out-of-place reconstructs may write each output row's padding up to the
+        next 128-B line (rsgpu.h)."""
+        _check(_lib.lib().rs_set_out_pad_writes(self.ctx, 1 if enable else 0))
+
     def set_parity_pad_writes(self, enable: bool) -> None:
         """Encode may write parity slot padding up to the next 128-B line (rsgpu.h)."""
         _check(_lib.lib().rs_set_parity_pad_writes(self.ctx, 1 if enable else 0))

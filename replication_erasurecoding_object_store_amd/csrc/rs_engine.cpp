@@ -273,6 +273,7 @@ struct Engine {
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
+  bool out_pad = false;                   // out-of-place outputs likewise (rs_set_out_pad_writes)
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -571,8 +572,9 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  if (e->parity_pad && a.data_inputs && !a.out) {
-    // rs_set_parity_pad_writes: run encode over whole 128-B lines of the slot
+  if ((e->parity_pad && a.data_inputs && !a.out) || (e->out_pad && a.out)) {
+    // rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
+    // the slot (inputs' padding read, the written rows' padding written)
     const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
     if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
       a.shard_len = static_cast<uint32_t>(s_eff);
@@ -1695,6 +1697,12 @@ const char* rs_last_host_path(const rs_ctx* c) { return c ? c->shared.last_host_
 int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->parity_pad = enable != 0;
+  return RS_OK;
+}
+
+int rs_set_out_pad_writes(rs_ctx* c, int enable) {
+  if (!c) return RS_ERR_INVALID_ARG;
+  for (auto& e : c->engines) e->out_pad = enable != 0;
   return RS_OK;
 }
 

@@ -209,3 +209,41 @@ def test_out_of_place_stress(engines, k, m, S, bound):
                 if len(unused):
                     assert (got[unused, r] == 0xC3).all(), (mode, trial, r, "unused output slot written")
             assert (got[:, :, S:] == 0xC3).all(), "output padding written"
+
+
+@pytest.mark.parametrize("k,m,S,bound", [(10, 4, 6554, 1), (10, 4, 6554, 2), (10, 4, 6554, 0), (8, 4, 8192, 2),
+                                         (4, 2, 1000, 1), (6, 3, 413, 0)])
+def test_out_pad_writes(engines, k, m, S, bound):
+    """rs_set_out_pad_writes: every output row written keeps bytes [0, S) exact and
+    may fill its padding up to the next 128-B line; bytes past that line and rows a
+    stripe does not miss stay untouched.  Device masks, with the caller's bound and
+    without (bound 0 -> E = M)."""
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, N = k + m, 777
+    P = shard_pitch_for(S) + 256  # room past the 128-B line
+    g = torch.Generator(device="cuda").manual_seed(S + k)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    full = torch.cat([data, parity], dim=1).cpu().numpy()
+    rng = np.random.default_rng(S * 7 + bound)
+    masks = _masks(rng, N, t, 1, bound or m)
+    rows = bound or m
+    out = torch.full((N, rows, P), 0xC3, dtype=torch.uint8, device="cuda")
+    eng.set_out_pad_writes(True)
+    try:
+        eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
+                            max_missing=bound, shard_pitch=P)
+        eng.sync()
+    finally:
+        eng.set_out_pad_writes(False)
+    got = out.cpu().numpy()
+    line_end = min(P, (S + 127) // 128 * 128)
+    for i in range(N):
+        missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+        for r, j in enumerate(missing):
+            assert np.array_equal(got[i, r, :S], full[i, j, :S]), (i, r, j)
+            assert (got[i, r, line_end:] == 0xC3).all(), ("past the line", i, r)
+        assert (got[i, len(missing):] == 0xC3).all(), ("unused rows", i)

@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--out-rows", default="full", choices=["full", "dense", "both"],
                     help="out-of-place outputs: m rows per stripe (full), or only the launch's erasure "
                          "bound (dense: a bounded 1-erasure launch writes stripe after stripe back to back)")
+    ap.add_argument("--out-pad", default="0", choices=["0", "1", "both"],
+                    help="rs_set_out_pad_writes: out-of-place rows written to the next 128-B line "
+                         "(both: each out-of-place workload twice, +outpad)")
     ap.add_argument("--parity-pad", action="store_true",
                     help="rs_set_parity_pad_writes(1): encode writes parity padding to the next 128-B line")
     args = ap.parse_args()
@@ -127,12 +130,18 @@ def main():
         else:
             workloads = {kk: vv for n, w in workloads.items() for kk, vv in
                          ([(n, w)] + ([(f"{n}+dense", w)] if w[4] in bounded_rows else []))}
+    if args.out_pad != "0":
+        padded = {f"{n}+outpad": w for n, w in workloads.items() if "out" in w[4]}
+        workloads = padded if args.out_pad == "1" else {
+            kk: vv for n, w in workloads.items()
+            for kk, vv in ([(n, w)] + ([(f"{n}+outpad", w)] if "out" in w[4] else []))}
     for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
             if args.parity_pad:
                 engines[(k, m)].set_parity_pad_writes(True)
         eng = engines[(k, m)]
+        eng.set_out_pad_writes(name.endswith("+outpad"))
         t = k + m
         P = shard_pitch_for(S) + pad
         nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))
