@@ -329,11 +329,13 @@ def link_peak(torch, nbytes=256 << 20):
 def host_e2e(torch, eng, k, m, S, N):
     """Pinned host -> H2D -> kernel -> D2H (split layout, shards back to back as
     Split produces them): encode, then 1-erasure reconstruct.  Rates are user data
-    bytes (N*K*S) per second; the link moves K+M (encode: K in, M out) shards."""
-    data = np.random.default_rng(2).integers(0, 256, (N, k, S), dtype=np.uint8)
-    parity = np.zeros((N, m, S), np.uint8)
-    eng.host_register(data)
-    eng.host_register(parity)
+    bytes (N*K*S) per second; the link moves K+M (encode: K in, M out) shards.
+    The shards live in the context's own page-locked memory (rs_host_alloc), the
+    only host memory the kernels address in place."""
+    data = eng.host_alloc(N * k * S).reshape(N, k, S)
+    parity = eng.host_alloc(N * m * S).reshape(N, m, S)
+    data[:] = np.random.default_rng(2).integers(0, 256, (N, k, S), dtype=np.uint8)
+    parity[:] = 0
     out = {"bytes_user": N * k * S}
     try:
         for zc in (True, False):
@@ -351,8 +353,8 @@ def host_e2e(torch, eng, k, m, S, N):
                          "reconstruct1_GiBps": round(N * k * S / t_rec / GiB, 2)}
     finally:
         eng.set_host_zero_copy(True)
-        eng.host_unregister(data)
-        eng.host_unregister(parity)
+        eng.host_free(data)
+        eng.host_free(parity)
     out.update(link_peak(torch))
     return out
 
@@ -375,8 +377,10 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
     lost_all = rng.integers(0, t, N_total)
     is_rec, lost = is_rec_all[b:e], lost_all[b:e]
     masks = np.where(is_rec, full & ~(1 << lost), (1 << k) - 1).astype(np.uint32)
-    data = torch.empty((N, k, S), dtype=torch.uint8, pin_memory=True)
-    parity = torch.empty((N, m, S), dtype=torch.uint8, pin_memory=True)
+    # the context's own page-locked memory (rs_host_alloc): zero-copy qualifies
+    dn = eng.host_alloc(N * k * S).reshape(N, k, S)
+    pn = eng.host_alloc(N * m * S).reshape(N, m, S)
+    data, parity = torch.from_numpy(dn), torch.from_numpy(pn)
     g = torch.Generator(device="cuda").manual_seed(seed + rank)
     step = 1 << 16
     for s0 in range(0, N, step):  # random data + its true parity, made on the GPU
@@ -387,7 +391,6 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
         data[s0:s0 + n].copy_(dd)
         parity[s0:s0 + n].copy_(pp)
     torch.cuda.synchronize()
-    dn, pn = data.numpy(), parity.numpy()
     sample = rng.choice(N, size=min(N, 4096), replace=False)
     ref_d, ref_p = dn[sample].copy(), pn[sample].copy()
     lost_d = ((~masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
@@ -398,7 +401,7 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
         pn[lost_p] = 0
 
     e2e, ok = {}, True
-    for zc in (True, False):  # torch's pinned pages are GPU-mapped: zero-copy qualifies
+    for zc in (True, False):
         eng.set_host_zero_copy(zc)
         erase()
         eng.reconstruct_host(dn, pn, S, N, masks)  # warm: pipeline slabs, LUT
@@ -421,6 +424,8 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
                                  * 1e-3)
     eng.sync()
     del dd, pd, md, data, parity
+    eng.host_free(dn)
+    eng.host_free(pn)
     torch.cuda.empty_cache()
     user = N_total * k * S
     return {"objects": N_total, "objects_per_gpu": N, "shard_len": S,

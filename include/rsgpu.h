@@ -117,8 +117,9 @@ int rs_verify(rs_ctx *ctx, uint8_t *const *shards, const size_t *lens, int *ok);
  *   bases 16-B aligned (the kernels read whole 16-B columns; bytes of a slot past S
  *   may be read, never written).  The call enqueues on `stream` and returns;
  *   synchronise with hipStreamSynchronize or rs_sync.  S up to 0xFFFFFFF0.
- * RS_MEM_HOST: any pitches; pinned shards (rs_host_register / hipHostMalloc) are
- *   read and written in place by the kernels (zero-copy), others are staged
+ * RS_MEM_HOST: any pitches; shards in memory the context allocated (rs_host_alloc)
+ *   are read and written in place by the kernels (zero-copy), all others --
+ *   pageable, rs_host_register'ed, or pinned by another allocator -- are staged
  *   through device slabs with H2D / kernel / D2H overlapped on several streams.
  *   Returns when the outputs are in host memory.  A multi-GPU context splits the
  *   batch into contiguous stripe ranges, one per GPU, run in parallel.
@@ -219,6 +220,8 @@ typedef struct {
   int spin_waiters;       /* callers that may spin-wait for their batch at once instead of
                              sleeping on a futex: 0 = none (default), > 0 = that many, capped
                              at the CPUs this process may use minus the coalescer's threads */
+  int plain_copy;         /* 0 (default): shard-sized staging copies use streaming stores;
+                             1: plain memcpy (A/B measurements) */
 } rs_coalescer_opts;
 int rs_coalescer_create(rs_ctx *ctx, const rs_coalescer_opts *opts /* NULL = defaults */,
                         rs_coalescer **out);
@@ -279,6 +282,11 @@ int rs_co_reap(rs_coalescer *co, uint64_t *tags, int *rcs, int max, int timeout_
 /* Counters since creation: calls, device batches, stripes batched, largest batch. */
 int rs_co_stats(rs_coalescer *co, uint64_t *calls, uint64_t *batches, uint64_t *stripes,
                 uint64_t *max_batch);
+/* Launcher diagnostics since creation (any pointer may be NULL): time spent waiting
+ * for callers still staging a closed batch, time in launch calls, time batches
+ * executed, and how often a caller waited for a free batch. */
+int rs_co_timing(rs_coalescer *co, uint64_t *straggle_ns, uint64_t *launch_ns, uint64_t *exec_ns,
+                 uint64_t *free_waits);
 
 /* ---- batched SHA-256 (cold_hash next to encode) -----
  * The reference hashes every EC-written value (writeservice.go:51-54
@@ -295,33 +303,40 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
                         const uint64_t *lens, size_t n, uint8_t *digests, void *stream);
 
 /* ---- host memory helpers ------------------------------------------------ */
-/* Pins [ptr, ptr + bytes) for every GPU of the process (DMA + zero-copy) and
- * remembers the range: a coalesced call (rs_co_encode / rs_co_reconstruct, their
- * _submit_ and _many forms, and the _hash forms when the data shards holding the
- * value are contiguous -- shard c at shard 0 + c*S, as Split carves them; not the
- * _data form) whose shards -- the ones it reads and the ones it fills -- all lie
- * inside one registered range, 16-B aligned, runs in place: the kernel reads the caller's shards and writes the
- * parity / missing shards straight into the caller's buffers over PCIe, with no
- * staging copy either way (the request body and the HTTP send
- * buffers, or a healer's shard buffers, in a registered arena).  Such a call writes
- * nothing outside [0, S) of any shard.  Unregister only when no call is using the
- * range. */
-int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);
-int rs_host_unregister(rs_ctx *ctx, void *ptr);
-/* The same in-place eligibility on memory the context allocates itself:
- * page-locked (hipHostMalloc, portable, on the first GPU's NUMA node when the
- * runtime allows), GPU-mapped, page aligned.  Unlike a registered range of
- * malloc'ed memory, whose pages the OS may still migrate or compact (amdgpu maps
- * registered user memory without pinning it for life), these pages stay put, so an
- * arena of long-lived request / shard buffers is best taken from here (the Go
- * shim's and the C++ mirror's Arena do).  rs_host_free only pointers rs_host_alloc
- * returned, when no call is using them; rs_destroy frees any left. */
+/* In-place host memory: page-locked memory the context allocates itself
+ * (hipHostMalloc, portable, on the first GPU's NUMA node when the runtime allows),
+ * GPU-mapped, page aligned.  A coalesced call (rs_co_encode / rs_co_reconstruct,
+ * their _submit_ and _many forms, and the _hash forms when the data shards holding
+ * the value are contiguous -- shard c at shard 0 + c*S, as Split carves them; not
+ * the _data form) whose shards -- the ones it reads and the ones it fills -- all lie
+ * inside one rs_host_alloc'ed range, 16-B aligned, runs in place: the kernel reads
+ * the caller's shards and writes the parity / missing shards straight into them
+ * over PCIe, with no staging copy either way (the request
+ * body and the HTTP send buffers, or a healer's shard buffers, in an arena).  Such a
+ * call writes nothing outside [0, S) of any shard.  RS_MEM_HOST batches in such
+ * memory run zero-copy.  rs_host_free only pointers rs_host_alloc returned, when no
+ * call is using them; rs_destroy frees any left (after every queued kernel). */
 int rs_host_alloc(rs_ctx *ctx, size_t bytes, void **out);
 int rs_host_free(rs_ctx *ctx, void *ptr);
+/* Records [ptr, ptr + bytes) as caller memory and nothing more: the library never
+ * pins, maps or addresses caller memory in place (round 4).  amdgpu maps
+ * hipHostRegister'ed pageable memory as a user-pointer range whose pages may still
+ * be migrated, compacted or collapsed into huge pages while a kernel runs, which is
+ * how in-place writes into it were lost.  Calls on registered
+ * buffers are staged like any pageable buffer; use rs_host_alloc for in-place
+ * work.  Kept for ABI compatibility: RS_ERR_INVALID_ARG for a range overlapping a
+ * known one; rs_host_unregister(ptr) forgets the range starting at ptr
+ * (RS_ERR_INVALID_ARG if there is none, or it is rs_host_free's). */
+int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);
+int rs_host_unregister(rs_ctx *ctx, void *ptr);
 
 /* ---- measurement helpers (bench.py) ------------------------------------- */
-/* Name of the kernel the last batched call on this context launched. */
+/* Name of the kernel the last batched call on this context launched (any thread). */
 const char *rs_last_kernel(const rs_ctx *ctx);
+/* Name of the last kernel this context launched on `stream` ("none" if none): the
+ * launch that preceded a device error reported on that stream, whatever other
+ * threads launched meanwhile. */
+const char *rs_last_kernel_on(rs_ctx *ctx, void *stream);
 /* Streaming device copy, the measured HBM ceiling beside the RS kernels. */
 int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *stream);
 /* Tuning knob: workgroups (256 threads) per CU for the batched kernels
@@ -344,10 +359,10 @@ int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
  * is read over the same range.  Bytes [0, S) are unchanged.  0 (the default): no
  * byte past S of an output row is written. */
 int rs_set_out_pad_writes(rs_ctx *ctx, int enable);
-/* RS_MEM_HOST batches whose shards are all in pinned host memory (hipHostMalloc or
- * rs_host_register) and 16-B aligned run zero-copy by default: the kernel reads
- * the survivors and writes the missing shards across PCIe in place.  0 forces
- * the staged H2D -> kernel -> D2H pipeline (A/B and tests). */
+/* RS_MEM_HOST batches whose shards all lie in rs_host_alloc'ed memory, 16-B
+ * aligned, run zero-copy by default: the kernel reads the survivors and writes the
+ * missing shards across PCIe in place.  0 forces the staged H2D -> kernel -> D2H
+ * pipeline (A/B and tests). */
 int rs_set_host_zero_copy(rs_ctx *ctx, int enable);
 /* "zero-copy" or "staged": how the last RS_MEM_HOST batch ran. */
 const char *rs_last_host_path(const rs_ctx *ctx);

@@ -75,6 +75,7 @@ SIGNATURES = {
     "rs_co_reconstruct_data": (_i, [_vp, _u8pp, _szp]),
     "rs_co_verify": (_i, [_vp, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_stats": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "rs_co_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "rs_co_reconstruct_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_encode_many": (_i, [_vp, _sz, _u8pp, _szp, ctypes.POINTER(_i)]),
     "rs_co_encode_hash": (_i, [_vp, _u8pp, _szp, _sz, _u8p]),
@@ -87,6 +88,7 @@ SIGNATURES = {
     "rs_host_alloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
     "rs_host_free": (_i, [_vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
+    "rs_last_kernel_on": (ctypes.c_char_p, [_vp, _vp]),
     "rs_device_copy": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "rs_set_blocks_per_cu": (_i, [_vp, _i]),
     "rs_set_parity_pad_writes": (_i, [_vp, _i]),

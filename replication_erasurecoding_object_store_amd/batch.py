@@ -208,6 +208,8 @@ class BatchEngine(Service):
         return bad
 
     def host_register(self, arr: np.ndarray) -> None:
+        """Records arr as caller memory (rs_host_register): never mapped into the GPU,
+        calls on it are staged; host_alloc gives memory the kernels use in place."""
         _check(_lib.lib().rs_host_register(self.ctx, arr.ctypes.data, arr.nbytes))
 
     def host_unregister(self, arr: np.ndarray) -> None:
@@ -230,6 +232,11 @@ class BatchEngine(Service):
 
     def last_kernel(self) -> str:
         return _lib.lib().rs_last_kernel(self.ctx).decode()
+
+    def last_kernel_on(self, stream=None) -> str:
+        """The last kernel this context launched on `stream` (torch's current stream by
+        default): names the launch before a device error on that stream."""
+        return _lib.lib().rs_last_kernel_on(self.ctx, _stream_handle(stream)).decode()
 
     def set_host_zero_copy(self, enable: bool) -> None:
         _check(_lib.lib().rs_set_host_zero_copy(self.ctx, 1 if enable else 0))

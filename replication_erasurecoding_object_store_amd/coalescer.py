@@ -20,7 +20,7 @@ from .ec import ECError, ErrTooFewShards, M, K, Service, _check, _shard_array
 class CoalescerOpts(ctypes.Structure):
     _fields_ = [("max_batch", ctypes.c_size_t), ("max_wait_us", ctypes.c_uint32), ("inflight", ctypes.c_int),
                 ("max_batch_bytes", ctypes.c_size_t), ("max_exec", ctypes.c_int),
-                ("staged_dma", ctypes.c_int), ("spin_waiters", ctypes.c_int)]
+                ("staged_dma", ctypes.c_int), ("spin_waiters", ctypes.c_int), ("plain_copy", ctypes.c_int)]
 
 
 class CoalescingService(Service):

@@ -117,7 +117,7 @@ struct Batch {
   std::atomic<uint32_t> fill_err{0};   // a slot's plan could not be resolved (plan mode)
   std::atomic<uint32_t> max_missing{0};  // most shards any slot fills: the launch's erasure bound
   std::atomic<uint32_t> hash_in{0};      // some slot wants the SHA-256 of its value (cold_hash)
-  std::atomic<uint32_t> direct_in{0};    // some slot is addressed in the caller's registered buffers
+  std::atomic<uint32_t> direct_in{0};    // some slot is addressed in place in the caller's rs_host_alloc'ed buffers
   uint8_t* host_dev = nullptr;           // zero-copy: GPU address of the pinned staging
   // asynchronous calls of the current run: their records, how many were made, how
   // many have been handed to reapers (under rs_coalescer::done_mu)
@@ -301,7 +301,8 @@ struct rs_coalescer {
 
   int max_exec = 2;   // batches on one device at once
   bool zero_copy = true;
-  // objects whose shards lie in rs_host_register'ed memory run in place (zero-copy
+  bool nt_copy = true;  // streaming stores in the staging copies (opts.plain_copy = 0)
+  // objects whose shards lie in rs_host_alloc'ed memory run in place (zero-copy
   // staging, k+m <= 16, a pointer-table kernel for (k, m))
   bool direct_ok = false;
   // callers that may spin-wait for their batch at once (opts.spin_waiters, capped at
@@ -325,14 +326,10 @@ struct rs_coalescer {
   std::deque<Batch*> done;
 
   std::atomic<uint64_t> calls{0}, n_batches{0}, stripes{0}, max_seen{0};
-  // diagnostics (printed at destroy when RS_CO_DEBUG is set)
+  // diagnostics (rs_co_timing)
   std::atomic<uint64_t> straggle_ns{0}, exec_ns{0}, free_waits{0}, launches_idle{0}, launch_ns{0};
 
   ~rs_coalescer() {
-    if (std::getenv("RS_CO_DEBUG"))
-      std::fprintf(stderr, "[rs_coalescer] batches %llu straggle_ms %.1f launch_ms %.1f exec_ms %.1f free_waits %llu\n",
-                   (unsigned long long)n_batches.load(), straggle_ns.load() / 1e6, launch_ns.load() / 1e6,
-                   exec_ns.load() / 1e6, (unsigned long long)free_waits.load());
     stop.store(true, std::memory_order_release);
     for (auto& d : disp) {
       poke(d.get());
@@ -460,7 +457,7 @@ int launch_batch(rs_coalescer* co, Batch* b, size_t n) {
   } else {
     if (b->fill_err.load(std::memory_order_acquire)) return RS_ERR_DEVICE;
     if (co->per_stripe && b->direct_in.load(std::memory_order_acquire)) {
-      // some slot is addressed in the caller's registered buffers: every slot
+      // some slot is addressed in place in the caller's rs_host_alloc'ed buffers: every slot
       // through its row of the pointer table (staged slots point into the staging)
       if (!zc || !b->host_dev || at(0) != b->host_dev) return RS_ERR_DEVICE;
       const int bound = static_cast<int>(b->max_missing.load(std::memory_order_acquire));
@@ -589,7 +586,7 @@ constexpr auto kStraggleGrace = std::chrono::microseconds(100);
 // staged and fewer than max_exec batches of this GPU are executing.  Round 3: the
 // launcher no longer waits on a closed batch's staging copies before it can look
 // at other batches -- with 1.5 MB objects those copies took 41 % of its time while
-// the device idled between batches (RS_CO_DEBUG straggle_ms).  The last caller to
+// the device idled between batches (rs_co_timing straggle_ns).  The last caller to
 // stage into a closed batch always wakes the launcher.
 void launcher_loop(rs_coalescer* co, Dispatcher* d) {
   std::vector<Closing> closing;
@@ -862,8 +859,8 @@ struct RecItem {
   size_t S = 0;
   uint32_t present = 0;
   bool parity_used = false;  // a parity shard is among the k survivors
-  bool direct = false;       // every shard it reads or writes is registered: addressed in place
-  uint64_t dev[32] = {};     // direct: GPU address of every shard (rs_host_register'ed)
+  bool direct = false;       // every shard it reads or writes is rs_host_alloc'ed: addressed in place
+  uint64_t dev[32] = {};     // direct: GPU address of every shard (rs_host_alloc'ed)
 };
 
 // Checks one object; *need = false when there is nothing to do (rc RS_OK).
@@ -946,7 +943,7 @@ void stage_ptrs(const rs_coalescer* co, Batch* b, size_t slot, uint32_t present)
 }
 
 // GPU addresses of a call's shards when every one the kernel touches lies in
-// rs_host_register'ed memory, 16-B aligned: `touched` bit s = shard s is read (one of
+// rs_host_alloc'ed memory (the context's own page-locked pages), 16-B aligned: `touched` bit s = shard s is read (one of
 // the first k present) or written (an output).  Other entries repeat the first
 // touched address (never dereferenced).  False: the call is staged.
 bool direct_ptrs(rs_coalescer* co, uint8_t* const* shards, size_t S, uint32_t touched, uint64_t* dev) {
@@ -957,7 +954,7 @@ bool direct_ptrs(rs_coalescer* co, uint8_t* const* shards, size_t S, uint32_t to
     dev[s] = 0;
     if (!((touched >> s) & 1u)) continue;
     if (!shards[s] || reinterpret_cast<uintptr_t>(shards[s]) % 16) return false;
-    uint8_t* d = rs::ctx_registered(co->ctx, shards[s], S);
+    uint8_t* d = rs::ctx_owned(co->ctx, shards[s], S);
     if (!d || reinterpret_cast<uintptr_t>(d) % 16) return false;
     dev[s] = reinterpret_cast<uint64_t>(d);
     if (!first) first = dev[s];
@@ -1010,7 +1007,7 @@ void encode_fill(const rs_coalescer* co, Batch* b, size_t slot, uint8_t* const* 
     if (value_len != rs::kSha256Skip) set_hash_direct(b, slot, value_len, dev[0]);
     return;
   }
-  for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
+  for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S, co->nt_copy);
   set_hash(b, k, slot, value_len);
   if (co->per_stripe) {
     reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = data_mask;
@@ -1051,7 +1048,7 @@ void rec_fill(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it, 
     if (!it.lens[i]) continue;
     ++staged;
     uint8_t* dst = i < k ? host_at(b, b->o_data + (slot * k + i) * P) : host_at(b, b->o_parity + (slot * m + (i - k)) * P);
-    rs::stage_copy(dst, it.shards[i], it.S);
+    rs::stage_copy(dst, it.shards[i], it.S, co->nt_copy);
   }
   if (co->per_stripe) {
     reinterpret_cast<uint32_t*>(host_at(b, b->o_masks))[slot] = it.present;
@@ -1068,7 +1065,7 @@ void rec_drain(const rs_coalescer* co, Batch* b, size_t slot, const RecItem& it,
   for (int i = 0; i < t; ++i) {
     if (it.lens[i]) continue;
     if (!data_only || i < k) {
-      if (!it.direct) rs::stage_copy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S);
+      if (!it.direct) rs::stage_copy(it.shards[i], host_at(b, b->o_out + (slot * m + r) * b->P), it.S, co->nt_copy);
       it.lens[i] = it.S;  // direct: the kernel wrote the caller's buffer
     }
     ++r;
@@ -1095,7 +1092,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   if (!ctx || !out) return RS_ERR_INVALID_ARG;
   *out = nullptr;
   const int ne = rs::ctx_engine_count(ctx);
-  rs_coalescer_opts o{4096, 0, std::max(16, 8 * ne), size_t(32) << 20, 2, 0, 0};
+  rs_coalescer_opts o{4096, 0, std::max(16, 8 * ne), size_t(32) << 20, 2, 0, 0, 0};
   if (opts) {
     if (opts->max_batch) o.max_batch = opts->max_batch;
     o.max_wait_us = opts->max_wait_us;
@@ -1104,6 +1101,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
     if (opts->max_exec > 0) o.max_exec = opts->max_exec;
     o.staged_dma = opts->staged_dma;
     o.spin_waiters = opts->spin_waiters;
+    o.plain_copy = opts->plain_copy;
   }
   if (o.inflight > 256 || o.max_exec > o.inflight || o.inflight < ne || o.spin_waiters < 0) return RS_ERR_INVALID_ARG;
   auto co = std::make_unique<rs_coalescer>();
@@ -1116,6 +1114,7 @@ int rs_coalescer_create(rs_ctx* ctx, const rs_coalescer_opts* opts, rs_coalescer
   co->max_wait = std::chrono::microseconds(o.max_wait_us);
   co->max_exec = o.max_exec;
   co->zero_copy = o.staged_dma == 0;
+  co->nt_copy = o.plain_copy == 0;
   co->direct_ok = co->zero_copy && co->k + co->m <= 16 && rs::apply_ptrs_supported(co->k, co->m);
   co->spin_slots = std::min(o.spin_waiters, std::max(0, usable_cpus() - 2 - 2 * ne));
   co->engine_load.assign(static_cast<size_t>(ne), 0);
@@ -1177,7 +1176,7 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
   for (int i = 0; i < k + m; ++i)
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
-  // every shard in registered memory (a cold_hash's value contiguous in it): the
+  // every shard in rs_host_alloc'ed memory (a cold_hash's value contiguous in it): the
   // kernels read the data and write the parity in place
   uint64_t dev[32];
   const bool direct =
@@ -1185,7 +1184,7 @@ static int co_encode(rs_coalescer* co, uint8_t* const* shards, const size_t* len
   auto fill = [&](Batch* b, size_t slot) { encode_fill(co, b, slot, shards, S, direct ? dev : nullptr, value_len); };
   auto drain = [&](Batch* b, size_t slot) {
     if (!direct)
-      for (int r = 0; r < m; ++r) rs::stage_copy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+      for (int r = 0; r < m; ++r) rs::stage_copy(shards[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S, co->nt_copy);
     if (hash) std::memcpy(digest, host_at(b, b->o_digest + slot * 32), 32);
   };
   return submit(co, Kind::kApply, S, false, fill, drain);
@@ -1220,8 +1219,8 @@ int rs_co_verify(rs_coalescer* co, uint8_t* const* shards, const size_t* lens, i
     if (!shards[i]) return RS_ERR_INVALID_ARG;
   if (S > 0xFFFFFFF0u) return RS_ERR_INVALID_ARG;
   auto fill = [&](Batch* b, size_t slot) {
-    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S);
-    for (int r = 0; r < m; ++r) rs::stage_copy(host_at(b, b->o_parity + (slot * m + r) * b->P), shards[k + r], S);
+    for (int c = 0; c < k; ++c) rs::stage_copy(host_at(b, b->o_data + (slot * k + c) * b->P), shards[c], S, co->nt_copy);
+    for (int r = 0; r < m; ++r) rs::stage_copy(host_at(b, b->o_parity + (slot * m + r) * b->P), shards[k + r], S, co->nt_copy);
   };
   auto drain = [&](Batch* b, size_t slot) { *ok = reinterpret_cast<uint32_t*>(host_at(b, b->o_bad))[slot] == 0; };
   return submit(co, Kind::kVerify, S, true, fill, drain);
@@ -1286,7 +1285,7 @@ int rs_co_reap(rs_coalescer* co, uint64_t* tags, int* rcs, int max, int timeout_
         const AsyncRec& r = b->arec[j];
         if (brc == RS_OK) {
           for (uint32_t o = 0; o < r.n_out; ++o)
-            rs::stage_copy(r.out[o], host_at(b, b->o_out + (static_cast<size_t>(r.slot) * m + o) * b->P), b->S);
+            rs::stage_copy(r.out[o], host_at(b, b->o_out + (static_cast<size_t>(r.slot) * m + o) * b->P), b->S, co->nt_copy);
         }
         tags[got] = r.tag;
         rcs[got] = brc;
@@ -1363,7 +1362,7 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
     rcs[i] = rc;
     if (rc == RS_OK && m > 0) by_len[S].push_back(i);
   }
-  // objects whose shards are all registered run in place (as rs_co_encode's)
+  // objects whose shards are all rs_host_alloc'ed run in place (as rs_co_encode's)
   std::vector<uint64_t> devs(co->direct_ok ? n_objects * t : 0);
   std::vector<uint8_t> direct(n_objects, 0);
   for (auto& g : by_len)
@@ -1384,7 +1383,7 @@ static int co_encode_many(rs_coalescer* co, size_t n_objects, uint8_t* const* sh
           const size_t i = idx[j];
           uint8_t* const* sh = shards + i * t;
           if (!direct[i])
-            for (int r = 0; r < m; ++r) rs::stage_copy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S);
+            for (int r = 0; r < m; ++r) rs::stage_copy(sh[k + r], host_at(b, b->o_out + (slot * m + r) * b->P), S, co->nt_copy);
           if (hash) std::memcpy(digests + i * 32, host_at(b, b->o_digest + slot * 32), 32);
         });
     if (rc) {
@@ -1411,6 +1410,16 @@ int rs_co_stats(rs_coalescer* co, uint64_t* calls, uint64_t* batches, uint64_t* 
   if (batches) *batches = co->n_batches.load();
   if (stripes) *stripes = co->stripes.load();
   if (max_batch) *max_batch = co->max_seen.load();
+  return RS_OK;
+}
+
+int rs_co_timing(rs_coalescer* co, uint64_t* straggle_ns, uint64_t* launch_ns, uint64_t* exec_ns,
+                 uint64_t* free_waits) {
+  if (!co) return RS_ERR_INVALID_ARG;
+  if (straggle_ns) *straggle_ns = co->straggle_ns.load();
+  if (launch_ns) *launch_ns = co->launch_ns.load();
+  if (exec_ns) *exec_ns = co->exec_ns.load();
+  if (free_waits) *free_waits = co->free_waits.load();
   return RS_OK;
 }
 

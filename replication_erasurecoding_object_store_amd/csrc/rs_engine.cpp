@@ -253,10 +253,24 @@ struct StatusChunk {
   PinnedBuf host;
 };
 
-// Context-wide "what ran last" (measurement helpers).
+// "What ran last" (measurement and fault diagnostics): context-wide, and per launch
+// stream -- a device fault surfaces asynchronously, and only the stream's own record
+// names the launch that preceded it when other threads launch on the context too.
 struct Shared {
   std::atomic<const char*> last_kernel{"none"};
   std::atomic<const char*> last_host_path{"none"};
+  std::mutex stream_mu;
+  std::unordered_map<hipStream_t, const char*> by_stream;
+  void note(hipStream_t s, const char* name) {
+    last_kernel.store(name);
+    std::lock_guard<std::mutex> g(stream_mu);
+    by_stream[s] = name;
+  }
+  const char* on(hipStream_t s) {
+    std::lock_guard<std::mutex> g(stream_mu);
+    auto it = by_stream.find(s);
+    return it == by_stream.end() ? "none" : it->second;
+  }
 };
 
 }  // namespace
@@ -266,6 +280,7 @@ namespace rs {
 
 struct Engine {
   int k = 0, m = 0, device = 0, cu_count = 0, numa = -1;
+  rs_ctx* ctx = nullptr;                  // owner (its rs_host_alloc'ed ranges)
   const Matrix* enc = nullptr;            // the context's
   const std::vector<uint32_t>* h_lut = nullptr;
   Shared* shared = nullptr;
@@ -364,21 +379,23 @@ struct Engine {
 
 using rs::Engine;
 
-// A host range pinned and GPU-mapped through rs_host_register.
+// A host range the context knows: rs_host_alloc'ed (owned: page-locked by the
+// driver, GPU-mapped, eligible for in-place kernels) or rs_host_register'ed (caller
+// memory: recorded only, never mapped into a GPU, always staged).
 struct RegRange {
   uintptr_t lo = 0, hi = 0;  // [lo, hi)
-  uint8_t* dev = nullptr;     // GPU address of lo (portable mapping: every device)
+  uint8_t* dev = nullptr;     // owned: GPU address of lo (portable mapping: every device)
   bool owned = false;         // rs_host_alloc'ed (freed by rs_host_free / rs_destroy)
 };
 
 struct rs_ctx {
   int k = 0, m = 0;
   Matrix enc;
-  // rs_host_register'ed ranges, sorted by lo (the coalescer addresses buffers that
-  // lie inside one in place instead of staging them)
+  // known host ranges, sorted by lo, never overlapping (kernels address buffers that
+  // lie inside an owned one in place instead of staging them)
   std::shared_mutex reg_mu;
   std::vector<RegRange> reg;
-  std::atomic<uint32_t> n_reg{0};
+  std::atomic<uint32_t> n_owned{0};
   std::vector<uint32_t> h_lut;            // missing mask -> plan index (k+m <= 16)
   std::vector<std::unique_ptr<Engine>> engines;
   Shared shared;
@@ -586,7 +603,7 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   const char* name =
       rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
-  e->shared->last_kernel.store(name);
+  e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -597,7 +614,7 @@ int launch_verify_args(Engine* e, rs::KernelArgs& a, hipStream_t s) {
   const char* name =
       rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
-  e->shared->last_kernel.store(name);
+  e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -830,42 +847,27 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   return RS_OK;
 }
 
-// GPU address of a pinned host range [p, p+bytes) (hipHostMalloc'ed or
-// rs_host_register'ed), or nullptr if any part of it is pageable.
-uint8_t* mapped(const void* p, size_t bytes) {
-  if (!p || bytes == 0) return nullptr;
-  hipPointerAttribute_t a{}, b{};
-  if (hipPointerGetAttributes(&a, p) != hipSuccess || a.type != hipMemoryTypeHost || !a.devicePointer) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  const void* last = static_cast<const uint8_t*>(p) + bytes - 1;
-  if (hipPointerGetAttributes(&b, last) != hipSuccess || b.type != hipMemoryTypeHost || !b.devicePointer) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  uint8_t* d = static_cast<uint8_t*>(a.devicePointer);
-  if (static_cast<uint8_t*>(b.devicePointer) != d + (bytes - 1)) return nullptr;  // one linear mapping
-  return d;
-}
-
 int ensure_pipe_stream(Engine* e, int i) {
   if (!e->pipe_st[i]) RS_HIP(hipStreamCreateWithFlags(&e->pipe_st[i], hipStreamNonBlocking));
   return RS_OK;
 }
 
-// Zero-copy host batch: with the shards in pinned host memory the kernel itself
-// reads the K survivors and writes only the missing shards across PCIe, in place
-// -- per stripe exactly the bytes the codec needs, no staging slab, no DMA of
-// slots it does not touch (the staged pipeline must move every slot a stripe
-// might use).  Returns RS_ERR_NOT_SUPPORTED when the layout does not qualify.
+// Zero-copy host batch: with the shards in the context's own page-locked memory
+// (rs_host_alloc) the kernel itself reads the K survivors and writes only the
+// missing shards across PCIe, in place -- per stripe exactly the bytes the codec
+// needs, no staging slab, no DMA of slots it does not touch (the staged pipeline
+// must move every slot a stripe might use).  Memory the library does not own --
+// pageable, rs_host_register'ed or pinned by someone else -- never qualifies: a
+// kernel never reads or writes pages whose lifetime and placement the library does
+// not control.  Returns RS_ERR_NOT_SUPPORTED when the batch does
+// not qualify.
 int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
                    const uint32_t* masks_host, int e_out, uint32_t* bad_host) {
   const int k = e->k, m = e->m;
   const size_t dbytes = (N - 1) * hl.data_sp + static_cast<size_t>(k - 1) * hl.pitch + S;
   const size_t pbytes = m ? (N - 1) * hl.parity_sp + static_cast<size_t>(m - 1) * hl.pitch + S : 0;
-  uint8_t* dd = mapped(hl.data, dbytes);
-  uint8_t* pd = m ? mapped(hl.parity, pbytes) : nullptr;
+  uint8_t* dd = rs::ctx_owned(e->ctx, hl.data, dbytes);
+  uint8_t* pd = m ? rs::ctx_owned(e->ctx, hl.parity, pbytes) : nullptr;
   if (!dd || (m && !pd)) return RS_ERR_NOT_SUPPORTED;
   const Layout dl{dd, hl.data_sp, pd, hl.parity_sp, hl.pitch};
   if (!device_layout_ok(dl, m, S)) return RS_ERR_NOT_SUPPORTED;
@@ -964,6 +966,7 @@ int create_engine(rs_ctx* c, int device, const PlanSet& ps, std::unique_ptr<Engi
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RS_ERR_DEVICE;
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RS_ERR_NO_DEVICE;
   auto e = std::make_unique<Engine>();
+  e->ctx = c;
   e->k = c->k;
   e->m = c->m;
   e->device = device;
@@ -1048,15 +1051,15 @@ namespace rs {
 
 int ctx_engine_count(const rs_ctx* c) { return c ? static_cast<int>(c->engines.size()) : 0; }
 
-uint8_t* ctx_registered(rs_ctx* c, const void* p, size_t bytes) {
-  if (!c || !p || c->n_reg.load(std::memory_order_acquire) == 0) return nullptr;
+uint8_t* ctx_owned(rs_ctx* c, const void* p, size_t bytes) {
+  if (!c || !p || bytes == 0 || c->n_owned.load(std::memory_order_acquire) == 0) return nullptr;
   const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
   std::shared_lock<std::shared_mutex> g(c->reg_mu);
   auto it = std::upper_bound(c->reg.begin(), c->reg.end(), lo,
                              [](uintptr_t x, const RegRange& r) { return x < r.lo; });
   if (it == c->reg.begin()) return nullptr;
   --it;  // the last range starting at or before p
-  if (lo >= it->hi || bytes > it->hi - lo) return nullptr;
+  if (!it->owned || lo >= it->hi || bytes > it->hi - lo) return nullptr;
   return it->dev + (lo - it->lo);
 }
 Engine* ctx_engine(rs_ctx* c, int i) { return c->engines[static_cast<size_t>(i)].get(); }
@@ -1163,7 +1166,7 @@ int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uin
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, bound);
   const char* name = rs::launch_apply_ptrs(a, bound, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_NOT_SUPPORTED;
-  e->shared->last_kernel.store(name);
+  e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -1277,12 +1280,13 @@ int rs_create_multi(int k, int m, uint64_t device_mask, int flags, rs_ctx** out)
 
 void rs_destroy(rs_ctx* ctx) {
   if (!ctx) return;
-  if (!ctx->engines.empty()) {
-    DeviceScope ds(ctx->engines[0]->device);
-    for (const RegRange& r : ctx->reg)  // rs_host_alloc'ed memory never freed by the caller
-      if (r.owned) rs::pinned_free(reinterpret_cast<void*>(r.lo));
-  }
+  std::vector<void*> owned;  // rs_host_alloc'ed memory never freed by the caller
+  for (const RegRange& r : ctx->reg)
+    if (r.owned) owned.push_back(reinterpret_cast<void*>(r.lo));
+  // engines first: each joins its worker and synchronises its device, so no queued
+  // kernel still reads or writes an arena when it is freed
   delete ctx;
+  for (void* p : owned) rs::pinned_free(p);
 }
 
 int rs_data_shards(const rs_ctx* c) { return c ? c->k : 0; }
@@ -1294,6 +1298,7 @@ int rs_device_at(const rs_ctx* c, int i) {
 }
 const char* rs_backend(const rs_ctx* c) { return c ? c->backend.c_str() : "none"; }
 const char* rs_last_kernel(const rs_ctx* c) { return c ? c->shared.last_kernel.load() : "none"; }
+const char* rs_last_kernel_on(rs_ctx* c, void* stream) { return c ? c->shared.on(as_stream(stream)) : "none"; }
 
 int rs_encode_matrix(const rs_ctx* c, uint8_t* out) {
   if (!c || !out) return RS_ERR_INVALID_ARG;
@@ -1548,6 +1553,10 @@ static int sync_stream(rs_ctx* c, void* stream, bool release) {
     e->status_idx.erase(s);
     e->status_free.push_back(idx);
   }
+  if (release) {
+    std::lock_guard<std::mutex> g(c->shared.stream_mu);
+    c->shared.by_stream.erase(s);
+  }
   if (word & 1u) return RS_ERR_TOO_FEW_SHARDS;
   if (word & 2u) return RS_ERR_INVALID_ARG;
   return RS_OK;
@@ -1557,12 +1566,22 @@ int rs_sync(rs_ctx* c, void* stream) { return sync_stream(c, stream, false); }
 int rs_stream_release(rs_ctx* c, void* stream) { return sync_stream(c, stream, true); }
 
 namespace {
-void reg_insert(rs_ctx* c, const RegRange& r) {
+uint32_t count_owned(const rs_ctx* c) {
+  uint32_t n = 0;
+  for (const RegRange& r : c->reg) n += r.owned ? 1u : 0u;
+  return n;
+}
+
+// Inserts r unless it overlaps a known range (false then).
+bool reg_insert(rs_ctx* c, const RegRange& r) {
   std::unique_lock<std::shared_mutex> g(c->reg_mu);
   auto it = std::lower_bound(c->reg.begin(), c->reg.end(), r.lo,
                              [](const RegRange& a, uintptr_t lo) { return a.lo < lo; });
+  if (it != c->reg.end() && it->lo < r.hi) return false;
+  if (it != c->reg.begin() && std::prev(it)->hi > r.lo) return false;
   c->reg.insert(it, r);
-  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+  c->n_owned.store(count_owned(c), std::memory_order_release);
+  return true;
 }
 
 // Removes the range starting at ptr if its ownership matches; false if none does.
@@ -1572,40 +1591,29 @@ bool reg_erase(rs_ctx* c, void* ptr, bool owned) {
   auto it = std::find_if(c->reg.begin(), c->reg.end(), [&](const RegRange& r) { return r.lo == lo; });
   if (it == c->reg.end() || it->owned != owned) return false;
   c->reg.erase(it);
-  c->n_reg.store(static_cast<uint32_t>(c->reg.size()), std::memory_order_release);
+  c->n_owned.store(count_owned(c), std::memory_order_release);
   return true;
 }
 }  // namespace
 
-// Pins for every GPU of the process (portable) and maps into their address spaces;
-// the range is remembered so coalesced calls on buffers inside it run in place.
+// Caller memory is recorded, not pinned or mapped (round 4).  amdgpu maps
+// hipHostRegister'ed pageable memory as a user-pointer range whose pages the kernel
+// may still migrate, compact or collapse into huge pages under a running kernel;
+// the round-3 records show lost in-place writes and a late-reported illegal address
+// right after the only tests that ran GPU work on such ranges.  So no
+// kernel and no DMA of this library touches caller pages in place: calls on
+// registered buffers are staged through the library's own page-locked memory, and
+// in-place work needs rs_host_alloc.
 int rs_host_register(rs_ctx* c, void* ptr, size_t bytes) {
-  if (!c || !ptr || bytes == 0) return RS_ERR_INVALID_ARG;
-  DeviceScope ds(c->engines[0]->device);
-  RS_HIP(hipHostRegister(ptr, bytes, hipHostRegisterPortable | hipHostRegisterMapped));
-  void* dev = nullptr;
-  if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
-    (void)hipGetLastError();
-    (void)hipHostUnregister(ptr);
-    return RS_ERR_DEVICE;
-  }
-  reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(ptr), reinterpret_cast<uintptr_t>(ptr) + bytes,
-                         static_cast<uint8_t*>(dev), false});
-  return RS_OK;
+  if (!c || !ptr || bytes == 0 || reinterpret_cast<uintptr_t>(ptr) + bytes < reinterpret_cast<uintptr_t>(ptr))
+    return RS_ERR_INVALID_ARG;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(ptr);
+  return reg_insert(c, RegRange{lo, lo + bytes, nullptr, false}) ? RS_OK : RS_ERR_INVALID_ARG;
 }
-
 
 int rs_host_unregister(rs_ctx* c, void* ptr) {
   if (!c || !ptr) return RS_ERR_INVALID_ARG;
-  {
-    std::shared_lock<std::shared_mutex> g(c->reg_mu);
-    for (const RegRange& r : c->reg)
-      if (r.lo == reinterpret_cast<uintptr_t>(ptr) && r.owned) return RS_ERR_INVALID_ARG;  // rs_host_free's
-  }
-  (void)reg_erase(c, ptr, false);
-  DeviceScope ds(c->engines[0]->device);
-  RS_HIP(hipHostUnregister(ptr));
-  return RS_OK;
+  return reg_erase(c, ptr, false) ? RS_OK : RS_ERR_INVALID_ARG;  // rs_host_alloc's are rs_host_free's
 }
 
 int rs_host_alloc(rs_ctx* c, size_t bytes, void** out) {
@@ -1623,8 +1631,11 @@ int rs_host_alloc(rs_ctx* c, size_t bytes, void** out) {
     rs::pinned_free(p);
     return RS_ERR_DEVICE;
   }
-  reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + n,
-                         static_cast<uint8_t*>(dev), true});
+  if (!reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + n,
+                              static_cast<uint8_t*>(dev), true})) {
+    rs::pinned_free(p);  // a caller range recorded over memory that was not the caller's
+    return RS_ERR_DEVICE;
+  }
   *out = p;
   return RS_OK;
 }
@@ -1649,7 +1660,7 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   const uint32_t grid = static_cast<uint32_t>(
       std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count) * 16, (bytes / 16 + 1023) / 1024)));
   rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
-  c->shared.last_kernel.store("copy_kernel");
+  c->shared.note(as_stream(stream), "copy_kernel");
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -1667,7 +1678,7 @@ int rs_sha256_batch(rs_ctx* c, const uint8_t* base, size_t stride, size_t len, s
   DeviceScope ds(e->device);
   const rs::Sha256Args a{base, stride, nullptr, nullptr, len, static_cast<uint32_t>(n), digests};
   if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
-  c->shared.last_kernel.store("sha256_kernel");
+  c->shared.note(as_stream(stream), "sha256_kernel");
   return RS_OK;
 }
 
@@ -1682,7 +1693,7 @@ int rs_sha256_batch_var(rs_ctx* c, const uint8_t* base, const uint64_t* offsets,
   DeviceScope ds(e->device);
   const rs::Sha256Args a{base, 0, offsets, lens, 0, static_cast<uint32_t>(n), digests};
   if (rs::launch_sha256(a, as_stream(stream))) return RS_ERR_DEVICE;
-  c->shared.last_kernel.store("sha256_kernel");
+  c->shared.note(as_stream(stream), "sha256_kernel");
   return RS_OK;
 }
 

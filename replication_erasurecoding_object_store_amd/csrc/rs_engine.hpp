@@ -78,9 +78,12 @@ int engine_apply_batch_plans(Engine* e, const uint8_t* data, size_t data_sp, con
 // deferred errors as for device masks.
 int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uint32_t* masks_dev, size_t S,
                             size_t N, int max_missing, hipStream_t s);
-// GPU address of [p, p + bytes) when it lies inside one rs_host_register'ed range of
-// the context, else nullptr.  Cheap when nothing is registered.
-uint8_t* ctx_registered(rs_ctx* c, const void* p, size_t bytes);
+// GPU address of [p, p + bytes) when it lies inside one range of page-locked memory
+// the context allocated itself (rs_host_alloc), else nullptr.  Only such memory is
+// ever read or written in place by a kernel: its pages are the driver's and never
+// move.  Caller memory -- rs_host_register'ed ranges included -- is staged
+// (DESIGN.md §2).  Cheap when the context owns no host memory.
+uint8_t* ctx_owned(rs_ctx* c, const void* p, size_t bytes);
 bool apply_ptrs_supported(int k, int m);  // engine_apply_batch_ptrs has a kernel for (k, m)
 
 }  // namespace rs

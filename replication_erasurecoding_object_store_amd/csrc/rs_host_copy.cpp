@@ -5,12 +5,11 @@
 
 #include <algorithm>
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 
 namespace rs {
 
-void stage_copy(void* dst, const void* src, size_t n);  // rs_host_util.hpp
+void stage_copy(void* dst, const void* src, size_t n, bool streaming);  // rs_host_util.hpp
 
 namespace {
 
@@ -19,7 +18,7 @@ namespace {
 // reads the destination back soon -- the GPU reads the staging over PCIe, an output
 // buffer goes to the network -- and a streaming store skips the read-for-ownership
 // of every destination line, a third of a cached copy's DRAM traffic.  Small copies
-// stay with memcpy.  RS_CO_NT_COPY=0 turns streaming off (A/B).
+// stay with memcpy.  The coalescer's opts.plain_copy turns streaming off (A/B).
 constexpr size_t kStreamMin = 16 << 10;
 
 __attribute__((target("avx2"))) void copy_streaming(uint8_t* dst, const uint8_t* src, size_t n) {
@@ -46,18 +45,16 @@ __attribute__((target("avx2"))) void copy_streaming(uint8_t* dst, const uint8_t*
   _mm_sfence();  // the streamed lines are globally visible before the slot is published
 }
 
-bool streaming_enabled() {
-  const char* e = std::getenv("RS_CO_NT_COPY");
-  if (e && std::atoi(e) == 0) return false;
+bool have_avx2() {
   __builtin_cpu_init();
   return __builtin_cpu_supports("avx2");
 }
 
 }  // namespace
 
-void stage_copy(void* dst, const void* src, size_t n) {
-  static const bool streaming = streaming_enabled();
-  if (streaming && n >= kStreamMin)
+void stage_copy(void* dst, const void* src, size_t n, bool streaming) {
+  static const bool avx2 = have_avx2();
+  if (streaming && avx2 && n >= kStreamMin)
     copy_streaming(static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n);
   else
     std::memcpy(dst, src, n);

@@ -40,9 +40,9 @@ void* pinned_alloc(size_t bytes, int numa_node);
 void pinned_free(void* p);
 // NUMA node of a GPU from sysfs (-1 if unknown).
 int device_numa_node(int device);
-// Copy into / out of pinned staging: streaming stores for shard-sized copies
-// (rs_host_copy.cpp).
-void stage_copy(void* dst, const void* src, size_t n);
+// Copy into / out of pinned staging: streaming stores for shard-sized copies unless
+// `streaming` is false (the coalescer's opts.plain_copy A/B setting; rs_host_copy.cpp).
+void stage_copy(void* dst, const void* src, size_t n, bool streaming = true);
 
 // Device memory on the calling thread's current device (callers hold a
 // DeviceScope).  ensure() only grows; hipFree synchronises the device first, so

@@ -17,6 +17,7 @@ computed by the HIP kernels behind the C-ABI; this module only marshals.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import List, Optional, Sequence, Union
 
 from . import _lib
@@ -90,9 +91,12 @@ class Service:
     def __init__(self, k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0):
         self._ctx = _create(k, m, device)
         self.k, self.m = k, m
+        self._arenas = weakref.WeakSet()  # invalidated before rs_destroy frees their memory
 
     def close(self) -> None:
         if getattr(self, "_ctx", None):
+            for a in list(getattr(self, "_arenas", ())):
+                a._invalidate()
             _lib.lib().rs_destroy(self._ctx)
             self._ctx = None
 
@@ -191,23 +195,48 @@ class Arena:
         _check(_lib.lib().rs_host_alloc(svc.ctx, n, ctypes.byref(p)))
         self._svc, self._base, self._size, self._off = svc, p.value, n, 0
         self._mem = (ctypes.c_uint8 * n).from_address(p.value)
+        self._views: List[memoryview] = []  # released when the memory goes away
+        svc._arenas.add(self)
 
     def Alloc(self, n: int) -> Optional[memoryview]:
         off = (self._off + 15) // 16 * 16
         if n <= 0 or self._base is None or off + n > self._size:
             return None
         self._off = off + n
-        return memoryview(self._mem).cast("B")[off:off + n]
+        root = memoryview(self._mem).cast("B")
+        v = root[off:off + n]
+        self._views += [v, root]
+        return v
 
     def Reset(self) -> None:
+        """Makes the whole arena free again (no view may be in use): the views handed
+        out so far are released."""
+        self._release_views()
         self._off = 0
+
+    def _release_views(self) -> None:
+        for v in reversed(self._views):
+            try:
+                v.release()
+            except BufferError:  # re-exported by the caller (e.g. numpy): cannot be revoked
+                pass
+        self._views = []
+
+    def _invalidate(self) -> None:
+        """The memory is about to be freed: every view handed out is released (using
+        one afterwards raises ValueError instead of touching freed memory) and Alloc
+        returns None."""
+        self._release_views()
+        self._base, self._mem = None, None
 
     def Close(self) -> None:
         """Frees the memory (no view may be in use); after the service closed,
         rs_destroy has freed it already."""
         if self._base is not None and self._svc.ctx:
-            _check(_lib.lib().rs_host_free(self._svc.ctx, self._base))
-        self._base, self._mem = None, None
+            base = self._base
+            self._invalidate()
+            _check(_lib.lib().rs_host_free(self._svc.ctx, base))
+        self._invalidate()
 
 
 def NewService(k: int = K, m: int = M, device: Union[int, str, Sequence[int]] = 0) -> Service:

@@ -446,15 +446,16 @@ def test_async_submit_reap_matches_oracle(gpu, k, m):
                                        (4, 2, 100000, "alloc"), (10, 4, 6554, "alloc"),
                                        # tiny shards: partial first column, byte-exact stores
                                        (4, 2, 1, "alloc"), (4, 2, 3, "alloc"), (10, 4, 17, "register")])
-def test_registered_buffers_run_in_place(gpu, k, m, S, mem):
-    """Objects whose shards lie in rs_host_register'ed memory (request bodies and
-    storage-node reads in a pinned arena) are encoded and
-    reconstructed by the coalescer in place -- the pointer-table kernel reads and
-    writes the caller's buffers, nothing is staged -- with the oracle's bytes and no
-    byte outside [0, S) of any shard written; pageable objects join the same
-    batches (staged); after rs_host_unregister the same calls are staged again.
-    Asynchronous calls run in place too (nothing left to copy at reap).  mem="alloc":
-    the same on context-owned page-locked memory (rs_host_alloc)."""
+def test_owned_buffers_run_in_place_registered_staged(gpu, k, m, S, mem):
+    """mem="alloc": objects whose shards lie in context-owned page-locked memory
+    (rs_host_alloc: request bodies and storage-node reads in an arena, SURVEY.md §8f
+    rank 4) are encoded and reconstructed by the coalescer in place -- the
+    pointer-table kernel reads and writes the caller's buffers, nothing is staged --
+    with the oracle's bytes and no byte outside [0, S) of any shard written; pageable
+    objects join the same batches (staged).  Asynchronous calls run in place too
+    (nothing left to copy at reap).  mem="register": the same calls on
+    rs_host_register'ed memory are staged (round 4: no kernel touches caller pages
+    in place), same bytes, same guard bytes."""
     import ctypes
     import mmap
 
@@ -544,7 +545,7 @@ def test_registered_buffers_run_in_place(gpu, k, m, S, mem):
                 assert rcs[j] == _lib.RS_OK
                 reaped.add(tags[j])
         assert reaped == set(range(0, n_obj, 2))
-        assert "apply_ptr_kernel" in L.rs_last_kernel(svc._ctx).decode()
+        assert ("apply_ptr_kernel" in L.rs_last_kernel(svc._ctx).decode()) == (mem == "alloc")
         for i in range(n_obj):
             for s in range(t):
                 assert np.array_equal(view(i, s), want[i, s]), ("reconstruct", i, s, lost[i])
@@ -702,6 +703,17 @@ def test_python_arena_encode_in_place(gpu):
         assert arena.Alloc(16 << 20) is None
         with pytest.raises(TypeError):
             svc.Encode([bytes(8)] * (k + m))  # read-only buffers are refused
+        # closing the service frees the arena's memory: its views are released first,
+        # so a stale view raises instead of touching freed memory
+        svc2 = CoalescingService(k, m)
+        a2 = svc2.NewArena(4096)
+        v2 = a2.Alloc(64)
+        v2[:] = bytes(range(64))
+        svc2.close()
+        with pytest.raises(ValueError):
+            v2[0]
+        assert a2.Alloc(16) is None
+        a2.Close()  # nothing left to free
     finally:
         arena.Close()
         svc.close()

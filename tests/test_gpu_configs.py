@@ -113,8 +113,11 @@ def test_config5_healer_mix_pinned_host(gpu):
         lost = rng.integers(0, t, N)
         # encode = "all parity missing"; repair = one lost shard anywhere
         masks = np.where(is_rec, full & ~(1 << lost), (1 << k) - 1).astype(np.uint32)
-        data = torch.empty((N, k, S), dtype=torch.uint8, pin_memory=True)
-        parity = torch.empty((N, m, S), dtype=torch.uint8, pin_memory=True)
+        # the context's own page-locked memory (rs_host_alloc): the only host memory
+        # kernels address in place
+        dn = eng.host_alloc(N * k * S).reshape(N, k, S)
+        pn = eng.host_alloc(N * m * S).reshape(N, m, S)
+        data, parity = torch.from_numpy(dn), torch.from_numpy(pn)
         g = torch.Generator(device="cuda").manual_seed(0x5EED0005)
         d_true = torch.randint(0, 256, (N, k, S), dtype=torch.uint8, device="cuda", generator=g)
         p_true = torch.empty((N, m, S), dtype=torch.uint8, device="cuda")
@@ -128,7 +131,6 @@ def test_config5_healer_mix_pinned_host(gpu):
         ref[:, k:] = 0
         rs_oracle.encode_batch_scalar(k, m, ref.reshape(-1), t * S, S, S, len(sample))
         assert np.array_equal(ref, buf)
-        dn, pn = data.numpy(), parity.numpy()
         lost_d = ((~masks[:, None] >> np.arange(k)[None, :]) & 1).astype(bool)
         lost_p = ((~masks[:, None] >> np.arange(k, t)[None, :]) & 1).astype(bool)
         for zc in (True, False):

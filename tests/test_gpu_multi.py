@@ -95,13 +95,17 @@ def test_multi_engine_context_batches_and_objects(gpu):
         assert "x2" in eng.backend()
         P = shard_pitch_for(S)
         g = torch.Generator(device="cuda").manual_seed(9)
-        data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g).cpu().numpy()
-        parity = np.zeros((N, m, P), np.uint8)
+        src = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g).cpu().numpy()
         for zc in (True, False):
             eng.set_host_zero_copy(zc)
+            # zero-copy runs on the context's own page-locked memory (rs_host_alloc);
+            # pageable memory is staged
             if zc:
-                eng.host_register(data)
-                eng.host_register(parity)
+                data = eng.host_alloc(N * k * P).reshape(N, k, P)
+                parity = eng.host_alloc(N * m * P).reshape(N, m, P)
+            else:
+                data, parity = np.empty((N, k, P), np.uint8), np.empty((N, m, P), np.uint8)
+            data[:] = src
             try:
                 parity[:] = 0
                 eng.encode_host(data, parity, S, N)
@@ -125,8 +129,8 @@ def test_multi_engine_context_batches_and_objects(gpu):
                 parity[N - 5, 1, 7] ^= 0x21
             finally:
                 if zc:
-                    eng.host_unregister(data)
-                    eng.host_unregister(parity)
+                    eng.host_free(data)
+                    eng.host_free(parity)
         eng.set_host_zero_copy(True)
 
         # per-object calls from many threads: least-busy dispatch over both engines

@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
   rs_coalescer_opts opts{0, 0, 0, 0, 0, 0, 0};
   if (const char* sw = std::getenv("SPIN")) opts.spin_waiters = std::atoi(sw);  // callers spin-waiting at once
   if (const char* mb = std::getenv("BATCH_MB")) opts.max_batch_bytes = std::strtoull(mb, nullptr, 10) << 20;
+  if (const char* pc = std::getenv("PLAIN_COPY")) opts.plain_copy = std::atoi(pc);  // A/B: memcpy staging copies
   if (argc > 5) opts.max_batch = std::strtoull(argv[5], nullptr, 10);
   if (argc > 6) opts.max_wait_us = static_cast<uint32_t>(std::atoi(argv[6]));
   const size_t obj = argc > 7 ? std::strtoull(argv[7], nullptr, 10) : 4096;
@@ -317,6 +318,13 @@ int main(int argc, char** argv) {
       static_cast<unsigned long long>(batches), batches ? static_cast<double>(stripes) / batches : 0.0,
       static_cast<unsigned long long>(maxb), opts.max_exec, opts.max_wait_us, opts.staged_dma, opts.inflight,
       async_mode ? depth : 0, static_cast<unsigned long long>(busy.load()), rotate_bytes >> 20, reg_mode);
+  if (co && std::getenv("CO_TIMING")) {  // launcher diagnostics (rs_co_timing)
+    uint64_t st = 0, la = 0, ex = 0, fw = 0, nb = 0;
+    rs_co_timing(co, &st, &la, &ex, &fw);
+    rs_co_stats(co, nullptr, &nb, nullptr, nullptr);
+    std::fprintf(stderr, "[rs_coalescer] batches %llu straggle_ms %.1f launch_ms %.1f exec_ms %.1f free_waits %llu\n",
+                 (unsigned long long)nb, st / 1e6, la / 1e6, ex / 1e6, (unsigned long long)fw);
+  }
   if (co) rs_coalescer_destroy(co);
   if (arena) {
     if (reg_mode == 2) {

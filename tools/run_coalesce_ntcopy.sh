@@ -1,12 +1,12 @@
 #!/bin/bash
 # A/B: staging copies with streaming stores (default) vs plain memcpy
-# (RS_CO_NT_COPY=0), staged per-object calls on DRAM-resident heap objects
+# (PLAIN_COPY=1 -> rs_coalescer_opts.plain_copy), staged per-object calls on DRAM-resident heap objects
 # (ROTATE_MB=1024), RS(4+2) mix, 64 blocking callers on the GPU's NUMA node,
 # alternating A B A B per size.
 set -o pipefail
 B=tools/coalesce_bench
 run() {
-  echo "# RS_CO_NT_COPY=${RS_CO_NT_COPY:-1} $*" >&2
+  echo "# PLAIN_COPY=${PLAIN_COPY:-0} $*" >&2
   timeout -k 5 90 "$@"
   local rc=$?
   if [ $rc -ge 124 ]; then exit $rc; fi
@@ -18,8 +18,8 @@ PIN="taskset -c $CPUS"
 export ROTATE_MB=1024
 for OBJ in ${SIZES:-102400 819200 1536000}; do
   for rep in 1 2; do
-    for NT in 1 0; do
-      RS_CO_NT_COPY=$NT run $PIN $B 64 2 mix co 0 0 $OBJ
+    for PC in 0 1; do
+      PLAIN_COPY=$PC run $PIN $B 64 2 mix co 0 0 $OBJ
     done
   done
 done
