@@ -50,7 +50,7 @@ extern "C" {
 #define RS_ERR_NO_DEVICE 17     /* no usable GPU */
 #define RS_ERR_DEVICE 18        /* HIP runtime failure */
 #define RS_ERR_NOT_SUPPORTED 19 /* klauspost ErrNotSupported "operation not supported" */
-#define RS_ERR_BUSY 20          /* coalescer: every batch awaits rs_co_reap; reap, then resubmit */
+#define RS_ERR_BUSY 20          /* coalescer: no staging batch free (all executing or awaiting rs_co_reap) */
 
 /* memory kinds for the batched entry points */
 #define RS_MEM_DEVICE 0 /* pointers are device memory; call is asynchronous on `stream` */
@@ -267,14 +267,20 @@ int rs_co_encode_hash_many(rs_coalescer *co, size_t n_objects, uint8_t *const *s
  * reconstruct -> every missing (len 0) shard filled with S bytes (lens is not
  * written).  Until then the caller keeps every shard buffer valid and untouched
  * (the arrays of pointers and lengths may be reused at once).  A call rejected at
- * submit returns its code and is never reaped; RS_ERR_BUSY: every staging batch
- * holds unreaped calls -- reap, then submit again (submit never blocks).  An object
+ * submit returns its code and is never reaped; RS_ERR_BUSY: no staging batch is
+ * free -- each is executing on a GPU or holds finished calls not reaped yet; wait
+ * until some reap has returned calls (a reaper can signal that), then submit again
+ * (submit never blocks).  An object
  * with nothing to compute (a reconstruct with nothing missing, m == 0) is rejected
  * with RS_ERR_NOT_SUPPORTED.
  * rs_co_reap: up to max completed calls -> tags[i], rcs[i]; copies their outputs
  * into the callers' buffers on the reaping thread.  Waits up to timeout_us for at
  * least one (0: poll, < 0: until one completes); returns how many (a negative
- * code on bad arguments).  Any number of threads may submit and reap.  Reap every
+ * code on bad arguments).  It returns 0 at once, or as soon as it wakes, once
+ * rs_coalescer_destroy has begun; still, no thread may be inside rs_co_reap when
+ * that call frees the coalescer, so stop reapers first (a finite timeout_us lets
+ * them notice).  Any number of threads may submit and reap; each reaper copies the
+ * outputs of the calls it returns, so several reapers share that work.  Reap every
  * submitted call before rs_coalescer_destroy. */
 int rs_co_submit_encode(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, uint64_t tag);
 int rs_co_submit_reconstruct(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, uint64_t tag);

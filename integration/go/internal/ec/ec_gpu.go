@@ -21,6 +21,7 @@ import (
 	"log"
 	"runtime"
 	"sync"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
@@ -34,26 +35,41 @@ import (
 // with the same shard length share one device launch (group commit), while each
 // call keeps rs_encode / rs_reconstruct's exact contract.  One Service drives
 // every MI355X of the node (rs_create_multi): the coalescer spreads its batches
-// over the GPUs.  On a host with no usable GPU, cpu is the reference's own codec
-// (klauspost, configured exactly as ec.go:26) and every call goes to it.
+// over the GPUs.  enc is the reference's own codec (klauspost, configured exactly
+// as ec.go:26) on every host: Split (no arithmetic) always runs there, and on a
+// host with no usable GPU (gpu == false) so does every other call.
 //
 // Encode and Reconstruct use the coalescer's asynchronous calls: the request
 // goroutine stages its object (rs_co_submit_*, no blocking in C), then parks on a
-// channel; one reaper goroutine collects finished calls (rs_co_reap) and wakes
-// their goroutines.  A blocking cgo call would instead hold an OS thread per
-// in-flight request and pay a futex sleep and wake-up per object.
+// channel; reaper goroutines collect finished calls (rs_co_reap, which also copies
+// the staged outputs into the callers' slices -- so several reapers share that copy
+// work) and wake their goroutines.  A blocking cgo call would instead hold an OS
+// thread per in-flight request and pay a futex sleep and wake-up per object.
 type Service struct {
 	ctx *C.rs_ctx
 	co  *C.rs_coalescer
-	cpu reedsolomon.Encoder
+	enc reedsolomon.Encoder
+	gpu bool
 
 	mu      sync.Mutex
 	nextTag uint64
 	waiting map[uint64]chan C.int
+
+	// back-pressure: a submit that finds no free staging batch (RS_ERR_BUSY) waits
+	// for the next reap instead of spinning
+	freeMu   sync.Mutex
+	freeCond *sync.Cond
+	reaped   uint64 // reap rounds so far (freeMu)
+
+	closing atomic.Bool
+	reapers sync.WaitGroup
 }
 
+// reapTimeoutUs bounds one rs_co_reap wait so a reaper notices Close.
+const reapTimeoutUs = 100000
+
 // call runs one asynchronous coalescer call: submit(tag) stages it; the result
-// arrives from the reaper.  The caller keeps its shard buffers pinned until then.
+// arrives from a reaper.  The caller keeps its shard buffers pinned until then.
 func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
 	ch := make(chan C.int, 1)
 	s.mu.Lock()
@@ -62,27 +78,46 @@ func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
 	s.waiting[tag] = ch
 	s.mu.Unlock()
 	for {
+		s.freeMu.Lock()
+		seen := s.reaped
+		s.freeMu.Unlock()
 		rc := submit(C.uint64_t(tag))
 		if rc == C.RS_OK {
 			return toErr(<-ch)
 		}
-		if rc != C.RS_ERR_BUSY { // rejected: never reaped
+		if rc != C.RS_ERR_BUSY || s.closing.Load() { // rejected: never reaped
 			s.mu.Lock()
 			delete(s.waiting, tag)
 			s.mu.Unlock()
 			return toErr(rc)
 		}
-		runtime.Gosched() // every staging batch awaits the reaper: let it run, retry
+		// no staging batch is free: batches still executing, or finished ones whose
+		// calls are not reaped yet -- sleep until a reaper has released some (a reap
+		// since `seen` means slots came back), then submit again
+		s.freeMu.Lock()
+		for s.reaped == seen && !s.closing.Load() {
+			s.freeCond.Wait()
+		}
+		s.freeMu.Unlock()
 	}
 }
 
-// reap delivers finished calls to their goroutines (one goroutine per Service).
+// reap delivers finished calls to their goroutines; several run per Service.
+// rs_co_reap returns 0 on its timeout (or when the coalescer stops) and a negative
+// code on bad arguments, which ends this reaper.
 func (s *Service) reap() {
+	defer s.reapers.Done()
 	const max = 256
 	tags := (*[max]C.uint64_t)(C.malloc(max * C.size_t(unsafe.Sizeof(C.uint64_t(0)))))
 	rcs := (*[max]C.int)(C.malloc(max * C.size_t(unsafe.Sizeof(C.int(0)))))
-	for {
-		n := int(C.rs_co_reap(s.co, &tags[0], &rcs[0], max, -1))
+	defer C.free(unsafe.Pointer(tags))
+	defer C.free(unsafe.Pointer(rcs))
+	for !s.closing.Load() {
+		n := int(C.rs_co_reap(s.co, &tags[0], &rcs[0], max, reapTimeoutUs))
+		if n < 0 {
+			log.Printf("EC Driver: rs_co_reap failed: %v; reaper stops", toErr(C.int(-n)))
+			return
+		}
 		for i := 0; i < n; i++ {
 			s.mu.Lock()
 			ch := s.waiting[uint64(tags[i])]
@@ -90,7 +125,28 @@ func (s *Service) reap() {
 			s.mu.Unlock()
 			ch <- rcs[i]
 		}
+		if n > 0 {
+			s.freeMu.Lock()
+			s.reaped++
+			s.freeCond.Broadcast()
+			s.freeMu.Unlock()
+		}
 	}
+}
+
+// Close stops the reapers and frees the engine.  No call may be in flight (an
+// IEcDriver lives for the process in the reference; this is for tests and a
+// graceful shutdown).
+func (s *Service) Close() {
+	if !s.gpu || s.closing.Swap(true) {
+		return
+	}
+	s.freeMu.Lock()
+	s.freeCond.Broadcast()
+	s.freeMu.Unlock()
+	s.reapers.Wait()
+	C.rs_coalescer_destroy(s.co)
+	C.rs_destroy(s.ctx)
 }
 
 // Keep klauspost's exported sentinels so errors.Is and %v output match ec.go.
@@ -122,16 +178,18 @@ func toErr(rc C.int) error {
 // runtime error; a GPU-less host gets the CPU codec instead.
 func NewService() interfaces.IEcDriver {
 	log.Println("--- Initializing EC Driver (Reed-Solomon, MI355X) ---")
+	// the reference's codec, exactly ec.go:26: Split on every host, everything on a
+	// GPU-less one
+	enc, err := reedsolomon.New(config.K, config.M, reedsolomon.WithAutoGoroutines(runtime.NumCPU()))
+	if err != nil {
+		log.Fatalf("Failed to create Reed-Solomon encoder: %v", err)
+	}
 	var ctx *C.rs_ctx
 	rc := C.rs_create_multi(C.int(config.K), C.int(config.M), 0 /* every visible gfx950 GPU */, 0, &ctx)
 	if rc == C.RS_ERR_NO_DEVICE {
-		enc, err := reedsolomon.New(config.K, config.M, reedsolomon.WithAutoGoroutines(runtime.NumCPU()))
-		if err != nil {
-			log.Fatalf("Failed to create Reed-Solomon encoder: %v", err)
-		}
 		log.Printf("EC Driver loaded (k=%d, m=%d): no MI355X visible (%v), using klauspost/reedsolomon on the CPU\n",
 			config.K, config.M, toErr(rc))
-		return &Service{cpu: enc}
+		return &Service{enc: enc}
 	}
 	if rc != C.RS_OK {
 		log.Fatalf("Failed to create Reed-Solomon encoder: %v", toErr(rc))
@@ -141,71 +199,22 @@ func NewService() interfaces.IEcDriver {
 		log.Fatalf("Failed to create Reed-Solomon batch coalescer: %v", toErr(rc))
 	}
 	log.Printf("EC Driver loaded (k=%d, m=%d) on %s\n", config.K, config.M, C.GoString(C.rs_backend(ctx)))
-	s := &Service{ctx: ctx, co: co, waiting: make(map[uint64]chan C.int)}
-	go s.reap()
+	s := &Service{ctx: ctx, co: co, enc: enc, gpu: true, waiting: make(map[uint64]chan C.int)}
+	s.freeCond = sync.NewCond(&s.freeMu)
+	// reapers share rs_co_reap's output copies: one per 4 Ps, 1..8
+	n := min(max(runtime.GOMAXPROCS(0)/4, 1), 8)
+	s.reapers.Add(n)
+	for i := 0; i < n; i++ {
+		go s.reap()
+	}
 	return s
 }
 
-// Split is klauspost v1.12.1's Split (reedsolomon.go) in Go -- no arithmetic, so it
-// never reaches the GPU (ec.go:48-50, writeservice.go:218,382):
-//   - perShard = ceil(len/K); len(data) == 0 -> ErrShortData;
-//   - spare capacity of `data` is used before anything is allocated: data is
-//     extended to min(cap, (K+M)*perShard) and zeroed past len, so with enough
-//     capacity every shard -- parity included -- aliases the caller's buffer;
-//   - only the shards that do not fit get fresh zeroed storage, the first of them
-//     holding the tail of the payload;
-//   - every shard is capped at perShard (data[:perShard:perShard]).
+// Split is klauspost's own Split (ec.go:48-50, writeservice.go:218,382): it does no
+// arithmetic, so the GPU build delegates to the reference codec on every host --
+// the same shards, aliasing and use of data's spare capacity as before.
 func (s *Service) Split(data []byte) ([][]byte, error) {
-	if s.cpu != nil {
-		return s.cpu.Split(data)
-	}
-	if len(data) == 0 {
-		return nil, reedsolomon.ErrShortData
-	}
-	k, total := config.K, config.K+config.M
-	if total == 1 {
-		return [][]byte{data}, nil
-	}
-	dataLen := len(data)
-	perShard := (len(data) + k - 1) / k
-	needTotal := total * perShard
-	if cap(data) > len(data) {
-		if cap(data) > needTotal {
-			data = data[:needTotal]
-		} else {
-			data = data[:cap(data)]
-		}
-		clear(data[dataLen:])
-	}
-	var padding [][]byte
-	if len(data) < needTotal {
-		fullShards := len(data) / perShard // shards that fit in data (its spare capacity included)
-		buf := make([]byte, (total-fullShards)*perShard)
-		padding = make([][]byte, total-fullShards)
-		for i := range padding {
-			padding[i] = buf[i*perShard : (i+1)*perShard : (i+1)*perShard]
-		}
-		if dataLen > perShard*fullShards { // the payload's tail does not fill a whole shard
-			copyFrom := data[perShard*fullShards : dataLen]
-			for i := range padding {
-				if len(copyFrom) == 0 {
-					break
-				}
-				copyFrom = copyFrom[copy(padding[i], copyFrom):]
-			}
-		}
-	}
-	dst := make([][]byte, total)
-	i := 0
-	for ; i < total && len(data) >= perShard; i++ {
-		dst[i] = data[:perShard:perShard]
-		data = data[perShard:]
-	}
-	for j := 0; i+j < total; j++ {
-		dst[i+j] = padding[0]
-		padding = padding[1:]
-	}
-	return dst, nil
+	return s.enc.Split(data)
 }
 
 // shardArgs builds C arrays of shard pointers and lengths.  Every Go pointer
@@ -227,8 +236,8 @@ func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, fu
 
 // Encode fills shards[K:] in place (ec.go:54-56).
 func (s *Service) Encode(shards [][]byte) error {
-	if s.cpu != nil {
-		return s.cpu.Encode(shards)
+	if !s.gpu {
+		return s.enc.Encode(shards)
 	}
 	if len(shards) != config.K+config.M {
 		return reedsolomon.ErrTooFewShards
@@ -243,8 +252,8 @@ func (s *Service) Encode(shards [][]byte) error {
 // Reconstruct fills every empty entry, data and parity (ec.go:59-61;
 // readservice.go:285 and poller.go:282 rely on all nil entries being filled).
 func (s *Service) Reconstruct(shards [][]byte) error {
-	if s.cpu != nil {
-		return s.cpu.Reconstruct(shards)
+	if !s.gpu {
+		return s.enc.Reconstruct(shards)
 	}
 	if len(shards) != config.K+config.M {
 		return reedsolomon.ErrTooFewShards
@@ -344,9 +353,9 @@ func (s *Service) EncodeHash(shards [][]byte, valueLen int) (sum [32]byte, err e
 func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 	t := config.K + config.M
 	errs = make([]error, len(objects))
-	if s.cpu != nil {
+	if !s.gpu {
 		for i, shards := range objects {
-			errs[i] = s.cpu.Reconstruct(shards)
+			errs[i] = s.enc.Reconstruct(shards)
 		}
 		return errs
 	}
@@ -404,11 +413,12 @@ func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 }
 
 // Arena hands out []byte backed by page-locked C memory the engine owns
-// (rs_host_alloc; registered for in-place calls like rs_host_register'ed memory,
-// but pinned for life, so the OS cannot migrate its pages under a call): a call whose shards -- those it reads and those it fills --
-// all come from an arena runs in place on the GPU, with no staging copy of the
-// request body and the parity written straight into the caller's slices
-// (DESIGN.md §6, "In place on registered buffers").  Meant for buffers the service
+// (rs_host_alloc: pinned by the driver for life, so no page can move under a call;
+// the only host memory the engine's kernels address in place -- Go heap slices and
+// rs_host_register'ed memory are staged): a call whose shards -- those it reads and
+// those it fills -- all come from an arena runs in place on the GPU, with no staging
+// copy of the request body and the parity written straight into the caller's slices
+// (DESIGN.md §6, "In place in an arena").  Meant for buffers the service
 // owns end to end: the gateway reading a request body into Alloc'd memory before
 // Split, parity slices for the storage-node uploads, the healer's shard fetches.
 // A bump allocator: Alloc until full, Reset when none of its slices is in use.
@@ -423,7 +433,7 @@ type Arena struct {
 
 // NewArena allocates `size` bytes of page-locked memory for in-place calls.
 func (s *Service) NewArena(size int) (*Arena, error) {
-	if s.cpu != nil || size <= 0 {
+	if !s.gpu || size <= 0 {
 		return nil, nil
 	}
 	n := (size + 4095) &^ 4095

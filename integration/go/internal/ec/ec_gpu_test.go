@@ -74,7 +74,7 @@ func TestNoGPUFallsBackToKlauspost(t *testing.T) {
 	if !ok {
 		t.Fatal("NewService must return *Service")
 	}
-	if svc.cpu == nil {
+	if svc.gpu {
 		t.Skip("a GPU is visible; hide it to exercise the fallback")
 	}
 	ref, _ := reedsolomon.New(config.K, config.M)
@@ -174,11 +174,11 @@ func TestEncodeHashMatchesSha256(t *testing.T) {
 	}
 }
 
-// Shards allocated from an Arena (registered C memory) are encoded and
-// reconstructed in place; the bytes equal klauspost's.
+// Shards allocated from an Arena (the engine's page-locked C memory) are encoded
+// and reconstructed in place; the bytes equal klauspost's.
 func TestArenaInPlaceMatchesKlauspost(t *testing.T) {
 	svc := NewService().(*Service)
-	if svc.cpu != nil {
+	if !svc.gpu {
 		t.Skip("no MI355X visible")
 	}
 	ref, err := reedsolomon.New(config.K, config.M, reedsolomon.WithAutoGoroutines(runtime.NumCPU()))

@@ -331,6 +331,10 @@ struct rs_coalescer {
 
   ~rs_coalescer() {
     stop.store(true, std::memory_order_release);
+    {
+      std::lock_guard<std::mutex> g(done_mu);  // a reaper waiting without a timeout returns 0
+      done_cv.notify_all();
+    }
     for (auto& d : disp) {
       poke(d.get());
       d->launcher_idle.store(true);

@@ -144,6 +144,26 @@ constexpr int out_cpol() {
   return (E == 1 && K >= 8) ? kCpolSc1 : (E == 2 && K >= 10) ? (kCpolSc1 | kCpolNt) : kCpolNt;
 }
 
+// Per-stripe kernels sized for E > 2 outputs (device masks without a caller bound:
+// E = M) compute only the rows a task's stripe(s) miss and then pick, in a
+// wave-uniform branch, the store sequence of that row count: 1 or 2 rows store with
+// the bounded E = 1 / 2 kernels' policy (out_cpol<K, 1 or 2>) and issue no dropped
+// stores for the other rows, more rows store E rows with out_cpol<K, E> (round 4).
+// Every store instruction has one policy for all its lanes and every 128-B output
+// line one writer instruction.  RS_WAVE_ROWS=0 builds the single-path kernels (A/B).
+#ifndef RS_WAVE_ROWS
+#define RS_WAVE_ROWS 1
+#endif
+// RS_WAVE_ROWS_CPOL=0: the 1- and 2-row paths store with out_cpol<K, E> too (A/B of
+// the dropped stores alone).
+#ifndef RS_WAVE_ROWS_CPOL
+#define RS_WAVE_ROWS_CPOL 1
+#endif
+template <int K, int E, int NR>
+constexpr int path_cpol() {
+  return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
+}
+
 // 16-B store at base + off, or nothing at all when !live: a raw buffer
 // store whose offset then fails the range check, so the hardware drops it -- no
 // branch around the store and no sink line to write back.  off < 2 GiB.
@@ -383,6 +403,24 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
 #pragma unroll
     for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, PER_STRIPE ? pv.in_idx(c) : uin[c]) + off);
 
+    const uint32_t n_out = PER_STRIPE ? pv.n_out() : u_nout;
+    // stores rows [0, NR) of the task (the rest of the launch's E rows need none)
+    // with cache policy CPOL; dropped per lane past the stripe's outputs
+    auto emit = [&](auto nr_tag, auto cpol_tag, const auto& yy) {
+      constexpr int NR = decltype(nr_tag)::value;
+      constexpr int CPOL = decltype(cpol_tag)::value;
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        store16_or_drop<CPOL>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                              full && static_cast<uint32_t>(r) < n_out, yy[r]);
+      if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
+        const bool part = col == a.full_cols;
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          store_part_or_drop<CPOL>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
+                                   part && static_cast<uint32_t>(r) < n_out, yy[r], nb);
+      }
+    };
     u32x4 y[E];
     if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
@@ -403,21 +441,17 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         y[r] = y[0];  // dropped unless computed
         if (static_cast<uint32_t>(r) < nrow) y[r] = gf_row_ix<K, M>(plan, ix, r);
       }
+      if (RS_WAVE_ROWS && n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
+        if (n_out <= 1u)
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
+        else
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+        continue;
+      }
     } else {
       gf_rows<K, M, 0, E>(plan, x, y);
     }
-    const uint32_t n_out = PER_STRIPE ? pv.n_out() : u_nout;
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-      store16_or_drop<out_cpol<K, E>()>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
-                                        full && static_cast<uint32_t>(r) < n_out, y[r]);
-    if (nb != 0u && blk + 1u == bps) {  // wave-uniform: this task holds the stripe's partial column
-      const bool part = col == a.full_cols;
-#pragma unroll
-      for (int r = 0; r < E; ++r)
-        store_part_or_drop<out_cpol<K, E>()>(out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]), off,
-                                             part && static_cast<uint32_t>(r) < n_out, y[r], nb);
-    }
+    emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
   }
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, bad);
 }
@@ -843,36 +877,6 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       }
     }
     const uint32_t nmax = nA > nB ? nA : nB;
-    u32x4 y[E];
-    if constexpr (E <= 2) {
-      // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
-      // launch computes a row it does not store): x[K] only, no index array
-      if (!diff)
-        gf_rows<K, M, 0, E>(planA, x, y);
-      else
-        gf_rows2<K, M, E>(planA, planB, inB, x, y);
-    } else {
-    Idx3 ix[K][4];
-#pragma unroll
-    for (int c = 0; c < K; ++c)
-#pragma unroll
-      for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
-    if (!diff) {
-      y[0] = gf_row_ix<K, M>(planA, ix, 0);
-#pragma unroll
-      for (int r = 1; r < E; ++r) {
-        y[r] = y[0];
-        if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix<K, M>(planA, ix, r);
-      }
-    } else {
-      y[0] = gf_row_ix2<K, M>(planA, planB, inB, ix, 0);
-#pragma unroll
-      for (int r = 1; r < E; ++r) {
-        y[r] = y[0];
-        if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix2<K, M>(planA, planB, inB, ix, r);
-      }
-    }
-    }
     // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
     const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
                                                         0x7FFFFFFF, 0x00020000);
@@ -880,14 +884,57 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     const uint32_t nl = inB ? nB : nA;
     const bool fullc = live && colr < a.full_cols;
     const bool part = nb != 0u && live && colr == a.full_cols;
+    // stores rows [0, NR) with cache policy CPOL, dropped per lane past its stripe's outputs
+    auto emit = [&](auto nr_tag, auto cpol_tag, const auto& yy) {
+      constexpr int NR = decltype(nr_tag)::value;
+      constexpr int CPOL = decltype(cpol_tag)::value;
 #pragma unroll
-    for (int r = 0; r < E; ++r)
-      __builtin_amdgcn_raw_buffer_store_b128(y[r], oout, fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
-                                             r * pitch, out_cpol<K, E>());
-    if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
+      for (int r = 0; r < NR; ++r)
+        __builtin_amdgcn_raw_buffer_store_b128(yy[r], oout, fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
+                                               r * pitch, CPOL);
+      if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
 #pragma unroll
-      for (int r = 0; r < E; ++r)
-        store_part_rsrc<out_cpol<K, E>()>(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, y[r], nb);
+        for (int r = 0; r < NR; ++r)
+          store_part_rsrc<CPOL>(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, yy[r], nb);
+      }
+    };
+    if constexpr (E <= 2) {
+      // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
+      // launch computes a row it does not store): x[K] only, no index array
+      u32x4 y[E];
+      if (!diff)
+        gf_rows<K, M, 0, E>(planA, x, y);
+      else
+        gf_rows2<K, M, E>(planA, planB, inB, x, y);
+      emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+    } else {
+      u32x4 y[E];
+      Idx3 ix[K][4];
+#pragma unroll
+      for (int c = 0; c < K; ++c)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+      if (!diff) {
+        y[0] = gf_row_ix<K, M>(planA, ix, 0);
+#pragma unroll
+        for (int r = 1; r < E; ++r) {
+          y[r] = y[0];
+          if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix<K, M>(planA, ix, r);
+        }
+      } else {
+        y[0] = gf_row_ix2<K, M>(planA, planB, inB, ix, 0);
+#pragma unroll
+        for (int r = 1; r < E; ++r) {
+          y[r] = y[0];
+          if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix2<K, M>(planA, planB, inB, ix, r);
+        }
+      }
+      if (RS_WAVE_ROWS && nmax <= 1u)  // wave-uniform: the bounded kernels' store policy
+        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
+      else if (RS_WAVE_ROWS && nmax == 2u)
+        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+      else
+        emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
     }
     c0 += step_c;
     s0 += step_s;

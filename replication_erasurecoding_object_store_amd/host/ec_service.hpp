@@ -315,8 +315,8 @@ class Service final : public IEcDriver {
 };
 
 // The Go shim's Arena (ec_gpu.go): slices backed by page-locked memory the
-// context owns (rs_host_alloc, eligible for in-place calls like rs_host_register'ed
-// memory and pinned for life), so a coalesced call whose shards -- read and
+// context owns (rs_host_alloc: pinned by the driver for life, the only host memory
+// the kernels address in place), so a coalesced call whose shards -- read and
 // filled -- all come from an arena runs in place on the GPU: no staging copy of the
 // request body, parity written straight into the caller's slices.  Allocations are
 // 16-B aligned (the in-place kernel's condition); anything else is staged as usual.
