@@ -582,7 +582,13 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 // Inputs stream through a window of kBsWindow loads in flight: input c+W is
 // loaded once input c has been transposed, so only W inputs' raw bytes are live
 // (registers for more waves) while W 2 KiB loads per wave stay in flight.
-constexpr int kBsWindow = 5;  // profiles/r01_ab_bs_window_occupancy.log
+#ifndef RS_BS_WINDOW
+#define RS_BS_WINDOW 5
+#endif
+#ifndef RS_BS_OCC
+#define RS_BS_OCC 3
+#endif
+constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
 
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2 /* nt */));
@@ -644,7 +650,7 @@ __device__ __forceinline__ FlatCol flat_col(const KernelArgs& a, uint32_t s0, ui
 // Full columns store 16 B; the lane holding a stripe's partial last column stores
 // it byte-exact in a wave-uniform branch taken by tasks that contain one.
 template <int K, int M>
-__global__ __launch_bounds__(256, 3) void encode_bitsliced_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
