@@ -212,6 +212,12 @@ struct Lane {
 struct UploadSlot {
   PinnedBuf host;
   DevBuf dev;
+  // bucketed device-mask launches (launch_bucketed): two banks of 4 count words, then
+  // three lists of {stripe, plan} entries.  The launch on this slot accumulates into
+  // bank `gen` and zeroes the other bank for the slot's next launch.
+  DevBuf lists;
+  uint32_t gen = 0;
+  bool lists_dirty = true;  // both banks need zeroing (new buffer, or a launch failed)
   hipEvent_t done = nullptr;
   bool used = false;
   bool busy = false;
@@ -289,6 +295,7 @@ struct Engine {
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
   bool out_pad = false;                   // out-of-place outputs likewise (rs_set_out_pad_writes)
+  bool devmask_buckets = true;            // E = M device-mask reconstructs: bucketed lists (launch_bucketed)
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -582,16 +589,10 @@ rs::KernelArgs make_args(Engine* e, const Layout& L, size_t S, size_t N) {
 
 // e_out = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
 // #missing for per-stripe patterns).
-int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s) {
-  if (args.n_stripes == 0 || args.shard_len == 0 || e_out <= 0) return RS_OK;
-  rs::KernelArgs a = args;
-  // the encode plan with a verified generated XOR program -> bitsliced kernel
-  a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
-  a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
-  if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
+// rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
+// the slot (inputs' padding read, the written rows' padding written).
+void apply_pad_writes(const Engine* e, rs::KernelArgs& a) {
   if ((e->parity_pad && a.data_inputs && !a.out) || (e->out_pad && a.out)) {
-    // rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
-    // the slot (inputs' padding read, the written rows' padding written)
     const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
     if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
       a.shard_len = static_cast<uint32_t>(s_eff);
@@ -599,6 +600,16 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
       a.full_cols = static_cast<uint32_t>(s_eff / 16);
     }
   }
+}
+
+int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s) {
+  if (args.n_stripes == 0 || args.shard_len == 0 || e_out <= 0) return RS_OK;
+  rs::KernelArgs a = args;
+  // the encode plan with a verified generated XOR program -> bitsliced kernel
+  a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
+  a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
+  if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
+  apply_pad_writes(e, a);
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
   const char* name =
       rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
@@ -816,8 +827,9 @@ struct UploadGuard {
   }
 };
 
-int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
-                   const uint32_t** dev) {
+// A free slot of the ring whose last reader has finished, held busy by g (its release
+// records the slot's event on s after the kernels the caller launches next).
+int slot_acquire(Engine* e, hipStream_t s, UploadGuard* g, UploadSlot** out) {
   UploadSlot* u = nullptr;
   {
     std::unique_lock<std::mutex> lk(e->upload_mu);
@@ -839,11 +851,70 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   g->s = s;
   if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
+  *out = u;
+  return RS_OK;
+}
+
+int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
+                   const uint32_t** dev) {
+  UploadSlot* u = nullptr;
+  int rc = slot_acquire(e, s, g, &u);
+  if (rc) return rc;
   u->host.numa = e->numa;
   if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
   std::memcpy(u->host.p, masks, n * 4);
   RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
   *dev = static_cast<const uint32_t*>(u->dev.p);
+  return RS_OK;
+}
+
+// Device masks without a caller bound (E = M): a pre-pass sorts the stripes into
+// lists by erasure count on the device, then each list runs on the kernel sized for
+// it -- 1 and 2 missing shards on the bounded E = 1 / 2 kernels (their store policy,
+// registers and occupancy), 3 or more on the E = M kernel -- with no host sync
+// (round 4).  The list kernels read their list's length on the device; an empty
+// list's launch ends at once.  Falls back to one E = M launch when (k, m) has no list
+// kernels or the layout exceeds their 32-bit addressing.
+int launch_bucketed(Engine* e, const rs::KernelArgs& args, hipStream_t s) {
+  rs::KernelArgs a = args;
+  if (a.n_stripes == 0 || a.shard_len == 0) return RS_OK;
+  apply_pad_writes(e, a);
+  if (!e->devmask_buckets || !e->have_lut || e->m <= 2 || !rs::bucketed_supported(a))
+    return launch(e, args, e->m, true, s);
+  if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
+  const size_t N = a.n_stripes;
+  UploadGuard ug;
+  UploadSlot* u = nullptr;
+  int rc = slot_acquire(e, s, &ug, &u);
+  if (rc) return rc;
+  const size_t lists_off = 64;  // bytes: two banks of 4 count words, padded
+  const void* before = u->lists.p;
+  if (u->lists.ensure(lists_off + 3 * N * 8)) return RS_ERR_DEVICE;
+  if (u->lists.p != before || u->lists_dirty) {
+    RS_HIP(hipMemsetAsync(u->lists.p, 0, lists_off, s));
+    u->gen = 0;
+    u->lists_dirty = false;
+  }
+  uint32_t* words = static_cast<uint32_t*>(u->lists.p);
+  uint32_t* counts = words + 4 * u->gen;
+  uint32_t* lists = words + lists_off / 4;
+  u->lists_dirty = true;  // until every launch below is queued
+  const rs::BucketArgs b{a.present_masks, a.lut, static_cast<uint32_t>(N), a.full_mask, lists, counts,
+                         words + 4 * (u->gen ^ 1u), a.status};
+  if (!rs::launch_buckets(b, static_cast<uint32_t>(e->cu_count), s)) return RS_ERR_DEVICE;
+  for (int q = 0; q < 3; ++q) {
+    const int eq = q < 2 ? q + 1 : e->m;
+    rs::KernelArgs ka = a;
+    ka.stripe_list = lists + static_cast<size_t>(2 * q) * N;
+    ka.list_count = counts + q;
+    const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, eq);
+    if (!rs::launch_apply_list(ka, eq, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s))
+      return RS_ERR_DEVICE;
+  }
+  u->gen ^= 1u;
+  u->lists_dirty = false;
+  e->shared->note(s, rs::bucketed_name(a));  // the bucketed launch: bucket_kernel + three list kernels
+  RS_HIP(hipGetLastError());
   return RS_OK;
 }
 
@@ -1096,7 +1167,9 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
     if (!out_layout_ok(out_sp, pitch, S, N, bound)) return RS_ERR_INVALID_ARG;
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
     a.present_masks = masks;
-    return launch(e, a, bound, true, s);
+    // no caller bound: bucketed by erasure count (the coalescer always passes its
+    // batch's bound, so its small mixed batches keep one launch)
+    return max_missing == 0 ? launch_bucketed(e, a, s) : launch(e, a, bound, true, s);
   }
   if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
   int most = 0;
@@ -1517,7 +1590,7 @@ int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8
   rs::KernelArgs a = make_args(e, L, S, N);
   a.plans = static_cast<const uint8_t*>(e->d_plans.p);
   a.present_masks = masks_dev;
-  return launch(e, a, c->m, true, as_stream(stream));
+  return launch_bucketed(e, a, as_stream(stream));
 }
 
 // Waits for stream s; returns and clears its deferred per-stripe errors (bit 0: a
@@ -1714,6 +1787,12 @@ int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
 int rs_set_out_pad_writes(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->out_pad = enable != 0;
+  return RS_OK;
+}
+
+int rs_set_devmask_buckets(rs_ctx* c, int enable) {
+  if (!c) return RS_ERR_INVALID_ARG;
+  for (auto& e : c->engines) e->devmask_buckets = enable != 0;
   return RS_OK;
 }
 

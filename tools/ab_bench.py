@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--out-pad", default="0", choices=["0", "1", "both"],
                     help="rs_set_out_pad_writes: out-of-place rows written to the next 128-B line "
                          "(both: each out-of-place workload twice, +outpad)")
+    ap.add_argument("--buckets", default="1", choices=["0", "1", "both"],
+                    help="rs_set_devmask_buckets for device-mask reconstructs without a bound "
+                         "(both: each such workload twice, +nb = one E = m launch)")
     ap.add_argument("--parity-pad", action="store_true",
                     help="rs_set_parity_pad_writes(1): encode writes parity padding to the next 128-B line")
     args = ap.parse_args()
@@ -135,6 +138,12 @@ def main():
         workloads = padded if args.out_pad == "1" else {
             kk: vv for n, w in workloads.items()
             for kk, vv in ([(n, w)] + ([(f"{n}+outpad", w)] if "out" in w[4] else []))}
+    unbounded = ("rec1p_out", "rec2p_out", "rec4p_out", "rec01p_out", "rec45p", "rec2p")
+    if args.buckets != "1":
+        nb_ = {f"{n}+nb": w for n, w in workloads.items() if w[4] in unbounded}
+        workloads = nb_ if args.buckets == "0" else {
+            kk: vv for n, w in workloads.items()
+            for kk, vv in ([(n, w)] + ([(f"{n}+nb", w)] if w[4] in unbounded else []))}
     for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
@@ -142,6 +151,7 @@ def main():
                 engines[(k, m)].set_parity_pad_writes(True)
         eng = engines[(k, m)]
         eng.set_out_pad_writes(name.endswith("+outpad"))
+        eng.set_devmask_buckets(not name.endswith("+nb"))
         t = k + m
         P = shard_pitch_for(S) + pad
         nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))

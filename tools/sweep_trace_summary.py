@@ -3,10 +3,11 @@ and config-3 leg, the HIP-event fraction the bench reported and the rocprof aver
 of the same dispatches in the same process, plus HBM traffic per dispatch from the
 PMC passes (FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024, MI355X_MICROARCH.md §HBM).
 
-A leg's timed window is the reps + 2 dispatches of its kernel that follow an idle gap
+A leg's timed window is the reps + 2 calls of its kernel that follow an idle gap
 of >= 2 ms (bench.py idles 3 ms before each window; kernel_ms_events issues two
 warm-up launches, then the timed ones), the first such after the previous leg's
-window.  The timed ones are the last reps.
+window.  The timed ones are the last reps.  A bucketed device-mask call (round 4)
+is four dispatches -- bucket_kernel and three list kernels -- whose durations add.
 
 Usage: python tools/sweep_trace_summary.py gpurun_out/sweep_<tag> <tag>
 """
@@ -52,25 +53,36 @@ def legs(doc):
 
 
 def windows(trace_csv, want):
-    """Dispatches of each leg's timed window: reps + 2 dispatches of the leg's kernel
-    starting right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each
-    window); the first two are kernel_ms_events' warm-up launches."""
+    """Calls of each leg's timed window: reps + 2 calls of the leg's kernel starting
+    right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each window); the
+    first two are kernel_ms_events' warm-up launches.  A call is one dispatch, or for
+    a bucketed device-mask leg ("bucket_kernel+...": round 4) the pre-pass and its
+    three list kernels.  Returns per leg a list of calls (lists of dispatches)."""
     ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"]]
     ds.sort(key=lambda r: int(r["Start_Timestamp"]))
     res, pos = [], 0
     for label, kern, reps, alg, frac in want:
+        group = 4 if kern.startswith("bucket_kernel+") else 1
+        first = "bucket_kernel" if group == 4 else kern.replace(" ", "")
+        need = (reps + 2) * group
         found = None
-        for i in range(pos, len(ds) - reps - 1):
+        for i in range(pos, len(ds) - need + 1):
             if i > 0 and int(ds[i]["Start_Timestamp"]) - int(ds[i - 1]["End_Timestamp"]) < 2_000_000:
                 continue
-            if short(ds[i]["Kernel_Name"]) != kern.replace(" ", ""):
+            if short(ds[i]["Kernel_Name"]) != first:
                 continue
-            if all(ds[j]["Kernel_Name"] == ds[i]["Kernel_Name"] for j in range(i, i + reps + 2)):
-                found = ds[i + 2:i + reps + 2]
-                pos = i + reps + 2
+            heads = [ds[j]["Kernel_Name"] for j in range(i, i + need, group)]
+            if all(h == ds[i]["Kernel_Name"] for h in heads):
+                calls = [ds[j:j + group] for j in range(i, i + need, group)]
+                found = calls[2:]
+                pos = i + need
                 break
         res.append(found)
     return res
+
+
+def dur(d):
+    return int(d["End_Timestamp"]) - int(d["Start_Timestamp"])
 
 
 def main():
@@ -92,7 +104,8 @@ def main():
                 vals[r["Dispatch_Id"]] = float(r["Counter_Value"])
         for (label, *_), win in zip(legs(pdoc), pw):
             if win:
-                v = [vals[d["Dispatch_Id"]] for d in win if d["Dispatch_Id"] in vals]
+                v = [sum(vals[d["Dispatch_Id"]] for d in call) for call in win
+                     if all(d["Dispatch_Id"] in vals for d in call)]
                 if v:
                     traffic.setdefault(label, {})[counter] = statistics.mean(v)
     lines = [f"# bench.py K/M sweep + config 3 under rocprofv3, same process ({tag})", "",
@@ -106,7 +119,8 @@ def main():
         if not win:
             lines.append(f"| {label} | `{kern}` | (window not found) | {frac:.4f} | | | | |")
             continue
-        avg = statistics.mean(int(d["End_Timestamp"]) - int(d["Start_Timestamp"]) for d in win)
+        # per call: the sum of its dispatches' durations (one dispatch, or a bucketed call's four)
+        avg = statistics.mean(sum(dur(d) for d in call) for call in win)
         rf = alg / avg / HBM_PEAK_GBS
         diff = (frac - rf) * 100
         worst = max(worst, abs(diff))
