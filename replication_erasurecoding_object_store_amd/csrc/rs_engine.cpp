@@ -918,6 +918,77 @@ int launch_bucketed(Engine* e, const rs::KernelArgs& args, hipStream_t s) {
   return RS_OK;
 }
 
+// Per-stripe host masks: the host already scans them (checks, the erasure bound
+// `most`), so when a batch mixes 1-2 erasure stripes with stripes missing 3 or more,
+// it builds the three lists itself -- {stripe, plan} entries in stripe order, in the
+// slot's pinned buffer, uploaded instead of the masks -- and launches only the
+// non-empty lists, each with a grid for its exact length (round 4).  Otherwise one
+// launch sized for `most`, as before.
+int launch_host_masks(Engine* e, const rs::KernelArgs& args, const uint32_t* masks, size_t N, int most,
+                      hipStream_t s) {
+  rs::KernelArgs a = args;
+  apply_pad_writes(e, a);
+  const uint32_t full = a.full_mask;
+  bool mixed = false;
+  if (e->devmask_buckets && e->have_lut && e->m > 2 && most > 2 && rs::bucketed_supported(a))
+    for (size_t i = 0; i < N && !mixed; ++i) mixed = __builtin_popcount(~masks[i] & full) <= 2;
+  if (!mixed) {
+    UploadGuard ug;
+    const uint32_t* dm = nullptr;
+    int rc = upload_acquire(e, masks, N, s, &ug, &dm);
+    if (rc) return rc;
+    rs::KernelArgs b = args;
+    b.present_masks = dm;
+    return launch(e, b, most, true, s);
+  }
+  if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
+  uint32_t cnt[3] = {0, 0, 0};
+  for (size_t i = 0; i < N; ++i) {
+    const int ne = __builtin_popcount(~masks[i] & full);
+    if (ne > 0) ++cnt[ne >= 3 ? 2 : ne - 1];
+  }
+  UploadGuard ug;
+  UploadSlot* u = nullptr;
+  int rc = slot_acquire(e, s, &ug, &u);
+  if (rc) return rc;
+  const size_t bytes = 16 + 8 * N;
+  u->host.numa = e->numa;
+  if (u->host.ensure(bytes) || u->dev.ensure(bytes)) return RS_ERR_DEVICE;
+  uint32_t* hw = static_cast<uint32_t*>(u->host.p);
+  hw[0] = cnt[0];
+  hw[1] = cnt[1];
+  hw[2] = cnt[2];
+  hw[3] = 0;
+  size_t pos[3] = {0, cnt[0], static_cast<size_t>(cnt[0]) + cnt[1]};
+  const size_t first[3] = {pos[0], pos[1], pos[2]};
+  uint32_t* ent = hw + 4;
+  for (size_t i = 0; i < N; ++i) {
+    const uint32_t missing = ~masks[i] & full;
+    const int ne = __builtin_popcount(missing);
+    if (ne == 0) continue;
+    const size_t q = ne >= 3 ? 2 : static_cast<size_t>(ne - 1);
+    ent[2 * pos[q]] = static_cast<uint32_t>(i);
+    ent[2 * pos[q] + 1] = (*e->h_lut)[missing];
+    ++pos[q];
+  }
+  RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, bytes, hipMemcpyHostToDevice, s));
+  const uint32_t* dw = static_cast<const uint32_t*>(u->dev.p);
+  for (int q = 0; q < 3; ++q) {
+    if (!cnt[q]) continue;
+    const int eq = q < 2 ? q + 1 : e->m;
+    rs::KernelArgs ka = a;
+    ka.stripe_list = dw + 4 + 2 * first[q];
+    ka.list_count = dw + q;
+    ka.n_stripes = cnt[q];  // the grid: this list's exact length
+    const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, eq);
+    if (!rs::launch_apply_list(ka, eq, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s))
+      return RS_ERR_DEVICE;
+  }
+  e->shared->note(s, rs::bucketed_name(a));
+  RS_HIP(hipGetLastError());
+  return RS_OK;
+}
+
 int ensure_pipe_stream(Engine* e, int i) {
   if (!e->pipe_st[i]) RS_HIP(hipStreamCreateWithFlags(&e->pipe_st[i], hipStreamNonBlocking));
   return RS_OK;
@@ -955,14 +1026,7 @@ int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(bad_host, a.bad, N * 4, hipMemcpyDeviceToHost, st));
   } else {
-    UploadGuard ug;
-    if (masks_host) {
-      const uint32_t* dm = nullptr;
-      rc = upload_acquire(e, masks_host, N, st, &ug, &dm);
-      if (rc) return rc;
-      a.present_masks = dm;
-    }
-    rc = launch(e, a, e_out, masks_host != nullptr, st);
+    rc = masks_host ? launch_host_masks(e, a, masks_host, N, e_out, st) : launch(e, a, e_out, false, st);
     if (rc) return rc;
   }
   RS_HIP(hipStreamSynchronize(st));
@@ -1188,13 +1252,8 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
     return launch(e, a, most, false, s);
   }
   if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
-  UploadGuard ug;
-  const uint32_t* dm = nullptr;
-  int rc = upload_acquire(e, masks, N, s, &ug, &dm);
-  if (rc) return rc;
   a.plans = static_cast<const uint8_t*>(e->d_plans.p);
-  a.present_masks = dm;
-  return launch(e, a, most, true, s);
+  return launch_host_masks(e, a, masks, N, most, s);
 }
 
 int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan) {
@@ -1489,13 +1548,8 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
       if (rc) return rc;
       return launch(e, a, max_missing, false, s);
     }
-    UploadGuard ug;
-    const uint32_t* dm = nullptr;
-    int rc = upload_acquire(e, masks, N, s, &ug, &dm);
-    if (rc) return rc;
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
-    a.present_masks = dm;
-    return launch(e, a, max_missing, true, s);
+    return launch_host_masks(e, a, masks, N, max_missing, s);
   }
   std::vector<int> in_slots, out_slots;
   if (n_masks == 1) {

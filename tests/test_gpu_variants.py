@@ -249,11 +249,12 @@ def test_out_pad_writes(engines, k, m, S, bound):
         assert (got[i, len(missing):] == 0xC3).all(), ("unused rows", i)
 
 
-# Bucketed device-mask reconstructs (round 4): without a caller bound, a device
+# Bucketed reconstructs (round 4): device masks without a caller bound -- a device
 # pre-pass sorts the stripes into lists by erasure count (1, 2, >= 3) and each list
 # runs on its own kernel (flat list kernels for ragged out-of-place shapes,
-# stripe-aligned list kernels otherwise).  Same bytes and deferred errors as the
-# single E = M launch, over many calls (the ring slots' count banks alternate).
+# stripe-aligned list kernels otherwise); mixed host masks -- the host builds the
+# lists.  Same bytes and deferred errors as the single launch, over many calls (the
+# ring slots' count banks alternate).
 @pytest.mark.parametrize("k,m,S", [(8, 4, 8192), (10, 4, 6554), (6, 3, 10923), (10, 4, 413), (8, 4, 100)])
 def test_bucketed_devmask_matches_single_launch(engines, k, m, S):
     import torch
@@ -287,13 +288,18 @@ def test_bucketed_devmask_matches_single_launch(engines, k, m, S):
                 out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
                 eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
                 res.append(out)
+                # host masks: mixed batches are bucketed on the host
+                out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+                eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
+                res.append(out)
             eng.sync()
             outs[buckets] = [o.cpu().numpy() for o in res]
         finally:
             eng.set_devmask_buckets(True)
-    for it, masks in enumerate(draws):
-        a, b = outs[True][it], outs[False][it]
-        assert np.array_equal(a, b), ("bucketed != single launch", it)
+    for j in range(2 * len(draws)):
+        it, masks = j // 2, draws[j // 2]
+        a, b = outs[True][j], outs[False][j]
+        assert np.array_equal(a, b), ("bucketed != single launch", it, "host" if j % 2 else "device")
         missing = [[j for j in range(t) if not (int(masks[i]) >> j) & 1] for i in range(N)]
         for r in range(m):
             rows = np.array([i for i in range(N) if len(missing[i]) > r])

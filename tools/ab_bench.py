@@ -75,6 +75,12 @@ WORKLOADS = {
     "rs104_64K_encu_out": (10, 4, 6554, 16384, "encu_out"),        # lookup encode (uniform data-only mask)
     "rs84_64K_encu_out": (8, 4, 8192, 16384, "encu_out"),
     "rs84_64K_rec2ph_out": (8, 4, 8192, 16384, "rec2ph_out"),      # per-stripe host masks -> E=2 kernel
+    # mixed erasure counts per stripe (0..m, uniform), no caller bound: device masks
+    # (bucketed on the device) and host masks (bucketed on the host); bytes counted exactly
+    "rs104_64K_recmix_out": (10, 4, 6554, 16384, "recmix_out"),
+    "rs104_64K_recmixh_out": (10, 4, 6554, 16384, "recmixh_out"),
+    "rs84_64K_recmix_out": (8, 4, 8192, 16384, "recmix_out"),
+    "rs84_64K_recmixh_out": (8, 4, 8192, 16384, "recmixh_out"),
 }
 
 
@@ -138,7 +144,7 @@ def main():
         workloads = padded if args.out_pad == "1" else {
             kk: vv for n, w in workloads.items()
             for kk, vv in ([(n, w)] + ([(f"{n}+outpad", w)] if "out" in w[4] else []))}
-    unbounded = ("rec1p_out", "rec2p_out", "rec4p_out", "rec01p_out", "rec45p", "rec2p")
+    unbounded = ("rec1p_out", "rec2p_out", "rec4p_out", "rec01p_out", "rec45p", "rec2p", "recmix_out", "recmixh_out")
     if args.buckets != "1":
         nb_ = {f"{n}+nb": w for n, w in workloads.items() if w[4] in unbounded}
         workloads = nb_ if args.buckets == "0" else {
@@ -172,6 +178,11 @@ def main():
         four = np.array([((1 << t) - 1) & ~sum(1 << int(j) for j in rng.choice(t, size=min(4, m), replace=False))
                          for _ in range(N)], np.uint32)
         masks4 = torch.from_numpy(four.view(np.int32)).cuda()
+        mix = np.full(N, (1 << t) - 1, np.uint32)
+        for i, ne in enumerate(rng.integers(0, m + 1, N)):
+            for j in rng.choice(t, size=int(ne), replace=False):
+                mix[i] &= ~np.uint32(1 << int(j))
+        mixd = torch.from_numpy(mix.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
         md0 = torch.full((N,), ((1 << t) - 1) & ~1, dtype=torch.int32, device="cuda")
@@ -179,6 +190,9 @@ def main():
         rows = bounded_rows[mode] if name.endswith("+dense") else m
         outs = [torch.empty((N, rows, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
         alg = alg_bytes(name.split("+")[0])  # "+<pad>" / "+dense" variants move the same bytes
+        if mode in ("recmix_out", "recmixh_out"):  # K reads + one write per missing shard, complete stripes none
+            nmiss = np.array([bin(int(x) ^ ((1 << t) - 1)).count("1") for x in mix])
+            alg = int(S * (k * np.count_nonzero(nmiss) + nmiss.sum()))
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
         def run(i):
@@ -217,6 +231,10 @@ def main():
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=m01)
             elif mode == "rec2ph_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=masks_np[i % nb])
+            elif mode == "recmix_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=mixd)
+            elif mode == "recmixh_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=mix)
             elif mode == "encu_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=(1 << k) - 1)
             elif mode == "rec2u_out":
