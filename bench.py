@@ -47,6 +47,7 @@ sys.path.insert(0, ROOT)
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: "6.29 TB/s measured (float4 copy, 79%)"
 # Compute-free ceilings of the RS access patterns on MI355X (tools/pattern_probe.hip,
 # profiles/r02_pattern_probe.log): the best the split layout's traffic reaches with no
 # arithmetic at all, fraction of 8 TB/s.
@@ -138,6 +139,40 @@ class RSWorkload:
         d, p = self.bufs[i % self.nb]
         self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks1[i % self.nb],
                                  max_missing=bound)
+
+    def rec_mix(self, i, host=False):
+        """0..m erased shards per stripe (seeded, uniform count), no caller bound: a
+        scan's mix of intact and damaged stripes.  host: the masks come from host
+        memory (rs_reconstruct_batch_out with per-stripe host masks)."""
+        if not hasattr(self, "masks_mix"):
+            rng = np.random.default_rng(0x5EED0003 + 2)
+            t = self.k + self.m
+            self.masks_mix_np = []
+            for _ in range(self.nb):
+                mk = np.full(self.N, (1 << t) - 1, np.uint32)
+                for s, ne in enumerate(rng.integers(0, self.m + 1, self.N)):
+                    for j in rng.choice(t, size=int(ne), replace=False):
+                        mk[s] &= ~np.uint32(1 << int(j))
+                self.masks_mix_np.append(mk)
+            self.masks_mix = [self.torch.from_numpy(mk.view(np.int32)).cuda() for mk in self.masks_mix_np]
+        d, p = self.bufs[i % self.nb]
+        if host:
+            self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N,
+                                     present_masks=self.masks_mix_np[i % self.nb])
+        else:
+            self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks_mix[i % self.nb])
+
+    def mix_alg_bytes(self):
+        """Algorithmic bytes of a mixed batch (mean over the rotation): K survivors read
+        and one shard written per erased shard, for each damaged stripe; intact stripes
+        need nothing."""
+        self.rec_mix(0)
+        t = self.k + self.m
+        per = []
+        for mk in self.masks_mix_np:
+            ne = np.array([t - bin(int(x)).count("1") for x in mk])
+            per.append(self.S * (self.k * np.count_nonzero(ne) + int(ne.sum())))
+        return float(np.mean(per))
 
     def alg_bytes(self):
         return {"encode": self.N * self.S * (self.k + self.m), "reconstruct": self.N * self.S * (self.k + 2),
@@ -300,12 +335,18 @@ def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
     }
 
 
-def copy_peak(torch, eng, nbytes=1 << 30, iters=20):
-    # random bytes, as the RS kernels stream (constant fills measured ~5 % slower)
-    a = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda")
-    b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    ms = kernel_ms_events(torch, lambda i: eng.device_copy(b, a), iters)
-    del a, b
+def copy_peak(torch, eng, nbytes, pairs=6, min_ms=100.0):
+    """The HBM yardstick: rs_device_copy moving the same bytes per launch as the RS
+    launch it is compared with (nbytes read + nbytes written), rotating over `pairs`
+    buffer pairs as the RS batches rotate, random bytes (constant fills measured ~5 %
+    slower), >= min_ms of back-to-back launches.  (Round 3 copied one 1 GiB buffer:
+    6.0 TB/s; the same copy at this footprint reads 6.3-6.4 TB/s,
+    profiles/r04c_copy_probe.log.)"""
+    nbytes = nbytes // 16 * 16
+    bufs = [(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda"),
+             torch.empty(nbytes, dtype=torch.uint8, device="cuda")) for _ in range(pairs)]
+    ms, _ = sustained_kernel_ms(torch, lambda i: eng.device_copy(bufs[i % pairs][1], bufs[i % pairs][0]), min_ms)
+    del bufs
     torch.cuda.empty_cache()
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
@@ -482,8 +523,18 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             timed("reconstruct1_out_pad", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
             e2.set_out_pad_writes(False)
         if mm > 2:
-            timed("reconstruct2_unbounded", w.rec, alg["reconstruct"])
-            timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])
+            # no caller bound: one launch sized for m (rs_set_devmask_buckets(0)) and the
+            # bucketed form (device pre-pass + a list launch per erasure count); the mixed
+            # legs (0..m erasures per stripe, intact stripes included) also with host masks
+            mix = w.mix_alg_bytes()
+            ent["mixed_alg_bytes"] = mix
+            for bk, sfx in ((False, ""), (True, "_bucketed")):
+                e2.set_devmask_buckets(bk)
+                timed("reconstruct2_unbounded" + sfx, w.rec, alg["reconstruct"])
+                timed("reconstruct1_unbounded" + sfx, w.rec1, alg["reconstruct1"])
+                timed("reconstruct_mixed_unbounded" + sfx, w.rec_mix, mix)
+                timed("reconstruct_mixed_host" + sfx, lambda i: w.rec_mix(i, host=True), mix)
+            e2.set_devmask_buckets(True)
         ent["ok"] = rdist.all_true(w.check())
         ent["kernels"] = kern
         w.close()
@@ -755,8 +806,10 @@ def main():
         out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds, torch, eng)
     if not args.no_extras:
         extras = {}
-        cp = rdist.max_over_ranks(-copy_peak(torch, eng))  # slowest rank's copy rate
+        # the copy moves the dominant launch's bytes per launch (slowest rank's rate)
+        cp = rdist.max_over_ranks(-copy_peak(torch, eng, alg[dom] // 2))
         extras["copy_kernel_peak_GBps_per_gpu"] = round(-cp, 1)
+        extras["copy_kernel_bytes_per_launch"] = alg[dom] // 2 * 2
         extras["kmsweep_64KiB_device"] = kmsweep(torch, rdist, rotate)
         extras["healer_mix_config5"] = healer_mix(torch, eng, rdist, k, m, S, 1 << 20)
         if world == 1:
@@ -769,6 +822,8 @@ def main():
             extras["sha256_cold_hash_4KiB"] = sha256_rate(torch, eng)
         copy = extras["copy_kernel_peak_GBps_per_gpu"]
         out["roofline"]["frac_of_measured_copy"] = round(achieved / copy, 4)
+        # MI355X_MICROARCH.md: 6.29 TB/s measured float4 copy (79 % of 8 TB/s)
+        out["roofline"]["frac_of_guide_copy"] = round(achieved / GUIDE_COPY_GBS, 4)
         out["extras"] = extras
     if rank == 0:
         line = json.dumps(out)

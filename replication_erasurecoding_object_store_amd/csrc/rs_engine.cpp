@@ -913,7 +913,7 @@ int launch_bucketed(Engine* e, const rs::KernelArgs& args, hipStream_t s) {
   }
   u->gen ^= 1u;
   u->lists_dirty = false;
-  e->shared->note(s, rs::bucketed_name(a));  // the bucketed launch: bucket_kernel + three list kernels
+  e->shared->note(s, rs::bucketed_name(a, false));  // the bucketed launch: bucket_kernel + three list kernels
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -984,7 +984,7 @@ int launch_host_masks(Engine* e, const rs::KernelArgs& args, const uint32_t* mas
     if (!rs::launch_apply_list(ka, eq, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s))
       return RS_ERR_DEVICE;
   }
-  e->shared->note(s, rs::bucketed_name(a));
+  e->shared->note(s, rs::bucketed_name(a, true));
   RS_HIP(hipGetLastError());
   return RS_OK;
 }
@@ -1782,10 +1782,10 @@ int rs_device_copy(rs_ctx* c, void* dst, const void* src, size_t bytes, void* st
   Engine* e = engine_for_stream(c, as_stream(stream));
   if (!e) return RS_ERR_INVALID_ARG;
   DeviceScope ds(e->device);
-  // 16 workgroups per CU, 4 x 16 B in flight per lane: the best of tools/pattern_probe's
-  // copy sweep (U = 2..16 loads per lane x 1..16 workgroups per CU)
+  // one workgroup per CU, 4 KiB wave tasks: the best of tools/copy_probe.hip's sweep
+  // (task shape x loads in flight x store policy x 1..16 workgroups per CU)
   const uint32_t grid = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count) * 16, (bytes / 16 + 1023) / 1024)));
+      std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(e->cu_count), (bytes + 16383) / 16384)));
   rs::launch_copy(src, dst, bytes, grid, as_stream(stream));
   c->shared.note(as_stream(stream), "copy_kernel");
   RS_HIP(hipGetLastError());

@@ -403,6 +403,9 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         pid = over ? 0u : pid;
       }
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+      // a complete stripe (or one skipped above) needs no loads and no stores (round 4:
+      // a batch mixing intact and damaged stripes no longer reads the intact ones)
+      if (pid == 0u) continue;
     }
     if constexpr (K * ((PER_STRIPE && E > 2) ? 2 : E) * 5 > 48) {
       // Too many table dwords to keep resident in SGPRs across trips: make the plan
@@ -875,6 +878,14 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     return p;
   };
 
+  auto next_task = [&] {  // grid stride in the flat column space
+    c0 += step_c;
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
+    }
+  };
   while (s0 < N) {
     const uint32_t cl = c0 + lane;
     const bool inB = cl >= cstride;
@@ -890,6 +901,10 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     pB = pA + 1u;
     if (straddle) planB = plan_of(s0 + 1u, mB, nB, pB);
     const bool diff = planA != planB;  // wave-uniform: the two stripes' patterns differ
+    if ((nA | nB) == 0u) {  // complete stripes: no loads, no stores (round 4)
+      next_task();
+      continue;
+    }
     const bool lb = live && inB;
     // region bases at stripe `base`; each lane's stripe lies dA / dB stripes past it
     // (plain batches: base s0, dA 0, dB 1)
@@ -984,12 +999,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       else
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
     }
-    c0 += step_c;
-    s0 += step_s;
-    if (c0 >= cstride) {
-      c0 -= cstride;
-      ++s0;
-    }
+    next_task();
   }
   if (bad && lane == 0u) atomicOr(a.status, bad);
 }
@@ -1331,19 +1341,29 @@ __global__ __launch_bounds__(256) void bucket_kernel(const BucketArgs b) {
 
 // ---------------------------------------------------------------------------
 // Streaming copy (bench only): the measured HBM ceiling next to the RS kernels.
-// 4 independent 16-B nt loads per lane in flight, 16 workgroups per CU (the launch
-// in rs_device_copy): 6.0-6.2 TB/s read+write (tools/pattern_probe.hip copy sweep).
-__global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                   uint64_t n16) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256u * 4u;
-  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * 1024u + threadIdx.x; base < n16; base += stride) {
+// Wave-contiguous 4 KiB tasks (4 x 16-B loads per lane, 1 KiB per wave instruction),
+// non-temporal loads, stores NT + device-scope write-through, one workgroup per CU:
+// the fastest of tools/copy_probe.hip's sweep at the RS bench's traffic per launch
+// (402 MB over rotating buffers: 6.41 TB/s read+write, profiles/r04c_copy_probe.log;
+// the round-1..3 block-contiguous form 6.0-6.2).  Each task's descriptor starts at
+// the task and ends with the buffer, so the tail needs no branch and any size works.
+__global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                   uint64_t bytes) {
+  constexpr uint32_t kTask = 4096;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (blockDim.x >> 6);
+  for (uint64_t t = wave_index(); t * kTask < bytes; t += nw) {
+    const uint64_t base = t * kTask;
+    const uint64_t left = bytes - base;
+    const uint32_t nrec = static_cast<uint32_t>(left < kTask ? left : kTask);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src) + base, 0, nrec, 0x00020000);
+    const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + base, 0, nrec, 0x00020000);
     u32x4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (base + u * 256u < n16) v[u] = __builtin_nontemporal_load(src + base + u * 256u);
+    for (int u = 0; u < 4; ++u) v[u] = bload16(rs, lane * 16u + u * 1024u, 0);
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (base + u * 256u < n16) __builtin_nontemporal_store(v[u], dst + base + u * 256u);
+      __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, lane * 16u + u * 1024u, 0, kCpolNt | kCpolSc1);
   }
 }
 
@@ -1552,12 +1572,16 @@ bool bucketed_supported(const KernelArgs& a) {
   return n * a.data_sp + span < lim && n * a.parity_sp + span < lim && n * a.out_sp + span < lim;
 }
 
-const char* bucketed_name(const KernelArgs& a) {
+const char* bucketed_name(const KernelArgs& a, bool host_lists) {
   const bool flat = list_flat(a);
 #define RS_BNAME(KK, MM, EM)                                                                          \
-  if (a.k == KK && a.m == MM)                                                                         \
+  if (a.k == KK && a.m == MM) {                                                                       \
+    if (host_lists)                                                                                   \
+      return flat ? "lists3+apply_flat_ps_kernel<" #KK "," #MM ",1|2|" #EM ",true>"                   \
+                  : "lists3+apply_kernel<" #KK "," #MM ",1|2|" #EM ",true,true>";                     \
     return flat ? "bucket_kernel+apply_flat_ps_kernel<" #KK "," #MM ",1|2|" #EM ",true>"              \
-                : "bucket_kernel+apply_kernel<" #KK "," #MM ",1|2|" #EM ",true,true>";
+                : "bucket_kernel+apply_kernel<" #KK "," #MM ",1|2|" #EM ",true,true>";                \
+  }
   RS_BNAME(8, 4, 4) RS_BNAME(10, 4, 4) RS_BNAME(6, 3, 3)
 #undef RS_BNAME
   return "bucket_kernel+list";
@@ -1634,8 +1658,8 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
 }
 
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(copy_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const u32x4*>(src),
-                     static_cast<u32x4*>(dst), bytes / 16);
+  hipLaunchKernelGGL(copy_kernel, dim3(grid_blocks), dim3(256), 0, s, static_cast<const uint8_t*>(src),
+                     static_cast<uint8_t*>(dst), bytes);
 }
 
 }  // namespace rs

@@ -151,8 +151,9 @@ bool apply_ptrs_supported(int k, int m);  // a specialised pointer-table kernel 
 bool bucketed_supported(const KernelArgs& a);
 bool launch_buckets(const BucketArgs& b, uint32_t cu_count, hipStream_t s);
 const char* launch_apply_list(const KernelArgs& a, int e, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
-// "bucket_kernel+<list kernel>" naming the four launches of one bucketed call.
-const char* bucketed_name(const KernelArgs& a);
+// "bucket_kernel+<list kernels>" naming the four launches of one device-bucketed call;
+// host_lists: "lists3+<list kernels>", the list launches of a host-bucketed call.
+const char* bucketed_name(const KernelArgs& a, bool host_lists);
 // a.bad must be zeroed first (launch_verify does it on s).
 const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
 

@@ -328,3 +328,19 @@ def test_bucketed_devmask_matches_single_launch(engines, k, m, S):
     ok[[3, 700]] = False
     assert np.array_equal(got[ok], ref[ok])
     assert (got[[3, 700]][lost[[3, 700]]] == 0x33).all(), "a skipped stripe must stay untouched"
+
+
+@pytest.mark.parametrize("nbytes", [16, 4080, 4096, 4112, (1 << 20) + 16, 201326592])
+def test_device_copy_exact(engines, nbytes):
+    """rs_device_copy (the bench's HBM yardstick): 4 KiB wave tasks whose descriptors
+    end with the buffer -- every byte copied, nothing past the end written."""
+    import torch
+
+    eng = _engine(engines, 4, 2)
+    g = torch.Generator(device="cuda").manual_seed(nbytes % 1000)
+    src = torch.randint(0, 256, (nbytes + 4096,), dtype=torch.uint8, device="cuda", generator=g)
+    dst = torch.full((nbytes + 4096,), 0x5A, dtype=torch.uint8, device="cuda")
+    eng.device_copy(dst, src, nbytes)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:nbytes], src[:nbytes])
+    assert (dst[nbytes:] == 0x5A).all(), "bytes past the copy written"

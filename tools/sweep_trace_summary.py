@@ -20,7 +20,11 @@ import sys
 HBM_PEAK_GBS = 8000.0
 SHAPES = {"rs42_64KiB": (4, 2, 16384), "rs84_64KiB": (8, 4, 8192), "rs104_64KiB": (10, 4, 6554)}
 E_OF = {"encode": None, "encode_parity_pad": None, "reconstruct2": 2, "reconstruct1": 1,
-        "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1}
+        "reconstruct2_out_pad": 2, "reconstruct1_out_pad": 1,
+        "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1, "reconstruct_mixed_unbounded": "mix",
+        "reconstruct_mixed_host": "mix", "reconstruct2_unbounded_bucketed": 2,
+        "reconstruct1_unbounded_bucketed": 1, "reconstruct_mixed_unbounded_bucketed": "mix",
+        "reconstruct_mixed_host_bucketed": "mix"}
 CONFIG3 = {"rec1_per_stripe_out": 1, "rec_0_1_uniform_out": 2, "rec_0_4_uniform_out": 2,
            "rec_4_5_uniform_out": 2, "soa_encode": 2}
 
@@ -44,7 +48,8 @@ def legs(doc):
             if f"{leg}_launches" not in ent:
                 continue
             e = E_OF[leg] if E_OF[leg] is not None else m
-            out.append((f"{shape} {leg}", ent["kernels"][leg], ent[f"{leg}_launches"], N * S * (k + e),
+            alg = ent["mixed_alg_bytes"] if e == "mix" else N * S * (k + e)
+            out.append((f"{shape} {leg}", ent["kernels"][leg], ent[f"{leg}_launches"], alg,
                         ent[f"{leg}_hbm_frac"]))
     for leg, ent in doc.get("config3_patterns_and_soa_rs42_4KiB", {}).items():
         e = CONFIG3[leg]
@@ -62,8 +67,12 @@ def windows(trace_csv, want):
     ds.sort(key=lambda r: int(r["Start_Timestamp"]))
     res, pos = [], 0
     for label, kern, reps, alg, frac in want:
-        group = 4 if kern.startswith("bucket_kernel+") else 1
-        first = "bucket_kernel" if group == 4 else kern.replace(" ", "")
+        group, first = 1, kern.replace(" ", "")
+        if kern.startswith("bucket_kernel+"):
+            group, first = 4, "bucket_kernel"
+        elif kern.startswith("lists3+"):  # host-built lists: the three list kernels, E = 1 first
+            base = kern.split("+", 1)[1]
+            group, first = 3, base.replace("1|2|" + base.split("1|2|")[1].split(",")[0], "1")
         need = (reps + 2) * group
         found = None
         for i in range(pos, len(ds) - need + 1):
