@@ -523,18 +523,14 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             timed("reconstruct1_out_pad", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
             e2.set_out_pad_writes(False)
         if mm > 2:
-            # no caller bound: one launch sized for m (rs_set_devmask_buckets(0)) and the
-            # bucketed form (device pre-pass + a list launch per erasure count); the mixed
-            # legs (0..m erasures per stripe, intact stripes included) also with host masks
+            # no caller bound (kernel sized for m); the mixed legs: 0..m erasures per
+            # stripe, intact stripes included, device and host masks
             mix = w.mix_alg_bytes()
             ent["mixed_alg_bytes"] = mix
-            for bk, sfx in ((False, ""), (True, "_bucketed")):
-                e2.set_devmask_buckets(bk)
-                timed("reconstruct2_unbounded" + sfx, w.rec, alg["reconstruct"])
-                timed("reconstruct1_unbounded" + sfx, w.rec1, alg["reconstruct1"])
-                timed("reconstruct_mixed_unbounded" + sfx, w.rec_mix, mix)
-                timed("reconstruct_mixed_host" + sfx, lambda i: w.rec_mix(i, host=True), mix)
-            e2.set_devmask_buckets(True)
+            timed("reconstruct2_unbounded", w.rec, alg["reconstruct"])
+            timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])
+            timed("reconstruct_mixed_unbounded", w.rec_mix, mix)
+            timed("reconstruct_mixed_host", lambda i: w.rec_mix(i, host=True), mix)
         ent["ok"] = rdist.all_true(w.check())
         ent["kernels"] = kern
         w.close()

@@ -365,14 +365,6 @@ int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
  * is read over the same range.  Bytes [0, S) are unchanged.  0 (the default): no
  * byte past S of an output row is written. */
 int rs_set_out_pad_writes(rs_ctx *ctx, int enable);
-/* Device-mask reconstructs without a caller bound (rs_reconstruct_batch_devmask,
- * rs_reconstruct_batch_out with device masks, rs_reconstruct_batch_out_devmask with
- * max_missing 0) of RS(8+4), RS(10+4) and RS(6+3): by default a device pre-pass sorts
- * the stripes into lists by erasure count (1, 2, 3 or more missing) and each list
- * runs on the kernel sized for it, with no host sync (four launches on `stream`
- * instead of one).  Same bytes and the same deferred errors either way.  0: one
- * launch sized for m erasures (A/B and tests). */
-int rs_set_devmask_buckets(rs_ctx *ctx, int enable);
 /* RS_MEM_HOST batches whose shards all lie in rs_host_alloc'ed memory, 16-B
  * aligned, run zero-copy by default: the kernel reads the survivors and writes the
  * missing shards across PCIe in place.  0 forces the staged H2D -> kernel -> D2H

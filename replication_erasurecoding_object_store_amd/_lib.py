@@ -93,7 +93,6 @@ SIGNATURES = {
     "rs_set_blocks_per_cu": (_i, [_vp, _i]),
     "rs_set_parity_pad_writes": (_i, [_vp, _i]),
     "rs_set_out_pad_writes": (_i, [_vp, _i]),
-    "rs_set_devmask_buckets": (_i, [_vp, _i]),
     "rs_set_host_zero_copy": (_i, [_vp, _i]),
     "rs_last_host_path": (ctypes.c_char_p, [_vp]),
 }

@@ -252,11 +252,6 @@ class BatchEngine(Service):
         next 128-B line (rsgpu.h)."""
         _check(_lib.lib().rs_set_out_pad_writes(self.ctx, 1 if enable else 0))
 
-    def set_devmask_buckets(self, enable: bool) -> None:
-        """Device-mask reconstructs without a bound: bucketed by erasure count on the
-        device (default) or one launch sized for m (rsgpu.h)."""
-        _check(_lib.lib().rs_set_devmask_buckets(self.ctx, 1 if enable else 0))
-
     def set_parity_pad_writes(self, enable: bool) -> None:
         """Encode may write parity slot padding up to the next 128-B line (rsgpu.h)."""
         _check(_lib.lib().rs_set_parity_pad_writes(self.ctx, 1 if enable else 0))

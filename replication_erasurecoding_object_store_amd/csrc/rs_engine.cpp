@@ -212,12 +212,6 @@ struct Lane {
 struct UploadSlot {
   PinnedBuf host;
   DevBuf dev;
-  // bucketed device-mask launches (launch_bucketed): two banks of 4 count words, then
-  // three lists of {stripe, plan} entries.  The launch on this slot accumulates into
-  // bank `gen` and zeroes the other bank for the slot's next launch.
-  DevBuf lists;
-  uint32_t gen = 0;
-  bool lists_dirty = true;  // both banks need zeroing (new buffer, or a launch failed)
   hipEvent_t done = nullptr;
   bool used = false;
   bool busy = false;
@@ -295,7 +289,6 @@ struct Engine {
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
   bool out_pad = false;                   // out-of-place outputs likewise (rs_set_out_pad_writes)
-  bool devmask_buckets = true;            // E = M device-mask reconstructs: bucketed lists (launch_bucketed)
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -589,19 +582,6 @@ rs::KernelArgs make_args(Engine* e, const Layout& L, size_t S, size_t N) {
 
 // e_out = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
 // #missing for per-stripe patterns).
-// rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
-// the slot (inputs' padding read, the written rows' padding written).
-void apply_pad_writes(const Engine* e, rs::KernelArgs& a) {
-  if ((e->parity_pad && a.data_inputs && !a.out) || (e->out_pad && a.out)) {
-    const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
-    if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
-      a.shard_len = static_cast<uint32_t>(s_eff);
-      a.blocks_per_stripe = static_cast<uint32_t>((round_up(s_eff, 16) / 16 + 63) / 64);
-      a.full_cols = static_cast<uint32_t>(s_eff / 16);
-    }
-  }
-}
-
 int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s) {
   if (args.n_stripes == 0 || args.shard_len == 0 || e_out <= 0) return RS_OK;
   rs::KernelArgs a = args;
@@ -609,7 +589,16 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  apply_pad_writes(e, a);
+  if ((e->parity_pad && a.data_inputs && !a.out) || (e->out_pad && a.out)) {
+    // rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
+    // the slot (inputs' padding read, the written rows' padding written)
+    const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
+    if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
+      a.shard_len = static_cast<uint32_t>(s_eff);
+      a.blocks_per_stripe = static_cast<uint32_t>((round_up(s_eff, 16) / 16 + 63) / 64);
+      a.full_cols = static_cast<uint32_t>(s_eff / 16);
+    }
+  }
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
   const char* name =
       rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
@@ -827,9 +816,8 @@ struct UploadGuard {
   }
 };
 
-// A free slot of the ring whose last reader has finished, held busy by g (its release
-// records the slot's event on s after the kernels the caller launches next).
-int slot_acquire(Engine* e, hipStream_t s, UploadGuard* g, UploadSlot** out) {
+int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
+                   const uint32_t** dev) {
   UploadSlot* u = nullptr;
   {
     std::unique_lock<std::mutex> lk(e->upload_mu);
@@ -851,141 +839,11 @@ int slot_acquire(Engine* e, hipStream_t s, UploadGuard* g, UploadSlot** out) {
   g->s = s;
   if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
-  *out = u;
-  return RS_OK;
-}
-
-int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
-                   const uint32_t** dev) {
-  UploadSlot* u = nullptr;
-  int rc = slot_acquire(e, s, g, &u);
-  if (rc) return rc;
   u->host.numa = e->numa;
   if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
   std::memcpy(u->host.p, masks, n * 4);
   RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
   *dev = static_cast<const uint32_t*>(u->dev.p);
-  return RS_OK;
-}
-
-// Device masks without a caller bound (E = M): a pre-pass sorts the stripes into
-// lists by erasure count on the device, then each list runs on the kernel sized for
-// it -- 1 and 2 missing shards on the bounded E = 1 / 2 kernels (their store policy,
-// registers and occupancy), 3 or more on the E = M kernel -- with no host sync
-// (round 4).  The list kernels read their list's length on the device; an empty
-// list's launch ends at once.  Falls back to one E = M launch when (k, m) has no list
-// kernels or the layout exceeds their 32-bit addressing.
-int launch_bucketed(Engine* e, const rs::KernelArgs& args, hipStream_t s) {
-  rs::KernelArgs a = args;
-  if (a.n_stripes == 0 || a.shard_len == 0) return RS_OK;
-  apply_pad_writes(e, a);
-  if (!e->devmask_buckets || !e->have_lut || e->m <= 2 || !rs::bucketed_supported(a))
-    return launch(e, args, e->m, true, s);
-  if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  const size_t N = a.n_stripes;
-  UploadGuard ug;
-  UploadSlot* u = nullptr;
-  int rc = slot_acquire(e, s, &ug, &u);
-  if (rc) return rc;
-  const size_t lists_off = 64;  // bytes: two banks of 4 count words, padded
-  const void* before = u->lists.p;
-  if (u->lists.ensure(lists_off + 3 * N * 8)) return RS_ERR_DEVICE;
-  if (u->lists.p != before || u->lists_dirty) {
-    RS_HIP(hipMemsetAsync(u->lists.p, 0, lists_off, s));
-    u->gen = 0;
-    u->lists_dirty = false;
-  }
-  uint32_t* words = static_cast<uint32_t*>(u->lists.p);
-  uint32_t* counts = words + 4 * u->gen;
-  uint32_t* lists = words + lists_off / 4;
-  u->lists_dirty = true;  // until every launch below is queued
-  const rs::BucketArgs b{a.present_masks, a.lut, static_cast<uint32_t>(N), a.full_mask, lists, counts,
-                         words + 4 * (u->gen ^ 1u), a.status};
-  if (!rs::launch_buckets(b, static_cast<uint32_t>(e->cu_count), s)) return RS_ERR_DEVICE;
-  for (int q = 0; q < 3; ++q) {
-    const int eq = q < 2 ? q + 1 : e->m;
-    rs::KernelArgs ka = a;
-    ka.stripe_list = lists + static_cast<size_t>(2 * q) * N;
-    ka.list_count = counts + q;
-    const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, eq);
-    if (!rs::launch_apply_list(ka, eq, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s))
-      return RS_ERR_DEVICE;
-  }
-  u->gen ^= 1u;
-  u->lists_dirty = false;
-  e->shared->note(s, rs::bucketed_name(a, false));  // the bucketed launch: bucket_kernel + three list kernels
-  RS_HIP(hipGetLastError());
-  return RS_OK;
-}
-
-// Per-stripe host masks: the host already scans them (checks, the erasure bound
-// `most`), so when a batch mixes 1-2 erasure stripes with stripes missing 3 or more,
-// it builds the three lists itself -- {stripe, plan} entries in stripe order, in the
-// slot's pinned buffer, uploaded instead of the masks -- and launches only the
-// non-empty lists, each with a grid for its exact length (round 4).  Otherwise one
-// launch sized for `most`, as before.
-int launch_host_masks(Engine* e, const rs::KernelArgs& args, const uint32_t* masks, size_t N, int most,
-                      hipStream_t s) {
-  rs::KernelArgs a = args;
-  apply_pad_writes(e, a);
-  const uint32_t full = a.full_mask;
-  bool mixed = false;
-  if (e->devmask_buckets && e->have_lut && e->m > 2 && most > 2 && rs::bucketed_supported(a))
-    for (size_t i = 0; i < N && !mixed; ++i) mixed = __builtin_popcount(~masks[i] & full) <= 2;
-  if (!mixed) {
-    UploadGuard ug;
-    const uint32_t* dm = nullptr;
-    int rc = upload_acquire(e, masks, N, s, &ug, &dm);
-    if (rc) return rc;
-    rs::KernelArgs b = args;
-    b.present_masks = dm;
-    return launch(e, b, most, true, s);
-  }
-  if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  uint32_t cnt[3] = {0, 0, 0};
-  for (size_t i = 0; i < N; ++i) {
-    const int ne = __builtin_popcount(~masks[i] & full);
-    if (ne > 0) ++cnt[ne >= 3 ? 2 : ne - 1];
-  }
-  UploadGuard ug;
-  UploadSlot* u = nullptr;
-  int rc = slot_acquire(e, s, &ug, &u);
-  if (rc) return rc;
-  const size_t bytes = 16 + 8 * N;
-  u->host.numa = e->numa;
-  if (u->host.ensure(bytes) || u->dev.ensure(bytes)) return RS_ERR_DEVICE;
-  uint32_t* hw = static_cast<uint32_t*>(u->host.p);
-  hw[0] = cnt[0];
-  hw[1] = cnt[1];
-  hw[2] = cnt[2];
-  hw[3] = 0;
-  size_t pos[3] = {0, cnt[0], static_cast<size_t>(cnt[0]) + cnt[1]};
-  const size_t first[3] = {pos[0], pos[1], pos[2]};
-  uint32_t* ent = hw + 4;
-  for (size_t i = 0; i < N; ++i) {
-    const uint32_t missing = ~masks[i] & full;
-    const int ne = __builtin_popcount(missing);
-    if (ne == 0) continue;
-    const size_t q = ne >= 3 ? 2 : static_cast<size_t>(ne - 1);
-    ent[2 * pos[q]] = static_cast<uint32_t>(i);
-    ent[2 * pos[q] + 1] = (*e->h_lut)[missing];
-    ++pos[q];
-  }
-  RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, bytes, hipMemcpyHostToDevice, s));
-  const uint32_t* dw = static_cast<const uint32_t*>(u->dev.p);
-  for (int q = 0; q < 3; ++q) {
-    if (!cnt[q]) continue;
-    const int eq = q < 2 ? q + 1 : e->m;
-    rs::KernelArgs ka = a;
-    ka.stripe_list = dw + 4 + 2 * first[q];
-    ka.list_count = dw + q;
-    ka.n_stripes = cnt[q];  // the grid: this list's exact length
-    const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, eq);
-    if (!rs::launch_apply_list(ka, eq, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s))
-      return RS_ERR_DEVICE;
-  }
-  e->shared->note(s, rs::bucketed_name(a, true));
-  RS_HIP(hipGetLastError());
   return RS_OK;
 }
 
@@ -1026,7 +884,14 @@ int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_
     if (rc) return rc;
     RS_HIP(hipMemcpyAsync(bad_host, a.bad, N * 4, hipMemcpyDeviceToHost, st));
   } else {
-    rc = masks_host ? launch_host_masks(e, a, masks_host, N, e_out, st) : launch(e, a, e_out, false, st);
+    UploadGuard ug;
+    if (masks_host) {
+      const uint32_t* dm = nullptr;
+      rc = upload_acquire(e, masks_host, N, st, &ug, &dm);
+      if (rc) return rc;
+      a.present_masks = dm;
+    }
+    rc = launch(e, a, e_out, masks_host != nullptr, st);
     if (rc) return rc;
   }
   RS_HIP(hipStreamSynchronize(st));
@@ -1231,9 +1096,7 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
     if (!out_layout_ok(out_sp, pitch, S, N, bound)) return RS_ERR_INVALID_ARG;
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
     a.present_masks = masks;
-    // no caller bound: bucketed by erasure count (the coalescer always passes its
-    // batch's bound, so its small mixed batches keep one launch)
-    return max_missing == 0 ? launch_bucketed(e, a, s) : launch(e, a, bound, true, s);
+    return launch(e, a, bound, true, s);
   }
   if (n_masks != 1 && n_masks != N) return RS_ERR_INVALID_ARG;
   int most = 0;
@@ -1252,8 +1115,13 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
     return launch(e, a, most, false, s);
   }
   if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
+  UploadGuard ug;
+  const uint32_t* dm = nullptr;
+  int rc = upload_acquire(e, masks, N, s, &ug, &dm);
+  if (rc) return rc;
   a.plans = static_cast<const uint8_t*>(e->d_plans.p);
-  return launch_host_masks(e, a, masks, N, most, s);
+  a.present_masks = dm;
+  return launch(e, a, most, true, s);
 }
 
 int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan) {
@@ -1548,8 +1416,13 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
       if (rc) return rc;
       return launch(e, a, max_missing, false, s);
     }
+    UploadGuard ug;
+    const uint32_t* dm = nullptr;
+    int rc = upload_acquire(e, masks, N, s, &ug, &dm);
+    if (rc) return rc;
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
-    return launch_host_masks(e, a, masks, N, max_missing, s);
+    a.present_masks = dm;
+    return launch(e, a, max_missing, true, s);
   }
   std::vector<int> in_slots, out_slots;
   if (n_masks == 1) {
@@ -1644,7 +1517,7 @@ int rs_reconstruct_batch_devmask(rs_ctx* c, uint8_t* data, size_t data_sp, uint8
   rs::KernelArgs a = make_args(e, L, S, N);
   a.plans = static_cast<const uint8_t*>(e->d_plans.p);
   a.present_masks = masks_dev;
-  return launch_bucketed(e, a, as_stream(stream));
+  return launch(e, a, c->m, true, as_stream(stream));
 }
 
 // Waits for stream s; returns and clears its deferred per-stripe errors (bit 0: a
@@ -1841,12 +1714,6 @@ int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
 int rs_set_out_pad_writes(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->out_pad = enable != 0;
-  return RS_OK;
-}
-
-int rs_set_devmask_buckets(rs_ctx* c, int enable) {
-  if (!c) return RS_ERR_INVALID_ARG;
-  for (auto& e : c->engines) e->devmask_buckets = enable != 0;
   return RS_OK;
 }
 

@@ -337,32 +337,21 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // Every trip issues the same loads and stores (dropped when not live); the
 // wave-uniform branches hold VALU work only, so the compiler's vmcnt bookkeeping
 // stays exact across them.
-//
-// LIST (bucketed device-mask launches, round 4): the launch computes only the stripes
-// of a device list of {stripe, plan index} entries that bucket_kernel filled with the
-// stripes of one erasure count (its length is a device word), so an E = 1 / 2 launch
-// needs no bound check and no LUT lookup, and the E = M launch sees only stripes
-// missing 3 or more shards.
-template <int K, int M, int E, bool PER_STRIPE, bool LIST = false>
+template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
   const uint32_t bps = a.blocks_per_stripe;   // the partial last column included
-  const uint32_t n_str = LIST ? wave_uniform(*as_const<uint32_t>(a.list_count)) : a.n_stripes;
-  const uint32_t ntasks = n_str * bps;  // host guarantees < 2^32
+  const uint32_t ntasks = a.n_stripes * bps;  // host guarantees < 2^32
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;      // bytes of a partial last column (0: none)
   uint32_t bad = 0u;
 
-  // mask (LIST: list entry) of task t's stripe; every lane loads the same words
+  // mask of task t's stripe; every lane loads the same word (one request)
   auto load_mask = [&](uint32_t t) -> uint32_t {
     const uint32_t tt = t < ntasks ? t : ntasks - 1u;
     return a.present_masks[tt / bps];
-  };
-  auto load_entry = [&](uint32_t t) -> uint2 {
-    const uint32_t tt = t < ntasks ? t : ntasks - 1u;
-    return as_const<uint2>(a.stripe_list)[tt / bps];
   };
 
   // uniform plan: slots once per launch
@@ -378,19 +367,12 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   }
 
   uint32_t mask = 0u;
-  uint2 ent = make_uint2(0u, 0u);
-  if (PER_STRIPE && !LIST && wave < ntasks) mask = load_mask(wave);
-  if (LIST && wave < ntasks) ent = load_entry(wave);
+  if (PER_STRIPE && wave < ntasks) mask = load_mask(wave);
   for (uint32_t t = wave; t < ntasks; t += nwaves) {
-    uint32_t stripe = t / bps;
+    const uint32_t stripe = t / bps;
     const uint32_t blk = t - stripe * bps;
     const uint8_t* plan = a.plans;
-    if constexpr (LIST) {
-      stripe = __builtin_amdgcn_readfirstlane(ent.x);  // waits for this entry only
-      const uint32_t pid = __builtin_amdgcn_readfirstlane(ent.y);
-      ent = load_entry(t + nwaves);                      // next task's entry in flight
-      plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
-    } else if (PER_STRIPE) {
+    if (PER_STRIPE) {
       const uint32_t present = __builtin_amdgcn_readfirstlane(mask);  // waits for this mask only
       mask = load_mask(t + nwaves);                                  // next task's mask in flight
       const uint32_t missing = (~present) & a.full_mask;
@@ -403,9 +385,6 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         pid = over ? 0u : pid;
       }
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
-      // a complete stripe (or one skipped above) needs no loads and no stores (round 4:
-      // a batch mixing intact and damaged stripes no longer reads the intact ones)
-      if (pid == 0u) continue;
     }
     if constexpr (K * ((PER_STRIPE && E > 2) ? 2 : E) * 5 > 48) {
       // Too many table dwords to keep resident in SGPRs across trips: make the plan
@@ -823,17 +802,12 @@ __device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* pl
   }
 }
 
-// LIST (round 4): the flat column space runs over the entries of a bucket list (see
-// apply_kernel), so a task straddles list entries j and j+1 -- any two stripes of the
-// batch.  Each region's descriptor then starts at the lower of the two stripes and
-// the lanes of each stripe add their own stripe distance (host: every region of the
-// batch spans < 2 GiB).
-template <int K, int M, int E, bool LIST = false>
+template <int K, int M, int E>
 __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t N = LIST ? wave_uniform(*as_const<uint32_t>(a.list_count)) : a.n_stripes;
+  const uint32_t N = a.n_stripes;
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
   const uint32_t cstride = (cols + 7u) & ~7u;
@@ -848,20 +822,8 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
   const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
   uint32_t bad = 0u;
 
-  // stripe s's present mask (an invalid one reads slots 0..K-1) and plan; LIST: of
-  // list entry s, whose stripe goes to phys (the plan's header holds its present mask)
-  auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout, uint32_t& phys) -> const uint8_t* {
-    if constexpr (LIST) {
-      const uint2 ent = as_const<uint2>(a.stripe_list)[s];
-      phys = __builtin_amdgcn_readfirstlane(ent.x);
-      const uint8_t* p = uniform_ptr(a.plans + static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(ent.y)) *
-                                                   a.plan_bytes);
-      const PlanView pv(p, K, M);
-      m = pv.present();
-      nout = pv.n_out();
-      return p;
-    }
-    phys = s;
+  // stripe s's present mask (an invalid one reads slots 0..K-1) and plan
+  auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
     const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
     uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
     bad |= (pid == kPlanInvalid) ? 1u : 0u;
@@ -893,29 +855,23 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
     const bool live = !inB || straddle;                         // past the batch end: dead
     const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
-    uint32_t mA, nA, mB, nB, pA, pB;
-    const uint8_t* planA = plan_of(s0, mA, nA, pA);
+    uint32_t mA, nA, mB, nB;
+    const uint8_t* planA = plan_of(s0, mA, nA);
     const uint8_t* planB = planA;
     mB = mA;
     nB = nA;
-    pB = pA + 1u;
-    if (straddle) planB = plan_of(s0 + 1u, mB, nB, pB);
+    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
     const bool diff = planA != planB;  // wave-uniform: the two stripes' patterns differ
-    if ((nA | nB) == 0u) {  // complete stripes: no loads, no stores (round 4)
+    if ((nA | nB) == 0u) {  // complete (or skipped) stripes: no loads, no stores (round 4)
       next_task();
       continue;
     }
     const bool lb = live && inB;
-    // region bases at stripe `base`; each lane's stripe lies dA / dB stripes past it
-    // (plain batches: base s0, dA 0, dB 1)
-    const uint32_t base = LIST ? (pA < pB ? pA : pB) : s0;
-    const uint32_t dA = pA - base, dB = pB - base;  // wave-uniform
-    const uint32_t dsp = static_cast<uint32_t>(a.data_sp), psp = static_cast<uint32_t>(a.parity_sp);
-    const uint32_t offD = (lb ? dB * dsp : dA * dsp) + col * 16u;
-    const uint32_t offP = (lb ? dB * psp : dA * psp) + col * 16u;
-    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(base) * a.data_sp, 0,
+    const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
+    const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
                                                        0x7FFFFFFF, 0x00020000);
-    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(base) * a.parity_sp, 0,
+    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
                                                        0x7FFFFFFF, 0x00020000);
     u32x4 x[K];
     uint32_t bitsA = mA, bitsB = mB;
@@ -940,10 +896,9 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     }
     const uint32_t nmax = nA > nB ? nA : nB;
     // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
-    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(base) * a.out_sp, 0,
+    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
                                                         0x7FFFFFFF, 0x00020000);
-    const uint32_t osp = static_cast<uint32_t>(a.out_sp);
-    const uint32_t offO = (lb ? dB * osp : dA * osp) + col * 16u;
+    const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
     const uint32_t nl = inB ? nB : nA;
     const bool fullc = live && colr < a.full_cols;
     const bool part = nb != 0u && live && colr == a.full_cols;
@@ -1301,45 +1256,6 @@ __global__ __launch_bounds__(256) void verify_kernel_generic(const KernelArgs a)
 }
 
 // ---------------------------------------------------------------------------
-// Bucketing pre-pass (round 4): one lane per stripe reads its mask, looks its plan up
-// and appends {stripe, plan} to the list of its erasure count (1, 2, >= 3) -- one
-// atomic per wave and list for the wave's slots, then a rank within the wave.  The
-// order of a list follows the order in which waves reach the atomics (not sorted;
-// the list kernels address any two stripes of the batch).
-__global__ __launch_bounds__(256) void bucket_kernel(const BucketArgs b) {
-  const uint32_t lane = threadIdx.x & 63u;
-  if (blockIdx.x == 0 && threadIdx.x < 3u) b.counts_next[threadIdx.x] = 0u;
-  uint32_t bad = 0u;
-  const uint32_t step = gridDim.x * 256u;
-  for (uint32_t i0 = blockIdx.x * 256u + (threadIdx.x & ~63u); i0 < b.n; i0 += step) {  // wave-uniform
-    const uint32_t i = i0 + lane;
-    int q = -1;
-    uint32_t pid = 0u;
-    if (i < b.n) {
-      const uint32_t missing = ~b.masks[i] & b.full_mask;
-      pid = b.lut[missing];
-      const uint32_t ne = static_cast<uint32_t>(__builtin_popcount(missing));
-      if (pid == kPlanInvalid)
-        bad = 1u;
-      else if (ne > 0u)
-        q = ne >= 3u ? 2 : static_cast<int>(ne) - 1;
-    }
-#pragma unroll
-    for (int l = 0; l < 3; ++l) {
-      const uint64_t bal = __builtin_amdgcn_ballot_w64(q == l);
-      if (bal == 0u) continue;  // wave-uniform
-      uint32_t base = 0u;
-      if (lane == 0u) base = atomicAdd(b.counts + l, static_cast<uint32_t>(__builtin_popcountll(bal)));
-      base = __builtin_amdgcn_readfirstlane(base);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
-      if (q == l) reinterpret_cast<uint2*>(b.lists)[static_cast<uint64_t>(l) * b.n + base + rank] = make_uint2(i, pid);
-    }
-  }
-  if (__builtin_amdgcn_ballot_w64(bad != 0u) != 0u && lane == 0u) atomicOr(b.status, 1u);
-}
-
-// ---------------------------------------------------------------------------
 // Streaming copy (bench only): the measured HBM ceiling next to the RS kernels.
 // Wave-contiguous 4 KiB tasks (4 x 16-B loads per lane, 1 KiB per wave instruction),
 // non-temporal loads, stores NT + device-scope write-through, one workgroup per CU:
@@ -1539,84 +1455,6 @@ const char* launch_apply_ptrs(const KernelArgs& a, int e_bound, uint32_t blocks_
   const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
   if (waves == 0) return name;
   if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess) return nullptr;
-  return name;
-}
-
-bool launch_buckets(const BucketArgs& b, uint32_t cu_count, hipStream_t s) {
-  const uint64_t need = (static_cast<uint64_t>(b.n) + 255u) / 256u;
-  const uint64_t cap = static_cast<uint64_t>(cu_count) * 4u;
-  const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
-  void* args[] = {const_cast<BucketArgs*>(&b)};
-  return hipLaunchKernel(reinterpret_cast<const void*>(&bucket_kernel), dim3(grid > 0 ? grid : 1), dim3(256), args,
-                         0, s) == hipSuccess;
-}
-
-// List kernels exist for the shapes whose E = M per-stripe kernel the bucketing
-// replaces (m > 2): (8, 4), (10, 4), (6, 3).
-static bool list_shape(int k, int m) { return (k == 8 && m == 4) || (k == 10 && m == 4) || (k == 6 && m == 3); }
-
-static bool list_flat(const KernelArgs& a) {
-  const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
-  return a.out && cols >= 64u && cols % 64u != 0u;
-}
-
-bool bucketed_supported(const KernelArgs& a) {
-  if (!list_shape(a.k, a.m) || a.stripe_plans || a.shard_ptrs || a.shard_len > kColumnWindow) return false;
-  // 32-bit stripe distances: every region (the whole batch) spans < 2 GiB past its
-  // base, with a task's widest reach (a column span and the last slot) added
-  const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
-  const uint64_t span = cols * 16u + static_cast<uint64_t>(a.k > a.m ? a.k : a.m) * a.shard_pitch;
-  const uint64_t n = a.n_stripes;
-  const uint64_t lim = 1ull << 31;
-  if (!list_flat(a)) return true;  // stripe-aligned tasks: 64-bit slot addresses, any layout
-  return n * a.data_sp + span < lim && n * a.parity_sp + span < lim && n * a.out_sp + span < lim;
-}
-
-const char* bucketed_name(const KernelArgs& a, bool host_lists) {
-  const bool flat = list_flat(a);
-#define RS_BNAME(KK, MM, EM)                                                                          \
-  if (a.k == KK && a.m == MM) {                                                                       \
-    if (host_lists)                                                                                   \
-      return flat ? "lists3+apply_flat_ps_kernel<" #KK "," #MM ",1|2|" #EM ",true>"                   \
-                  : "lists3+apply_kernel<" #KK "," #MM ",1|2|" #EM ",true,true>";                     \
-    return flat ? "bucket_kernel+apply_flat_ps_kernel<" #KK "," #MM ",1|2|" #EM ",true>"              \
-                : "bucket_kernel+apply_kernel<" #KK "," #MM ",1|2|" #EM ",true,true>";                \
-  }
-  RS_BNAME(8, 4, 4) RS_BNAME(10, 4, 4) RS_BNAME(6, 3, 3)
-#undef RS_BNAME
-  return "bucket_kernel+list";
-}
-
-const char* launch_apply_list(const KernelArgs& args, int e, uint32_t blocks_per_cu, uint32_t cu_count,
-                              hipStream_t s) {
-  KernelArgs a = args;
-  a.max_out = static_cast<uint32_t>(e);
-  const bool flat = list_flat(a);
-  const char* name = nullptr;
-  const void* fn = nullptr;
-#define RS_LIST(KK, MM, EE)                                                              \
-  if (!fn && a.k == KK && a.m == MM && e == EE) {                                        \
-    if (flat) {                                                                          \
-      name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ",true>";                       \
-      fn = reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE, true>);      \
-    } else {                                                                             \
-      name = "apply_kernel<" #KK "," #MM "," #EE ",true,true>";                          \
-      fn = reinterpret_cast<const void*>(&apply_kernel<KK, MM, EE, true, true>);        \
-    }                                                                                    \
-  }
-  RS_LIST(8, 4, 1) RS_LIST(8, 4, 2) RS_LIST(8, 4, 4)
-  RS_LIST(10, 4, 1) RS_LIST(10, 4, 2) RS_LIST(10, 4, 4)
-  RS_LIST(6, 3, 1) RS_LIST(6, 3, 2) RS_LIST(6, 3, 3)
-#undef RS_LIST
-  if (!fn) return nullptr;
-  const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
-  // the grid of the whole batch: the list's length is only known on the device
-  const uint64_t waves = flat ? (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u
-                              : static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
-  if (waves == 0) return name;
-  void* kargs[] = {&a};
-  if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), kargs, 0, s) != hipSuccess)
-    return nullptr;
   return name;
 }
 

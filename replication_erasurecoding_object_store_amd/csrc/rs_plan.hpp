@@ -102,24 +102,6 @@ struct KernelArgs {
   const uint64_t* shard_ptrs;      // pointer-table launches: stripe i's shard s at device address
                                    //   shard_ptrs[i*(k+m) + s] (inputs: present shards; outputs:
                                    //   the missing shards' buffers), each S bytes, 16-B aligned
-  const uint32_t* stripe_list;     // bucketed launches: entries {stripe, plan index} (2 words each)
-  const uint32_t* list_count;      //   of the stripes to compute; entry count (device word)
-};
-
-// Bucketing pre-pass of a device-mask reconstruct without a caller bound (round 4):
-// the batch's stripes split by erasure count into three lists of {stripe, plan
-// index} entries -- 1, 2, and 3 or more missing shards -- so each list runs on the
-// kernel sized for its count.  Complete stripes go nowhere (nothing to write);
-// stripes with fewer than k present set status bit 0 and go nowhere.
-struct BucketArgs {
-  const uint32_t* masks;   // n present masks (device)
-  const uint32_t* lut;     // missing mask -> plan index
-  uint32_t n;
-  uint32_t full_mask;
-  uint32_t* lists;         // list q (q = 0, 1, 2) at lists + 2*q*n
-  uint32_t* counts;        // 3 list lengths, zero on entry
-  uint32_t* counts_next;   // 3 words zeroed for the next launch that uses this buffer
-  uint32_t* status;
 };
 
 // Parity rows the generated bitsliced encode program of (k, m) was derived from
@@ -143,17 +125,6 @@ void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_block
 // shard's byte S-1, stores never past byte S-1.  e = the launch's erasure bound.
 const char* launch_apply_ptrs(const KernelArgs& a, int e, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
 bool apply_ptrs_supported(int k, int m);  // a specialised pointer-table kernel exists
-// Bucketed device-mask reconstruct: launch_buckets fills the lists, launch_apply_list
-// runs one list (a.stripe_list / a.list_count) with the kernel for e = 1, 2 or m
-// erasures.  a.n_stripes is the batch's stripe count (an upper bound of the list's
-// length: the grid).  bucketed_supported: (k, m) has the list kernels and the batch's
-// layout their 32-bit addressing (every region < 2 GiB, shard_len <= one window).
-bool bucketed_supported(const KernelArgs& a);
-bool launch_buckets(const BucketArgs& b, uint32_t cu_count, hipStream_t s);
-const char* launch_apply_list(const KernelArgs& a, int e, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
-// "bucket_kernel+<list kernels>" naming the four launches of one device-bucketed call;
-// host_lists: "lists3+<list kernels>", the list launches of a host-bucketed call.
-const char* bucketed_name(const KernelArgs& a, bool host_lists);
 // a.bad must be zeroed first (launch_verify does it on s).
 const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t cu_count, hipStream_t s);
 

@@ -249,87 +249,6 @@ def test_out_pad_writes(engines, k, m, S, bound):
         assert (got[i, len(missing):] == 0xC3).all(), ("unused rows", i)
 
 
-# Bucketed reconstructs (round 4): device masks without a caller bound -- a device
-# pre-pass sorts the stripes into lists by erasure count (1, 2, >= 3) and each list
-# runs on its own kernel (flat list kernels for ragged out-of-place shapes,
-# stripe-aligned list kernels otherwise); mixed host masks -- the host builds the
-# lists.  Same bytes and deferred errors as the single launch, over many calls (the
-# ring slots' count banks alternate).
-@pytest.mark.parametrize("k,m,S", [(8, 4, 8192), (10, 4, 6554), (6, 3, 10923), (10, 4, 413), (8, 4, 100)])
-def test_bucketed_devmask_matches_single_launch(engines, k, m, S):
-    import torch
-
-    eng = _engine(engines, k, m)
-    t, N, P = k + m, 1537, shard_pitch_for(S)
-    g = torch.Generator(device="cuda").manual_seed(S * 3 + k)
-    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
-    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
-    eng.encode(data, parity, S, N)
-    ref = torch.cat([data, parity], dim=1)[:, :, :S].cpu().numpy()
-    full = (1 << t) - 1
-    draws = []
-    rng = np.random.default_rng(S + 17 * k)
-    for it in range(12):
-        if it == 0:
-            masks = np.full(N, full, np.uint32)           # nothing missing: every list empty
-        elif it == 1:
-            masks = _masks(rng, N, t, 1, 1)               # only the E = 1 list
-        elif it == 2:
-            masks = _masks(rng, N, t, m, m)               # only the E = m list
-        else:
-            masks = _masks(rng, N, t, 0, m)
-        draws.append(masks)
-    outs = {}
-    for buckets in (True, False):
-        eng.set_devmask_buckets(buckets)
-        try:
-            res = []
-            for masks in draws:  # back to back: more calls than the 8 ring slots
-                out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
-                eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
-                res.append(out)
-                # host masks: mixed batches are bucketed on the host
-                out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
-                eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
-                res.append(out)
-            eng.sync()
-            outs[buckets] = [o.cpu().numpy() for o in res]
-        finally:
-            eng.set_devmask_buckets(True)
-    for j in range(2 * len(draws)):
-        it, masks = j // 2, draws[j // 2]
-        a, b = outs[True][j], outs[False][j]
-        assert np.array_equal(a, b), ("bucketed != single launch", it, "host" if j % 2 else "device")
-        missing = [[j for j in range(t) if not (int(masks[i]) >> j) & 1] for i in range(N)]
-        for r in range(m):
-            rows = np.array([i for i in range(N) if len(missing[i]) > r])
-            if len(rows):
-                src = np.array([missing[i][r] for i in rows])
-                bad = np.nonzero((a[rows, r, :S] != ref[rows, src]).any(axis=1))[0]
-                assert len(bad) == 0, (it, r, rows[bad][:8].tolist())
-            unused = np.array([i for i in range(N) if len(missing[i]) <= r])
-            if len(unused):
-                assert (a[unused, r] == 0xC3).all(), (it, r)
-        assert (a[:, :, S:] == 0xC3).all()
-    # in place (rs_reconstruct_batch_devmask) and a stripe with < k present: skipped,
-    # TOO_FEW_SHARDS from rs_sync, every other stripe rebuilt
-    masks = _masks(rng, N, t, 0, m)
-    masks[[3, 700]] = (1 << (k - 1)) - 1
-    lost = ((masks[:, None] >> np.arange(t)[None, :]) & 1) == 0
-    d2, p2 = data.clone(), parity.clone()
-    d2[:, :, :S][torch.from_numpy(lost[:, :k]).cuda()] = 0x33
-    p2[:, :, :S][torch.from_numpy(lost[:, k:]).cuda()] = 0x33
-    eng.reconstruct_devmask(d2, p2, S, N, torch.from_numpy(masks.view(np.int32)).cuda())
-    with pytest.raises(ECError) as ei:
-        eng.sync()
-    assert ei.value.code == _lib.RS_ERR_TOO_FEW_SHARDS
-    got = torch.cat([d2, p2], dim=1)[:, :, :S].cpu().numpy()
-    ok = np.ones(N, bool)
-    ok[[3, 700]] = False
-    assert np.array_equal(got[ok], ref[ok])
-    assert (got[[3, 700]][lost[[3, 700]]] == 0x33).all(), "a skipped stripe must stay untouched"
-
-
 @pytest.mark.parametrize("nbytes", [16, 4080, 4096, 4112, (1 << 20) + 16, 201326592])
 def test_device_copy_exact(engines, nbytes):
     """rs_device_copy (the bench's HBM yardstick): 4 KiB wave tasks whose descriptors

@@ -75,8 +75,8 @@ WORKLOADS = {
     "rs104_64K_encu_out": (10, 4, 6554, 16384, "encu_out"),        # lookup encode (uniform data-only mask)
     "rs84_64K_encu_out": (8, 4, 8192, 16384, "encu_out"),
     "rs84_64K_rec2ph_out": (8, 4, 8192, 16384, "rec2ph_out"),      # per-stripe host masks -> E=2 kernel
-    # mixed erasure counts per stripe (0..m, uniform), no caller bound: device masks
-    # (bucketed on the device) and host masks (bucketed on the host); bytes counted exactly
+    # mixed erasure counts per stripe (0..m, uniform), no caller bound: device masks and
+    # host masks; bytes counted exactly (intact stripes need none)
     "rs104_64K_recmix_out": (10, 4, 6554, 16384, "recmix_out"),
     "rs104_64K_recmixh_out": (10, 4, 6554, 16384, "recmixh_out"),
     "rs84_64K_recmix_out": (8, 4, 8192, 16384, "recmix_out"),
@@ -108,9 +108,6 @@ def main():
     ap.add_argument("--out-pad", default="0", choices=["0", "1", "both"],
                     help="rs_set_out_pad_writes: out-of-place rows written to the next 128-B line "
                          "(both: each out-of-place workload twice, +outpad)")
-    ap.add_argument("--buckets", default="1", choices=["0", "1", "both"],
-                    help="rs_set_devmask_buckets for device-mask reconstructs without a bound "
-                         "(both: each such workload twice, +nb = one E = m launch)")
     ap.add_argument("--parity-pad", action="store_true",
                     help="rs_set_parity_pad_writes(1): encode writes parity padding to the next 128-B line")
     args = ap.parse_args()
@@ -144,12 +141,6 @@ def main():
         workloads = padded if args.out_pad == "1" else {
             kk: vv for n, w in workloads.items()
             for kk, vv in ([(n, w)] + ([(f"{n}+outpad", w)] if "out" in w[4] else []))}
-    unbounded = ("rec1p_out", "rec2p_out", "rec4p_out", "rec01p_out", "rec45p", "rec2p", "recmix_out", "recmixh_out")
-    if args.buckets != "1":
-        nb_ = {f"{n}+nb": w for n, w in workloads.items() if w[4] in unbounded}
-        workloads = nb_ if args.buckets == "0" else {
-            kk: vv for n, w in workloads.items()
-            for kk, vv in ([(n, w)] + ([(f"{n}+nb", w)] if w[4] in unbounded else []))}
     for name, (k, m, S, N, mode, pad) in workloads.items():
         if (k, m) not in engines:
             engines[(k, m)] = BatchEngine(k, m, 0)
@@ -157,7 +148,6 @@ def main():
                 engines[(k, m)].set_parity_pad_writes(True)
         eng = engines[(k, m)]
         eng.set_out_pad_writes(name.endswith("+outpad"))
-        eng.set_devmask_buckets(not name.endswith("+nb"))
         t = k + m
         P = shard_pitch_for(S) + pad
         nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))

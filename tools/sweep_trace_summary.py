@@ -3,11 +3,10 @@ and config-3 leg, the HIP-event fraction the bench reported and the rocprof aver
 of the same dispatches in the same process, plus HBM traffic per dispatch from the
 PMC passes (FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024, MI355X_MICROARCH.md §HBM).
 
-A leg's timed window is the reps + 2 calls of its kernel that follow an idle gap
+A leg's timed window is the reps + 2 dispatches of its kernel that follow an idle gap
 of >= 2 ms (bench.py idles 3 ms before each window; kernel_ms_events issues two
 warm-up launches, then the timed ones), the first such after the previous leg's
-window.  The timed ones are the last reps.  A bucketed device-mask call (round 4)
-is four dispatches -- bucket_kernel and three list kernels -- whose durations add.
+window.  The timed ones are the last reps.
 
 Usage: python tools/sweep_trace_summary.py gpurun_out/sweep_<tag> <tag>
 """
@@ -21,10 +20,8 @@ HBM_PEAK_GBS = 8000.0
 SHAPES = {"rs42_64KiB": (4, 2, 16384), "rs84_64KiB": (8, 4, 8192), "rs104_64KiB": (10, 4, 6554)}
 E_OF = {"encode": None, "encode_parity_pad": None, "reconstruct2": 2, "reconstruct1": 1,
         "reconstruct2_out_pad": 2, "reconstruct1_out_pad": 1,
-        "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1, "reconstruct_mixed_unbounded": "mix",
-        "reconstruct_mixed_host": "mix", "reconstruct2_unbounded_bucketed": 2,
-        "reconstruct1_unbounded_bucketed": 1, "reconstruct_mixed_unbounded_bucketed": "mix",
-        "reconstruct_mixed_host_bucketed": "mix"}
+        "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1,
+        "reconstruct_mixed_unbounded": "mix", "reconstruct_mixed_host": "mix"}
 CONFIG3 = {"rec1_per_stripe_out": 1, "rec_0_1_uniform_out": 2, "rec_0_4_uniform_out": 2,
            "rec_4_5_uniform_out": 2, "soa_encode": 2}
 
@@ -48,7 +45,7 @@ def legs(doc):
             if f"{leg}_launches" not in ent:
                 continue
             e = E_OF[leg] if E_OF[leg] is not None else m
-            alg = ent["mixed_alg_bytes"] if e == "mix" else N * S * (k + e)
+            alg = ent["mixed_alg_bytes"] if e == "mix" else N * S * (k + e)  # mixed: bench's exact count
             out.append((f"{shape} {leg}", ent["kernels"][leg], ent[f"{leg}_launches"], alg,
                         ent[f"{leg}_hbm_frac"]))
     for leg, ent in doc.get("config3_patterns_and_soa_rs42_4KiB", {}).items():
@@ -58,40 +55,25 @@ def legs(doc):
 
 
 def windows(trace_csv, want):
-    """Calls of each leg's timed window: reps + 2 calls of the leg's kernel starting
-    right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each window); the
-    first two are kernel_ms_events' warm-up launches.  A call is one dispatch, or for
-    a bucketed device-mask leg ("bucket_kernel+...": round 4) the pre-pass and its
-    three list kernels.  Returns per leg a list of calls (lists of dispatches)."""
+    """Dispatches of each leg's timed window: reps + 2 dispatches of the leg's kernel
+    starting right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each
+    window); the first two are kernel_ms_events' warm-up launches."""
     ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"]]
     ds.sort(key=lambda r: int(r["Start_Timestamp"]))
     res, pos = [], 0
     for label, kern, reps, alg, frac in want:
-        group, first = 1, kern.replace(" ", "")
-        if kern.startswith("bucket_kernel+"):
-            group, first = 4, "bucket_kernel"
-        elif kern.startswith("lists3+"):  # host-built lists: the three list kernels, E = 1 first
-            base = kern.split("+", 1)[1]
-            group, first = 3, base.replace("1|2|" + base.split("1|2|")[1].split(",")[0], "1")
-        need = (reps + 2) * group
         found = None
-        for i in range(pos, len(ds) - need + 1):
+        for i in range(pos, len(ds) - reps - 1):
             if i > 0 and int(ds[i]["Start_Timestamp"]) - int(ds[i - 1]["End_Timestamp"]) < 2_000_000:
                 continue
-            if short(ds[i]["Kernel_Name"]) != first:
+            if short(ds[i]["Kernel_Name"]) != kern.replace(" ", ""):
                 continue
-            heads = [ds[j]["Kernel_Name"] for j in range(i, i + need, group)]
-            if all(h == ds[i]["Kernel_Name"] for h in heads):
-                calls = [ds[j:j + group] for j in range(i, i + need, group)]
-                found = calls[2:]
-                pos = i + need
+            if all(ds[j]["Kernel_Name"] == ds[i]["Kernel_Name"] for j in range(i, i + reps + 2)):
+                found = ds[i + 2:i + reps + 2]
+                pos = i + reps + 2
                 break
         res.append(found)
     return res
-
-
-def dur(d):
-    return int(d["End_Timestamp"]) - int(d["Start_Timestamp"])
 
 
 def main():
@@ -113,8 +95,7 @@ def main():
                 vals[r["Dispatch_Id"]] = float(r["Counter_Value"])
         for (label, *_), win in zip(legs(pdoc), pw):
             if win:
-                v = [sum(vals[d["Dispatch_Id"]] for d in call) for call in win
-                     if all(d["Dispatch_Id"] in vals for d in call)]
+                v = [vals[d["Dispatch_Id"]] for d in win if d["Dispatch_Id"] in vals]
                 if v:
                     traffic.setdefault(label, {})[counter] = statistics.mean(v)
     lines = [f"# bench.py K/M sweep + config 3 under rocprofv3, same process ({tag})", "",
@@ -128,8 +109,7 @@ def main():
         if not win:
             lines.append(f"| {label} | `{kern}` | (window not found) | {frac:.4f} | | | | |")
             continue
-        # per call: the sum of its dispatches' durations (one dispatch, or a bucketed call's four)
-        avg = statistics.mean(sum(dur(d) for d in call) for call in win)
+        avg = statistics.mean(int(d["End_Timestamp"]) - int(d["Start_Timestamp"]) for d in win)
         rf = alg / avg / HBM_PEAK_GBS
         diff = (frac - rf) * 100
         worst = max(worst, abs(diff))
