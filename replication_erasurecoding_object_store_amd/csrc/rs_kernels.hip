@@ -159,6 +159,12 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
+// RS_EM_TWOPASS=1 (A/B): the E > 2 per-stripe kernels compute rows input-outer in
+// passes of at most two rows (rows 0-1, then 2.. only for a task that misses more)
+// instead of splitting every input into chunk indices first.
+#ifndef RS_EM_TWOPASS
+#define RS_EM_TWOPASS 0
+#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -422,7 +428,29 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       }
     };
     u32x4 y[E];
-    if constexpr (PER_STRIPE && E > 2) {
+    if constexpr (PER_STRIPE && E > 2 && RS_EM_TWOPASS != 0) {
+      // input-outer passes of <= 2 rows (RS_EM_TWOPASS, see the flat kernel)
+      const uint32_t nrow = pv.n_out();
+      if (nrow <= 1u) {
+        u32x4 y1[1];
+        gf_rows<K, M, 0, 1>(plan, x, y1);
+        y[0] = y1[0];
+        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, out_cpol<K, 1>()>{}, y);
+        continue;
+      }
+      u32x4 y2[2];
+      gf_rows<K, M, 0, 2>(plan, x, y2);
+      y[0] = y2[0];
+      y[1] = y2[1];
+      if (nrow == 2u) {
+        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, out_cpol<K, 2>()>{}, y);
+        continue;
+      }
+      u32x4 y3[E - 2];
+      gf_rows<K, M, 2, E - 2>(plan, x, y3);
+#pragma unroll
+      for (int r = 2; r < E; ++r) y[r] = y3[r - 2];
+    } else if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
       // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
       // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
@@ -764,7 +792,7 @@ __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t*
 // Rows 0..NR-1 input-outer (as gf_rows) with table dwords chosen per lane between
 // two plans: no chunk-index array (K x 12 VGPRs) is kept, each input is split and
 // used once.  For flat per-stripe launches bounded to E <= 2 erasures.
-template <int K, int M, int NR>
+template <int K, int M, int NR, int R0 = 0>
 __device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* planB, bool inB, const u32x4 (&x)[K],
                                          u32x4 (&y)[NR]) {
   u32x4 pend[NR];
@@ -782,8 +810,8 @@ __device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* pl
     asm volatile("" : "+s"(pb));
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(r, c);
-      const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(r, c);
+      const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(R0 + r, c);
+      const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(R0 + r, c);
       uint32_t q[5];
 #pragma unroll
       for (int i = 0; i < 5; ++i) q[i] = __builtin_amdgcn_bitop3_b32(selB, tb[i], ta[i], 0xCA);  // selB ? tb : ta
@@ -925,6 +953,39 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       else
         gf_rows2<K, M, E>(planA, planB, inB, x, y);
       emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+    } else if constexpr (RS_EM_TWOPASS != 0) {
+      // input-outer passes of <= 2 rows: a task missing 1-2 shards runs the bounded
+      // kernels' code and store policy, x[K] is the only per-input state
+      u32x4 y[E];
+      if (nmax <= 1u) {
+        u32x4 y1[1];
+        if (!diff)
+          gf_rows<K, M, 0, 1>(planA, x, y1);
+        else
+          gf_rows2<K, M, 1>(planA, planB, inB, x, y1);
+        y[0] = y1[0];
+        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, out_cpol<K, 1>()>{}, y);
+      } else {
+        u32x4 y2[2];
+        if (!diff)
+          gf_rows<K, M, 0, 2>(planA, x, y2);
+        else
+          gf_rows2<K, M, 2>(planA, planB, inB, x, y2);
+        y[0] = y2[0];
+        y[1] = y2[1];
+        if (nmax == 2u) {
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, out_cpol<K, 2>()>{}, y);
+        } else {
+          u32x4 y3[E - 2];
+          if (!diff)
+            gf_rows<K, M, 2, E - 2>(planA, x, y3);
+          else
+            gf_rows2<K, M, E - 2, 2>(planA, planB, inB, x, y3);
+#pragma unroll
+          for (int r = 2; r < E; ++r) y[r] = y3[r - 2];
+          emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+        }
+      }
     } else {
       u32x4 y[E];
       Idx3 ix[K][4];
