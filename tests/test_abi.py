@@ -139,3 +139,23 @@ def test_single_hip_runtime_per_process():
     out = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT, check=True).stdout
     libs = eval(out.strip().splitlines()[-1])
     assert len(libs) == 1, libs
+
+
+def test_no_gpu_mapping_of_caller_memory():
+    """DESIGN.md §2 (round 4): the library never creates a GPU mapping of memory it
+    does not own -- no hipHostRegister (userptr ranges whose pages the host kernel may
+    move under a running kernel) and no environment-controlled switches.  In-place
+    kernels address only rs_host_alloc'ed (hipHostMalloc) memory."""
+    import re
+
+    for dirpath, _, files in os.walk(os.path.join(PKG, "csrc")):
+        for fn in files:
+            if not fn.endswith((".cpp", ".hip", ".hpp", ".h", ".inc")):
+                continue
+            src = open(os.path.join(dirpath, fn)).read()
+            code = re.sub(r"//[^\n]*|/\*.*?\*/", "", src, flags=re.S)  # comments may name them
+            assert "hipHostRegister(" not in code, fn
+            assert "getenv(" not in code, fn
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert "hipHostRegister" not in out and "getenv" not in out
