@@ -165,6 +165,13 @@ constexpr int out_cpol() {
 #ifndef RS_EM_TWOPASS
 #define RS_EM_TWOPASS 0
 #endif
+// RS_DEFER_STORES=1 (A/B): apply_kernel's input-outer paths issue a task's stores
+// after the NEXT task's loads, so a wave computes task t+1 while task t's stores are
+// still in flight (vmcnt counts loads and stores in order: stored last, they no longer
+// hold up the next task's first input).
+#ifndef RS_DEFER_STORES
+#define RS_DEFER_STORES 0
+#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -372,6 +379,31 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     for (int r = 0; r < E; ++r) uout[r] = wave_uniform(static_cast<uint32_t>(r) < u_nout ? pv0.out_idx(r) : 0u);
   }
 
+  // deferred stores (RS_DEFER_STORES): the previous task's rows, row bases and
+  // per-lane offsets (kDropOffset: dropped)
+  constexpr bool kDefer = RS_DEFER_STORES != 0 && !(PER_STRIPE && E > 2);
+  constexpr int kCp = out_cpol<K, E>();
+  // (before the first task every store is dropped: the same store sequence on every
+  // trip keeps the compiler's vmcnt counts exact)
+  [[maybe_unused]] u32x4 py[E];
+  [[maybe_unused]] uint8_t* pbase[E];
+  [[maybe_unused]] uint32_t poff[E], ppoff[E];
+  [[maybe_unused]] bool ppart = false;
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    py[r] = u32x4{0u, 0u, 0u, 0u};
+    pbase[r] = a.out ? a.out : a.parity;
+    poff[r] = ppoff[r] = kDropOffset;
+  }
+  [[maybe_unused]] auto flush = [&]() {
+#pragma unroll
+    for (int r = 0; r < E; ++r) __builtin_amdgcn_raw_buffer_store_b128(py[r], out_rsrc(pbase[r]), poff[r], 0, kCp);
+    if (ppart) {  // wave-uniform: the task held its stripe's partial column
+#pragma unroll
+      for (int r = 0; r < E; ++r) store_part_or_drop<kCp>(pbase[r], ppoff[r], ppoff[r] != kDropOffset, py[r], nb);
+    }
+  };
+
   uint32_t mask = 0u;
   if (PER_STRIPE && wave < ntasks) mask = load_mask(wave);
   for (uint32_t t = wave; t < ntasks; t += nwaves) {
@@ -476,11 +508,26 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
           emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
         continue;
       }
+    } else if constexpr (kDefer) {
+      flush();  // the previous task's stores, behind this task's loads
+      gf_rows<K, M, 0, E>(plan, x, y);
+      const bool part = col == a.full_cols;
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const bool row = static_cast<uint32_t>(r) < n_out;
+        py[r] = y[r];
+        pbase[r] = out_ptr(a, K, stripe, r, PER_STRIPE ? pv.out_idx(r) : uout[r]);
+        poff[r] = full && row ? off : kDropOffset;
+        ppoff[r] = part && row ? off : kDropOffset;
+      }
+      ppart = nb != 0u && blk + 1u == bps;
+      continue;
     } else {
       gf_rows<K, M, 0, E>(plan, x, y);
     }
     emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
   }
+  if constexpr (kDefer) flush();
   if (PER_STRIPE && bad && lane == 0u) atomicOr(a.status, bad);
 }
 
