@@ -159,18 +159,10 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
-// RS_EM_TWOPASS=1 (A/B): the E > 2 per-stripe kernels compute rows input-outer in
-// passes of at most two rows (rows 0-1, then 2.. only for a task that misses more)
-// instead of splitting every input into chunk indices first.
-#ifndef RS_EM_TWOPASS
-#define RS_EM_TWOPASS 0
-#endif
-// RS_DEFER_STORES=1 (A/B): apply_kernel's input-outer paths issue a task's stores
-// after the NEXT task's loads, so a wave computes task t+1 while task t's stores are
-// still in flight (vmcnt counts loads and stores in order: stored last, they no longer
-// hold up the next task's first input).
-#ifndef RS_DEFER_STORES
-#define RS_DEFER_STORES 0
+// Largest K whose stripe-aligned E = M kernel computes rows in input-outer passes
+// instead of chunk indices (A/B knob; see apply_kernel).
+#ifndef RS_TWOPASS_MAXK
+#define RS_TWOPASS_MAXK 32
 #endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
@@ -342,14 +334,14 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // per task behind an s_waitcnt vmcnt(0) that also drained the previous task's
 // stores: config 3's uniform 4 KiB patterns fell from 72-77 % to 67-70 %.)
 //
-// Per-stripe batches sized for E > 2 outputs (device masks: E = M) split every
-// input's bytes into chunk indices once (K x 12 VGPRs) and then compute only the
-// rows the stripe misses, one row at a time (gf_row_ix), in wave-uniform branches.
+// Per-stripe batches sized for E > 2 outputs (device masks: E = M) compute only the
+// rows the stripe misses, input-outer in passes of at most two rows, in wave-uniform
+// branches that end in the store sequence of that row count (round 4).
 // A stripe missing more than E shards (possible with device masks under a caller's
 // max_missing bound) is skipped and flagged (status bit 1).
-// Every trip issues the same loads and stores (dropped when not live); the
-// wave-uniform branches hold VALU work only, so the compiler's vmcnt bookkeeping
-// stays exact across them.
+// Every trip issues the same loads; the wave-uniform branches differ only in VALU
+// work and in how many stores end the trip, so the compiler's vmcnt bookkeeping
+// stays exact (a branch around the loads does not: DESIGN.md §9).
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -379,9 +371,16 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     for (int r = 0; r < E; ++r) uout[r] = wave_uniform(static_cast<uint32_t>(r) < u_nout ? pv0.out_idx(r) : 0u);
   }
 
-  // deferred stores (RS_DEFER_STORES): the previous task's rows, row bases and
-  // per-lane offsets (kDropOffset: dropped)
-  constexpr bool kDefer = RS_DEFER_STORES != 0 && !(PER_STRIPE && E > 2);
+  // Deferred stores (round 4): per-stripe RS(4+2) launches issue a task's stores
+  // behind the NEXT task's loads, so the wave computes while they drain -- vmcnt
+  // counts loads and stores in order, and stores issued last no longer hold up the
+  // next task's first input.  Interleaved A/B (profiles/r04f_ab_defer_twopass.log,
+  // >= 100 ms per point): RS(4+2) 4 KiB 2-erasure 73.3 -> 74.5 %, 64 KiB 73.8 -> 74.2 %,
+  // 1-erasure 76.9 -> 77.1 %; the uniform encode 76.7 -> 76.4 % and RS(8+4) bounded
+  // 1-erasure 77.4 -> 77.0 % lose, so those keep the in-order stores.
+  // Kept here: the previous task's rows, row bases and per-lane offsets (kDropOffset:
+  // dropped).
+  constexpr bool kDefer = PER_STRIPE && K <= 4 && E <= 2;
   constexpr int kCp = out_cpol<K, E>();
   // (before the first task every store is dropped: the same store sequence on every
   // trip keeps the compiler's vmcnt counts exact)
@@ -460,14 +459,20 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       }
     };
     u32x4 y[E];
-    if constexpr (PER_STRIPE && E > 2 && RS_EM_TWOPASS != 0) {
-      // input-outer passes of <= 2 rows (RS_EM_TWOPASS, see the flat kernel)
+    if constexpr (PER_STRIPE && E > 2 && K <= RS_TWOPASS_MAXK) {
+      // input-outer passes of <= 2 rows (round 4): rows 0-1, then 2.. only for a task
+      // that misses more.  x[K] is the only per-input state (no chunk-index array:
+      // RS(8+4) 136 -> fewer VGPRs), and a 1-2 erasure task runs the bounded kernels'
+      // row code and store policy.  Interleaved A/B against the former chunk-index form
+      // (profiles/r04f_ab_defer_twopass.log): RS(8+4) 64 KiB unbounded 1-erasure
+      // 73.9 -> 77.6 %, 2-erasure 71.1 -> 71.6 %.  (The flat kernel keeps the chunk-index
+      // form: there the passes lost 1.3 points on 2-erasure and mixed batches.)
       const uint32_t nrow = pv.n_out();
       if (nrow <= 1u) {
         u32x4 y1[1];
         gf_rows<K, M, 0, 1>(plan, x, y1);
         y[0] = y1[0];
-        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, out_cpol<K, 1>()>{}, y);
+        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
         continue;
       }
       u32x4 y2[2];
@@ -475,7 +480,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       y[0] = y2[0];
       y[1] = y2[1];
       if (nrow == 2u) {
-        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, out_cpol<K, 2>()>{}, y);
+        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
         continue;
       }
       u32x4 y3[E - 2];
@@ -484,11 +489,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       for (int r = 2; r < E; ++r) y[r] = y3[r - 2];
     } else if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
-      // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
-      // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
-      // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
-      // (profiles/r02c_ab_ix_rows.log; the former two-pass form recomputed the
-      // indices and computed two rows for every stripe).
+      // (wave-uniform branches; the round-2/3 form, kept for K > RS_TWOPASS_MAXK)
       Idx3 ix[K][4];
 #pragma unroll
       for (int c = 0; c < K; ++c)
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         y[r] = y[0];  // dropped unless computed
         if (static_cast<uint32_t>(r) < nrow) y[r] = gf_row_ix<K, M>(plan, ix, r);
       }
-      if (RS_WAVE_ROWS && n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
+      if (n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
         if (n_out <= 1u)
           emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
         else
@@ -1000,39 +1001,6 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       else
         gf_rows2<K, M, E>(planA, planB, inB, x, y);
       emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-    } else if constexpr (RS_EM_TWOPASS != 0) {
-      // input-outer passes of <= 2 rows: a task missing 1-2 shards runs the bounded
-      // kernels' code and store policy, x[K] is the only per-input state
-      u32x4 y[E];
-      if (nmax <= 1u) {
-        u32x4 y1[1];
-        if (!diff)
-          gf_rows<K, M, 0, 1>(planA, x, y1);
-        else
-          gf_rows2<K, M, 1>(planA, planB, inB, x, y1);
-        y[0] = y1[0];
-        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, out_cpol<K, 1>()>{}, y);
-      } else {
-        u32x4 y2[2];
-        if (!diff)
-          gf_rows<K, M, 0, 2>(planA, x, y2);
-        else
-          gf_rows2<K, M, 2>(planA, planB, inB, x, y2);
-        y[0] = y2[0];
-        y[1] = y2[1];
-        if (nmax == 2u) {
-          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, out_cpol<K, 2>()>{}, y);
-        } else {
-          u32x4 y3[E - 2];
-          if (!diff)
-            gf_rows<K, M, 2, E - 2>(planA, x, y3);
-          else
-            gf_rows2<K, M, E - 2, 2>(planA, planB, inB, x, y3);
-#pragma unroll
-          for (int r = 2; r < E; ++r) y[r] = y3[r - 2];
-          emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-        }
-      }
     } else {
       u32x4 y[E];
       Idx3 ix[K][4];

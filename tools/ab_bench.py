@@ -60,6 +60,10 @@ WORKLOADS = {
     # apply_kernel: 384 / 512 columns) and a tail-free flat one (416 columns)
     "rs104_S6144_rec1pb_out": (10, 4, 6144, 16384, "rec1pb_out"),
     "rs104_S6144_rec2pb_out": (10, 4, 6144, 16384, "rec2pb_out"),
+    "rs104_S6144_rec1p_out": (10, 4, 6144, 16384, "rec1p_out"),   # stripe-aligned E = M kernel
+    "rs104_S6144_rec2p_out": (10, 4, 6144, 16384, "rec2p_out"),
+    "rs104_S6144_rec4p_out": (10, 4, 6144, 16384, "rec4p_out"),
+    "rs84_64K_rec4p_out": (8, 4, 8192, 16384, "rec4p_out"),
     "rs104_S8192_rec1pb_out": (10, 4, 8192, 16384, "rec1pb_out"),
     "rs104_S8192_rec2pb_out": (10, 4, 8192, 16384, "rec2pb_out"),
     "rs104_S6656_rec1pb_out": (10, 4, 6656, 16384, "rec1pb_out"),
