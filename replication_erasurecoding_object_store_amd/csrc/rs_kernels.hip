@@ -159,11 +159,6 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
-// Largest K whose stripe-aligned E = M kernel computes rows in input-outer passes
-// instead of chunk indices (A/B knob; see apply_kernel).
-#ifndef RS_TWOPASS_MAXK
-#define RS_TWOPASS_MAXK 32
-#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -334,9 +329,10 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // per task behind an s_waitcnt vmcnt(0) that also drained the previous task's
 // stores: config 3's uniform 4 KiB patterns fell from 72-77 % to 67-70 %.)
 //
-// Per-stripe batches sized for E > 2 outputs (device masks: E = M) compute only the
-// rows the stripe misses, input-outer in passes of at most two rows, in wave-uniform
-// branches that end in the store sequence of that row count (round 4).
+// Per-stripe batches sized for E > 2 outputs (device masks: E = M) split every
+// input's bytes into chunk indices once (K x 12 VGPRs) and then compute only the
+// rows the stripe misses, one row at a time (gf_row_ix), in wave-uniform branches
+// that end in the store sequence of that row count (round 4).
 // A stripe missing more than E shards (possible with device masks under a caller's
 // max_missing bound) is skipped and flagged (status bit 1).
 // Every trip issues the same loads; the wave-uniform branches differ only in VALU
@@ -459,37 +455,14 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       }
     };
     u32x4 y[E];
-    if constexpr (PER_STRIPE && E > 2 && K <= RS_TWOPASS_MAXK) {
-      // input-outer passes of <= 2 rows (round 4): rows 0-1, then 2.. only for a task
-      // that misses more.  x[K] is the only per-input state (no chunk-index array:
-      // RS(8+4) 136 -> fewer VGPRs), and a 1-2 erasure task runs the bounded kernels'
-      // row code and store policy.  Interleaved A/B against the former chunk-index form
-      // (profiles/r04f_ab_defer_twopass.log): RS(8+4) 64 KiB unbounded 1-erasure
-      // 73.9 -> 77.6 %, 2-erasure 71.1 -> 71.6 %.  (The flat kernel keeps the chunk-index
-      // form: there the passes lost 1.3 points on 2-erasure and mixed batches.)
-      const uint32_t nrow = pv.n_out();
-      if (nrow <= 1u) {
-        u32x4 y1[1];
-        gf_rows<K, M, 0, 1>(plan, x, y1);
-        y[0] = y1[0];
-        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
-        continue;
-      }
-      u32x4 y2[2];
-      gf_rows<K, M, 0, 2>(plan, x, y2);
-      y[0] = y2[0];
-      y[1] = y2[1];
-      if (nrow == 2u) {
-        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-        continue;
-      }
-      u32x4 y3[E - 2];
-      gf_rows<K, M, 2, E - 2>(plan, x, y3);
-#pragma unroll
-      for (int r = 2; r < E; ++r) y[r] = y3[r - 2];
-    } else if constexpr (PER_STRIPE && E > 2) {
+    if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
-      // (wave-uniform branches; the round-2/3 form, kept for K > RS_TWOPASS_MAXK)
+      // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
+      // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
+      // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
+      // (profiles/r02c_ab_ix_rows.log).  Input-outer passes of <= 2 rows instead
+      // (round 4) lost 9-10 points on 4-erasure and mixed batches
+      // (profiles/r04g_ab_twopass.log).
       Idx3 ix[K][4];
 #pragma unroll
       for (int c = 0; c < K; ++c)
@@ -502,7 +475,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         y[r] = y[0];  // dropped unless computed
         if (static_cast<uint32_t>(r) < nrow) y[r] = gf_row_ix<K, M>(plan, ix, r);
       }
-      if (n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
+      if (RS_WAVE_ROWS && n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
         if (n_out <= 1u)
           emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
         else
