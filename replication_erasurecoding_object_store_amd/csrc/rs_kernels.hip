@@ -159,6 +159,11 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
+// RS_FLAT_DEFER=1 (A/B): the flat per-stripe kernel's E <= 2 path issues a task's
+// stores behind the next task's loads (as apply_kernel does for RS(4+2)).
+#ifndef RS_FLAT_DEFER
+#define RS_FLAT_DEFER 0
+#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -889,6 +894,29 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     return p;
   };
 
+  // deferred stores (RS_FLAT_DEFER, E <= 2): the previous task's rows, its output
+  // descriptor and per-lane offsets (kDropOffset: dropped; all dropped before the
+  // first task, so every trip issues the same store sequence)
+  constexpr bool kFDefer = RS_FLAT_DEFER != 0 && E <= 2;
+  constexpr int kFCp = out_cpol<K, E>();
+  [[maybe_unused]] u32x4 fpy[E];
+  [[maybe_unused]] uint32_t fpoff[E], fppoff[E];
+  [[maybe_unused]] bool fppart = false;
+  [[maybe_unused]] auto fpout = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    fpy[r] = u32x4{0u, 0u, 0u, 0u};
+    fpoff[r] = fppoff[r] = kDropOffset;
+  }
+  [[maybe_unused]] auto fflush = [&]() {
+#pragma unroll
+    for (int r = 0; r < E; ++r) __builtin_amdgcn_raw_buffer_store_b128(fpy[r], fpout, fpoff[r], r * pitch, kFCp);
+    if (fppart) {  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < E; ++r)
+        store_part_rsrc<kFCp>(fpout, fppoff[r], r * pitch, fppoff[r] != kDropOffset, fpy[r], nb);
+    }
+  };
   auto next_task = [&] {  // grid stride in the flat column space
     c0 += step_c;
     s0 += step_s;
@@ -969,11 +997,24 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
       // launch computes a row it does not store): x[K] only, no index array
       u32x4 y[E];
+      if constexpr (kFDefer) fflush();  // the previous task's stores, behind this task's loads
       if (!diff)
         gf_rows<K, M, 0, E>(planA, x, y);
       else
         gf_rows2<K, M, E>(planA, planB, inB, x, y);
-      emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+      if constexpr (kFDefer) {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const bool row = static_cast<uint32_t>(r) < nl;
+          fpy[r] = y[r];
+          fpoff[r] = fullc && row ? offO : kDropOffset;
+          fppoff[r] = part && row ? offO : kDropOffset;
+        }
+        fpout = oout;
+        fppart = __builtin_amdgcn_ballot_w64(part) != 0u;
+      } else {
+        emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+      }
     } else {
       u32x4 y[E];
       Idx3 ix[K][4];
@@ -1005,6 +1046,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     }
     next_task();
   }
+  if constexpr (kFDefer) fflush();
   if (bad && lane == 0u) atomicOr(a.status, bad);
 }
 
