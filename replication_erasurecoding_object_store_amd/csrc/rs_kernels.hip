@@ -642,6 +642,11 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #ifndef RS_BS_OCC
 #define RS_BS_OCC 3
 #endif
+// RS_BS_DEFER=1 (A/B): the bitsliced encode issues a task's full-column parity stores
+// behind the next task's first window of loads (8M dwords kept across the trip).
+#ifndef RS_BS_DEFER
+#define RS_BS_DEFER 0
+#endif
 constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
 
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -723,6 +728,22 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
   const uint64_t gstep = static_cast<uint64_t>(nwaves) * 128u;
   const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
   const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  // deferred parity stores (RS_BS_DEFER): the previous task's rows, descriptor and
+  // per-lane offsets (all dropped before the first task)
+  [[maybe_unused]] u32x4 dlo[M], dhi[M];
+  [[maybe_unused]] uint32_t doa = kDropOffset, dob = kDropOffset;
+  [[maybe_unused]] auto dout = __builtin_amdgcn_make_buffer_rsrc(a.parity, 0, 0x7FFFFFFF, 0x00020000);
+  if constexpr (RS_BS_DEFER != 0) {
+#pragma unroll
+    for (int r = 0; r < M; ++r) dlo[r] = dhi[r] = u32x4{0u, 0u, 0u, 0u};
+  }
+  [[maybe_unused]] auto dflush = [&]() {
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      __builtin_amdgcn_raw_buffer_store_b128(dlo[r], dout, doa, r * pitch, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(dhi[r], dout, dob, r * pitch, 2 /* nt */);
+    }
+  };
   while (s0 < a.n_stripes) {
     const FlatCol fa = flat_col(a, s0, c0 + lane, cstride, cols);
     const FlatCol fb = flat_col(a, s0, c0 + 64u + lane, cstride, cols);
@@ -736,6 +757,7 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       xa[c] = bload16(din, fa.doff, c * pitch);
       xb[c] = bload16(din, fb.doff, c * pitch);
     }
+    if constexpr (RS_BS_DEFER != 0) dflush();  // the previous task's parity, behind this task's loads
     uint32_t y[8 * M];
     bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
     const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
@@ -749,9 +771,19 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
       transpose8(d);
       const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
-      __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
-      __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
+      if constexpr (RS_BS_DEFER != 0) {
+        dlo[r] = lo;
+        dhi[r] = hi;
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
+        __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
+      }
       part[r] = pb ? hi : lo;
+    }
+    if constexpr (RS_BS_DEFER != 0) {
+      doa = sa ? fa.poff : kDropOffset;
+      dob = sb ? fb.poff : kDropOffset;
+      dout = pout;
     }
     if (nb != 0u && __builtin_amdgcn_ballot_w64(pa || pb) != 0u) {  // wave-uniform
       const uint32_t off = pb ? fb.poff : fa.poff;
@@ -765,6 +797,7 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       ++s0;
     }
   }
+  if constexpr (RS_BS_DEFER != 0) dflush();
 }
 
 // ---------------------------------------------------------------------------
