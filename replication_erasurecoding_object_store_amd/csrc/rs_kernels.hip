@@ -159,11 +159,6 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
-// RS_FLAT_DEFER=1 (A/B): the flat per-stripe kernel's E <= 2 path issues a task's
-// stores behind the next task's loads (as apply_kernel does for RS(4+2)).
-#ifndef RS_FLAT_DEFER
-#define RS_FLAT_DEFER 0
-#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -642,11 +637,6 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #ifndef RS_BS_OCC
 #define RS_BS_OCC 3
 #endif
-// RS_BS_DEFER=1 (A/B): the bitsliced encode issues a task's full-column parity stores
-// behind the next task's first window of loads (8M dwords kept across the trip).
-#ifndef RS_BS_DEFER
-#define RS_BS_DEFER 0
-#endif
 constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
 
 __device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
@@ -728,22 +718,6 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
   const uint64_t gstep = static_cast<uint64_t>(nwaves) * 128u;
   const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
   const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
-  // deferred parity stores (RS_BS_DEFER): the previous task's rows, descriptor and
-  // per-lane offsets (all dropped before the first task)
-  [[maybe_unused]] u32x4 dlo[M], dhi[M];
-  [[maybe_unused]] uint32_t doa = kDropOffset, dob = kDropOffset;
-  [[maybe_unused]] auto dout = __builtin_amdgcn_make_buffer_rsrc(a.parity, 0, 0x7FFFFFFF, 0x00020000);
-  if constexpr (RS_BS_DEFER != 0) {
-#pragma unroll
-    for (int r = 0; r < M; ++r) dlo[r] = dhi[r] = u32x4{0u, 0u, 0u, 0u};
-  }
-  [[maybe_unused]] auto dflush = [&]() {
-#pragma unroll
-    for (int r = 0; r < M; ++r) {
-      __builtin_amdgcn_raw_buffer_store_b128(dlo[r], dout, doa, r * pitch, 2 /* nt */);
-      __builtin_amdgcn_raw_buffer_store_b128(dhi[r], dout, dob, r * pitch, 2 /* nt */);
-    }
-  };
   while (s0 < a.n_stripes) {
     const FlatCol fa = flat_col(a, s0, c0 + lane, cstride, cols);
     const FlatCol fb = flat_col(a, s0, c0 + 64u + lane, cstride, cols);
@@ -757,7 +731,6 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       xa[c] = bload16(din, fa.doff, c * pitch);
       xb[c] = bload16(din, fb.doff, c * pitch);
     }
-    if constexpr (RS_BS_DEFER != 0) dflush();  // the previous task's parity, behind this task's loads
     uint32_t y[8 * M];
     bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
     const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
@@ -771,19 +744,9 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
       transpose8(d);
       const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
-      if constexpr (RS_BS_DEFER != 0) {
-        dlo[r] = lo;
-        dhi[r] = hi;
-      } else {
-        __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
-        __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
-      }
+      __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
       part[r] = pb ? hi : lo;
-    }
-    if constexpr (RS_BS_DEFER != 0) {
-      doa = sa ? fa.poff : kDropOffset;
-      dob = sb ? fb.poff : kDropOffset;
-      dout = pout;
     }
     if (nb != 0u && __builtin_amdgcn_ballot_w64(pa || pb) != 0u) {  // wave-uniform
       const uint32_t off = pb ? fb.poff : fa.poff;
@@ -797,7 +760,6 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       ++s0;
     }
   }
-  if constexpr (RS_BS_DEFER != 0) dflush();
 }
 
 // ---------------------------------------------------------------------------
@@ -927,29 +889,6 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     return p;
   };
 
-  // deferred stores (RS_FLAT_DEFER, E <= 2): the previous task's rows, its output
-  // descriptor and per-lane offsets (kDropOffset: dropped; all dropped before the
-  // first task, so every trip issues the same store sequence)
-  constexpr bool kFDefer = RS_FLAT_DEFER != 0 && E <= 2;
-  constexpr int kFCp = out_cpol<K, E>();
-  [[maybe_unused]] u32x4 fpy[E];
-  [[maybe_unused]] uint32_t fpoff[E], fppoff[E];
-  [[maybe_unused]] bool fppart = false;
-  [[maybe_unused]] auto fpout = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-  for (int r = 0; r < E; ++r) {
-    fpy[r] = u32x4{0u, 0u, 0u, 0u};
-    fpoff[r] = fppoff[r] = kDropOffset;
-  }
-  [[maybe_unused]] auto fflush = [&]() {
-#pragma unroll
-    for (int r = 0; r < E; ++r) __builtin_amdgcn_raw_buffer_store_b128(fpy[r], fpout, fpoff[r], r * pitch, kFCp);
-    if (fppart) {  // wave-uniform
-#pragma unroll
-      for (int r = 0; r < E; ++r)
-        store_part_rsrc<kFCp>(fpout, fppoff[r], r * pitch, fppoff[r] != kDropOffset, fpy[r], nb);
-    }
-  };
   auto next_task = [&] {  // grid stride in the flat column space
     c0 += step_c;
     s0 += step_s;
@@ -1030,24 +969,11 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
       // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
       // launch computes a row it does not store): x[K] only, no index array
       u32x4 y[E];
-      if constexpr (kFDefer) fflush();  // the previous task's stores, behind this task's loads
       if (!diff)
         gf_rows<K, M, 0, E>(planA, x, y);
       else
         gf_rows2<K, M, E>(planA, planB, inB, x, y);
-      if constexpr (kFDefer) {
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          const bool row = static_cast<uint32_t>(r) < nl;
-          fpy[r] = y[r];
-          fpoff[r] = fullc && row ? offO : kDropOffset;
-          fppoff[r] = part && row ? offO : kDropOffset;
-        }
-        fpout = oout;
-        fppart = __builtin_amdgcn_ballot_w64(part) != 0u;
-      } else {
-        emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-      }
+      emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
     } else {
       u32x4 y[E];
       Idx3 ix[K][4];
@@ -1079,7 +1005,6 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
     }
     next_task();
   }
-  if constexpr (kFDefer) fflush();
   if (bad && lane == 0u) atomicOr(a.status, bad);
 }
 
