@@ -77,6 +77,12 @@ __device__ __forceinline__ u32x4 load16(const uint8_t* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
+// 16-B non-temporal buffer load: an offset past the descriptor's range fetches
+// nothing and returns zeros.
+__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2 /* nt */));
+}
+
 __device__ __forceinline__ void store16(uint8_t* p, u32x4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
 }
@@ -158,6 +164,12 @@ constexpr int out_cpol() {
 // the dropped stores alone).
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
+#endif
+// RS_PS_BUFLOADS=1 (A/B): apply_kernel's per-stripe inputs through buffer descriptors
+// over their slots (range-checked), with every load of an intact or skipped stripe
+// out of range (nothing fetched, the same load sequence per trip).
+#ifndef RS_PS_BUFLOADS
+#define RS_PS_BUFLOADS 0
 #endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
@@ -405,6 +417,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t stripe = t / bps;
     const uint32_t blk = t - stripe * bps;
     const uint8_t* plan = a.plans;
+    [[maybe_unused]] bool work = true;  // the stripe has rows to fill
     if (PER_STRIPE) {
       const uint32_t present = __builtin_amdgcn_readfirstlane(mask);  // waits for this mask only
       mask = load_mask(t + nwaves);                                  // next task's mask in flight
@@ -418,6 +431,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         pid = over ? 0u : pid;
       }
       plan = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+      work = pid != 0u;
     }
     if constexpr (K * ((PER_STRIPE && E > 2) ? 2 : E) * 5 > 48) {
       // Too many table dwords to keep resident in SGPRs across trips: make the plan
@@ -433,8 +447,19 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
 
     u32x4 x[K];
+    if constexpr (PER_STRIPE && RS_PS_BUFLOADS != 0) {
+      const uint32_t loff = work ? off : kDropOffset;
 #pragma unroll
-    for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, PER_STRIPE ? pv.in_idx(c) : uin[c]) + off);
+      for (int c = 0; c < K; ++c) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(uniform_ptr(slot_ptr(a, K, stripe, pv.in_idx(c)))), 0,
+            static_cast<uint32_t>(a.shard_pitch), 0x00020000);
+        x[c] = bload16(r, loff, 0);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, PER_STRIPE ? pv.in_idx(c) : uin[c]) + off);
+    }
 
     const uint32_t n_out = PER_STRIPE ? pv.n_out() : u_nout;
     // stores rows [0, NR) of the task (the rest of the launch's E rows need none)
@@ -639,9 +664,6 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #endif
 constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
 
-__device__ __forceinline__ u32x4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 2 /* nt */));
-}
 
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off_a, uint32_t off_b,
