@@ -213,6 +213,7 @@ struct UploadSlot {
   PinnedBuf host;
   DevBuf dev;
   hipEvent_t done = nullptr;
+  hipEvent_t copied = nullptr;  // the masks' H2D on the engine's upload stream
   bool used = false;
   bool busy = false;
 };
@@ -316,6 +317,9 @@ struct Engine {
   std::condition_variable upload_cv;
   UploadSlot uploads[kUploadSlots];
   size_t upload_next = 0;
+  // Host-mask H2D copies run here, off the caller's stream, which only waits on the
+  // copy's event: the copy overlaps the kernels already queued there (round 4).
+  hipStream_t upload_st = nullptr;
 
   std::mutex host_mu;                     // host-resident batches: one at a time per engine
   hipStream_t pipe_st[kHostStreams] = {};
@@ -366,8 +370,11 @@ struct Engine {
     }
     if (worker.joinable()) worker.join();
     (void)hipDeviceSynchronize();
-    for (auto& s : uploads)
+    for (auto& s : uploads) {
       if (s.done) (void)hipEventDestroy(s.done);
+      if (s.copied) (void)hipEventDestroy(s.copied);
+    }
+    if (upload_st) (void)hipStreamDestroy(upload_st);
     for (auto& l : lanes)
       if (l->stream) (void)hipStreamDestroy(l->stream);
     for (auto& s : pipe_st)
@@ -833,16 +840,27 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
       e->upload_cv.wait(lk);
     }
     u->busy = true;
+    if (!e->upload_st && hipStreamCreateWithFlags(&e->upload_st, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      e->upload_st = nullptr;  // the copy then runs on the caller's stream
+    }
   }
   g->e = e;
   g->u = u;
   g->s = s;
   if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
+  if (!u->copied) RS_HIP(hipEventCreateWithFlags(&u->copied, hipEventDisableTiming));
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
   u->host.numa = e->numa;
   if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
   std::memcpy(u->host.p, masks, n * 4);
-  RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
+  if (e->upload_st) {
+    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, e->upload_st));
+    RS_HIP(hipEventRecord(u->copied, e->upload_st));
+    RS_HIP(hipStreamWaitEvent(s, u->copied, 0));
+  } else {
+    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
+  }
   *dev = static_cast<const uint32_t*>(u->dev.p);
   return RS_OK;
 }
