@@ -165,12 +165,6 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS_CPOL
 #define RS_WAVE_ROWS_CPOL 1
 #endif
-// RS_PS_BUFLOADS=1 (A/B): apply_kernel's per-stripe inputs through buffer descriptors
-// over their slots (range-checked), with every load of an intact or skipped stripe
-// out of range (nothing fetched, the same load sequence per trip).
-#ifndef RS_PS_BUFLOADS
-#define RS_PS_BUFLOADS 0
-#endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
   return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
@@ -447,7 +441,15 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
     const uint32_t off = (col < cols ? col : cols - 1u) * 16u;
 
     u32x4 x[K];
-    if constexpr (PER_STRIPE && RS_PS_BUFLOADS != 0) {
+    if constexpr (PER_STRIPE && E > 2) {
+      // Launches sized for E = M (device masks without a bound: a scan's batch of intact
+      // and damaged stripes) load through a descriptor over each input's slot
+      // (range-checked), and an intact or skipped stripe's loads are all out of range:
+      // nothing is fetched, and every trip keeps the same load sequence (round 4).
+      // Interleaved A/B (profiles/r04j_ab_psbuf.log): RS(8+4) mixed 0..4 erasures
+      // 57.0 -> 66.1 % (host masks 49.7 -> 56.7 %), uniform 1-erasure 76.2 -> 77.1 %;
+      // the E <= 2 kernels lose 0.8-2.0 points with these loads, so they keep global
+      // loads (their callers know the stripes are damaged).
       const uint32_t loff = work ? off : kDropOffset;
 #pragma unroll
       for (int c = 0; c < K; ++c) {
