@@ -956,14 +956,17 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
                                             : bload16(pin, offP, (s - static_cast<uint32_t>(K)) * pitch);
       }
     } else {
+      // E = M launches (a scan's mixed batch): the lanes of an intact stripe next to a
+      // damaged one fetch nothing either (their stores are dropped anyway)
+      const bool need = E <= 2 || (inB ? nB : nA) != 0u;
 #pragma unroll
       for (int c = 0; c < K; ++c) {
         const uint32_t sa = pop_low(bitsA), sb = pop_low(bitsB);
         const uint32_t s = inB ? sb : sa;
         const bool par = s >= static_cast<uint32_t>(K);
         const uint32_t so = (par ? s - static_cast<uint32_t>(K) : s) * pitch;
-        const u32x4 xd = bload16(din, par ? kDropOffset : offD + so, 0);
-        const u32x4 xp = bload16(pin, par ? offP + so : kDropOffset, 0);
+        const u32x4 xd = bload16(din, par || !need ? kDropOffset : offD + so, 0);
+        const u32x4 xp = bload16(pin, par && need ? offP + so : kDropOffset, 0);
         x[c] = xd | xp;
       }
     }
