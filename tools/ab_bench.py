@@ -44,6 +44,9 @@ WORKLOADS = {
     "rs84_64K_rec2pb_out": (8, 4, 8192, 16384, "rec2pb_out"),
     "rs84_64K_rec1p_out": (8, 4, 8192, 16384, "rec1p_out"),
     "rs42_4K_rec04u_out": (4, 2, 1024, 65536, "rec04u_out"),
+    "rs42_4K_rec04p_out": (4, 2, 1024, 65536, "rec04p_out"),    # devmask, all stripes miss {0,4}
+    "rs42_4K_rec01p_out": (4, 2, 1024, 65536, "rec01p_out"),    # devmask, all stripes miss {0,1}
+    "rs42_4K_rec01u_out": (4, 2, 1024, 65536, "rec2u_out"),     # uniform host mask {0,1}
     "rs42_4K_rec1pb_out": (4, 2, 1024, 65536, "rec1pb_out"),
     "rs42_64K_rec1pb_out": (4, 2, 16384, 16384, "rec1pb_out"),
     "rs42_4K_rec45u_out": (4, 2, 1024, 65536, "rec45u_out"),
@@ -179,6 +182,7 @@ def main():
         mixd = torch.from_numpy(mix.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
+        m04 = torch.full((N,), ((1 << t) - 1) & ~0b10001, dtype=torch.int32, device="cuda")
         md0 = torch.full((N,), ((1 << t) - 1) & ~1, dtype=torch.int32, device="cuda")
         mp13 = torch.full((N,), ((1 << t) - 1) & ~(1 << (t - 1)), dtype=torch.int32, device="cuda")
         rows = bounded_rows[mode] if name.endswith("+dense") else m
@@ -221,6 +225,8 @@ def main():
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks4)
             elif mode == "rec2p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=masks[i % nb])
+            elif mode == "rec04p_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=m04)
             elif mode == "rec01p_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=m01)
             elif mode == "rec2ph_out":
