@@ -624,9 +624,10 @@ struct BsNet {
 };
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_step(const uint32_t (&x)[8], uint32_t (&y)[8 * M]);
-// Prefix programs (parity rows 0..R-1 only) for the bitsliced reconstruct kernel.
-template <int K, int M, int R, int C>
-__device__ __forceinline__ void bs_pstep(const uint32_t (&x)[8], uint32_t (&y)[8 * R]);
+// Grouped programs: inputs C0..C0+N-1 (N <= 4) transposed into x[0 .. 8N), their
+// common pairs shared across the group (RS_BS_GROUP=4).
+template <int K, int M, int C0, int N>
+__device__ __forceinline__ void bs_gstep(const uint32_t (&x)[32], uint32_t (&y)[8 * M]);
 
 #include "rs_xor_networks.inc"
 
@@ -665,11 +666,17 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #define RS_BS_OCC 3
 #endif
 constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
+#ifndef RS_BS_GROUP
+#define RS_BS_GROUP 1
+#endif
+constexpr int kBsGroup = RS_BS_GROUP;  // 1: per-input programs; 4: grouped (bs_gstep)
+static_assert(kBsGroup == 1 || kBsGroup == 4, "rs_xor_networks.inc has groups of 4");
 
-
+// g: the transposed planes of the current group (kBsGroup = 4 only)
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off_a, uint32_t off_b,
-                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&y)[8 * M]) {
+                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&g)[32],
+                                        uint32_t (&y)[8 * M]) {
   if constexpr (C < K) {
     constexpr int slot = C % kBsWindow;
     uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
@@ -679,8 +686,15 @@ __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pit
       xb[slot] = bload16(din, off_b, (C + kBsWindow) * pitch);
     }
     transpose8(d);
-    bs_step<K, M, C>(d, y);
-    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, y);
+    if constexpr (kBsGroup == 1) {
+      bs_step<K, M, C>(d, y);
+    } else {
+      constexpr int gi = C % kBsGroup;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[gi * 8 + i] = d[i];
+      if constexpr (gi == kBsGroup - 1 || C == K - 1) bs_gstep<K, M, C - gi, gi + 1>(g, y);
+    }
+    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, g, y);
   }
 }
 
@@ -756,7 +770,8 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       xb[c] = bload16(din, fb.doff, c * pitch);
     }
     uint32_t y[8 * M];
-    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
+    uint32_t grp[32];
+    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, grp, y);
     const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
     const bool pa = nb != 0u && fa.live && fa.col == a.full_cols;  // this lane holds a partial column
     const bool pb = nb != 0u && fb.live && fb.col == a.full_cols;

@@ -173,7 +173,7 @@ def test_devmask_bound_flags_and_skips_excess(engines, k, m, S, bound):
 # Larger batches than the parity tests, two pattern draws each, every output row
 # and every unused output slot compared (vectorised).
 @pytest.mark.parametrize("k,m,S,bound", [(8, 4, 6554, 1), (10, 4, 6554, 2), (8, 4, 6554, 4), (8, 4, 8192, 1),
-                                         (10, 4, 6554, 1)])
+                                         (10, 4, 6554, 1), (8, 4, 8192, 4), (10, 4, 6554, 4), (4, 2, 1024, 2)])
 def test_out_of_place_stress(engines, k, m, S, bound):
     import torch
 
@@ -189,13 +189,17 @@ def test_out_of_place_stress(engines, k, m, S, bound):
         masks = _masks(rng, N, t, 0, bound)
         # expected out[i, r] = shard of the r-th missing index of stripe i
         missing = [[j for j in range(t) if not (int(masks[i]) >> j) & 1] for i in range(N)]
-        for mode in ("host", "dev"):
+        # dev: the caller's bound (E = bound kernels); devu: no bound, the E = M kernels
+        # (slot-descriptor loads, intact stripes and intact halves of straddling tasks
+        # fetch nothing, round 4)
+        for mode in ("host", "dev", "devu"):
             out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
             if mode == "host":
                 eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
             else:
                 eng.reconstruct_out(data, parity, out, S, N,
-                                    masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(), max_missing=bound)
+                                    masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
+                                    max_missing=bound if mode == "dev" else 0)
                 eng.sync()
             torch.cuda.synchronize()
             got = out.cpu().numpy()

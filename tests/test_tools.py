@@ -33,3 +33,23 @@ def test_xor_network_rows_are_the_oracle_encode_matrix():
     for k, m in mod.SHAPES:
         rows = np.array(mod.parity_rows(k, m), dtype=np.uint8)
         assert np.array_equal(rows, np.asarray(rs_oracle.build_matrix(k, m), dtype=np.uint8)[k:]), (k, m)
+
+
+def _planes(col: np.ndarray):
+    """32 bytes -> 8 plane words, plane j bit b = bit j of byte b."""
+    return [sum(((int(col[b]) >> j) & 1) << b for b in range(32)) for j in range(8)]
+
+
+def test_xor_programs_compute_the_encode():
+    """Both forms of the generated XOR programs (per input, and shared over groups of
+    4 inputs) evaluated on random bitsliced columns give the oracle's parity bytes."""
+    mod = _gen()
+    rng = np.random.default_rng(5)
+    for k, m in mod.SHAPES:
+        data = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        shards = [bytearray(data[c].tobytes()) for c in range(k)] + [bytearray(32) for _ in range(m)]
+        rs_oracle.encode(k, m, shards)
+        want = [_planes(np.frombuffer(bytes(shards[k + r]), np.uint8)) for r in range(m)]
+        for y in mod.evaluate(k, m, [_planes(data[c]) for c in range(k)]):
+            got = [y[r * 8:(r + 1) * 8] for r in range(m)]
+            assert got == want, (k, m)

@@ -26,9 +26,6 @@ import os
 from collections import Counter
 
 SHAPES = [(4, 2), (8, 4), (10, 4), (6, 3)]
-# shapes that also get prefix programs (parity rows 0..R-1, R = 1..M) for the
-# bitsliced reconstruct kernel
-PREFIX_SHAPES = [(8, 4), (10, 4)]
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "replication_erasurecoding_object_store_amd", "csrc", "rs_xor_networks.inc")
 
@@ -85,14 +82,21 @@ def parity_rows(k: int, m: int):
 
 
 # ---- XOR programs ---------------------------------------------------------------
-def input_rows(rows, k, m, c):
-    """For input c: output plane p = (r*8 + i) needs XOR of planes {j : bit i of
-    f_rc * 2^j}, for the first m parity rows."""
+# Group size of the grouped programs (bs_gstep): inputs C0..C0+G-1 transposed and live
+# together, their common pairs shared across the group (RS_BS_GROUP=4 in
+# rs_kernels.hip; the per-input bs_step programs are the default).
+GROUP = 4
+
+
+def group_rows(rows, m, cs):
+    """Output plane p = (r*8 + i) of parity row r < m needs the XOR of the input
+    planes (ci*8 + j) of inputs cs[ci] whose GF(2) matrix bit is set:
+    bit i of f_rc * 2^j."""
     out = []
     for r in range(m):
-        f = rows[r][c]
         for i in range(8):
-            out.append(frozenset(j for j in range(8) if (mul(f, 1 << j) >> i) & 1))
+            out.append(frozenset(ci * 8 + j for ci, c in enumerate(cs) for j in range(8)
+                                 if (mul(rows[r][c], 1 << j) >> i) & 1))
     return out
 
 
@@ -123,30 +127,56 @@ def paar(subsets):
     return temps, rows
 
 
-def emit_step(k, m, c, rows, r_rows=None):
-    """Step of input c.  r_rows=None: the full encode program bs_step<k, m, c>
-    (all m rows); r_rows=R: the prefix program bs_pstep<k, m, R, c> over parity
-    rows 0..R-1 only (the reconstruct kernel's syndrome / re-encode rows)."""
-    nr = m if r_rows is None else r_rows
-    subsets = input_rows(rows, k, nr, c)
-    temps, red = paar(subsets)
-    head = (f"bs_step<{k}, {m}, {c}>" if r_rows is None else f"bs_pstep<{k}, {m}, {r_rows}, {c}>")
-    lines = [f"template <> __device__ __forceinline__ void {head}(const uint32_t (&x)[8], "
-             f"uint32_t (&y)[{8 * nr}]) {{"]
+def program(k, m, cs):
+    """XOR program of inputs cs (a group, or one input): (temps, rows)."""
+    return paar(group_rows(parity_rows(k, m), m, cs))
+
+
+def evaluate(k, m, planes_by_input):
+    """Reference evaluation of the per-input and the grouped programs (tests):
+    planes_by_input[c] = 8 plane words of input c; returns (per-input result,
+    grouped result), each 8m plane words."""
+    res = []
+    for size in (1, GROUP):
+        y = [0] * (8 * m)
+        for c0 in range(0, k, size):
+            cs = list(range(c0, min(k, c0 + size)))
+            temps, red = program(k, m, cs)
+            env = {f"x{ci * 8 + j}": planes_by_input[c][j] for ci, c in enumerate(cs) for j in range(8)}
+            for name, a, b in temps:
+                env[name] = env[a] ^ env[b]
+            for p, r in enumerate(red):
+                for o in r:
+                    y[p] ^= env[o]
+        res.append(y)
+    return res
+
+
+def _operand(o):
+    return f"x[{o[1:]}]" if o[0] == "x" else o
+
+
+def emit(k, m, cs, grouped):
+    """bs_step<k, m, c> (one input, cs = [c]) or bs_gstep<k, m, c0, n> (a group of n
+    inputs c0.. in the first 8n planes of x[8 * GROUP])."""
+    temps, red = program(k, m, cs)
+    head = (f"bs_gstep<{k}, {m}, {cs[0]}, {len(cs)}>(const uint32_t (&x)[{8 * GROUP}], " if grouped
+            else f"bs_step<{k}, {m}, {cs[0]}>(const uint32_t (&x)[8], ")
+    first = cs[0] == 0
+    lines = [f"template <> __device__ __forceinline__ void {head}uint32_t (&y)[{8 * m}]) {{"]
     nx = 0
     for name, a, b in temps:
-        lines.append(f"  const uint32_t {name} = {a.replace('x', 'x[') + ']' if a[0] == 'x' else a} ^ "
-                     f"{b.replace('x', 'x[') + ']' if b[0] == 'x' else b};")
+        lines.append(f"  const uint32_t {name} = {_operand(a)} ^ {_operand(b)};")
         nx += 1
     for p, r in enumerate(red):
-        ops = [o.replace("x", "x[") + "]" if o[0] == "x" else o for o in sorted(r)]
+        ops = [_operand(o) for o in sorted(r)]
         if not ops:
-            if c == 0:
+            if first:
                 lines.append(f"  y[{p}] = 0u;")
             continue
         expr = " ^ ".join(ops)
         nx += len(ops) - 1
-        if c == 0:
+        if first:
             lines.append(f"  y[{p}] = {expr};")
         else:
             lines.append(f"  y[{p}] ^= {expr};")
@@ -162,30 +192,24 @@ def main():
     summary = []
     for k, m in SHAPES:
         rows = parity_rows(k, m)
-        total = 0
         out.append(f"// ---- RS({k}+{m}) parity rows: {rows}")
         flat = ", ".join(str(v) for r in rows for v in r)
         out.append(f"template <> struct BsNet<{k}, {m}> {{")
         out.append("  static constexpr bool kAvailable = true;")
         out.append(f"  static constexpr uint8_t kRows[{k * m}] = {{{flat}}};")
         out.append("};")
+        total = 0
         for c in range(k):
-            lines, nx = emit_step(k, m, c, rows)
+            lines, nx = emit(k, m, [c], False)
             out += lines
             total += nx
+        gtotal = 0
+        for c0 in range(0, k, GROUP):
+            lines, nx = emit(k, m, list(range(c0, min(k, c0 + GROUP))), True)
+            out += lines
+            gtotal += nx
         out.append("")
-        summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column")
-        if (k, m) in PREFIX_SHAPES:
-            pre = []
-            for r_rows in range(1, m + 1):
-                n_r = 0
-                for c in range(k):
-                    lines, nx = emit_step(k, m, c, rows, r_rows)
-                    out += lines
-                    n_r += nx
-                pre.append(f"{r_rows} rows {n_r}")
-            out.append("")
-            summary.append(f"RS({k}+{m}) prefix programs: " + ", ".join(pre))
+        summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column ({gtotal} in groups of {GROUP})")
     out.insert(3, "// " + "; ".join(summary))
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
