@@ -624,10 +624,6 @@ struct BsNet {
 };
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_step(const uint32_t (&x)[8], uint32_t (&y)[8 * M]);
-// Grouped programs: inputs C0..C0+N-1 (N <= 4) transposed into x[0 .. 8N), their
-// common pairs shared across the group (RS_BS_GROUP=4).
-template <int K, int M, int C0, int N>
-__device__ __forceinline__ void bs_gstep(const uint32_t (&x)[32], uint32_t (&y)[8 * M]);
 
 #include "rs_xor_networks.inc"
 
@@ -666,17 +662,13 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
 #define RS_BS_OCC 3
 #endif
 constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
-#ifndef RS_BS_GROUP
-#define RS_BS_GROUP 1
-#endif
-constexpr int kBsGroup = RS_BS_GROUP;  // 1: per-input programs; 4: grouped (bs_gstep)
-static_assert(kBsGroup == 1 || kBsGroup == 4, "rs_xor_networks.inc has groups of 4");
 
-// g: the transposed planes of the current group (kBsGroup = 4 only)
+// Programs shared over groups of 4 inputs (RS(10+4) 682 -> 573 XORs, RS(8+4) 564 ->
+// 473) were measured level on RS(8+4) and 2.5-3 points slower on RS(10+4)
+// (round 4, profiles/r04r_ab_bitsliced_groups.log): the per-input programs stay.
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off_a, uint32_t off_b,
-                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&g)[32],
-                                        uint32_t (&y)[8 * M]) {
+                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&y)[8 * M]) {
   if constexpr (C < K) {
     constexpr int slot = C % kBsWindow;
     uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
@@ -686,15 +678,8 @@ __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pit
       xb[slot] = bload16(din, off_b, (C + kBsWindow) * pitch);
     }
     transpose8(d);
-    if constexpr (kBsGroup == 1) {
-      bs_step<K, M, C>(d, y);
-    } else {
-      constexpr int gi = C % kBsGroup;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) g[gi * 8 + i] = d[i];
-      if constexpr (gi == kBsGroup - 1 || C == K - 1) bs_gstep<K, M, C - gi, gi + 1>(g, y);
-    }
-    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, g, y);
+    bs_step<K, M, C>(d, y);
+    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, y);
   }
 }
 
@@ -770,8 +755,7 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       xb[c] = bload16(din, fb.doff, c * pitch);
     }
     uint32_t y[8 * M];
-    uint32_t grp[32];
-    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, grp, y);
+    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
     const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
     const bool pa = nb != 0u && fa.live && fa.col == a.full_cols;  // this lane holds a partial column
     const bool pb = nb != 0u && fb.live && fb.col == a.full_cols;

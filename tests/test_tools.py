@@ -41,8 +41,9 @@ def _planes(col: np.ndarray):
 
 
 def test_xor_programs_compute_the_encode():
-    """Both forms of the generated XOR programs (per input, and shared over groups of
-    4 inputs) evaluated on random bitsliced columns give the oracle's parity bytes."""
+    """The generated XOR programs (per input, as emitted; and shared over groups of 4
+    inputs, the rejected form) evaluated on random bitsliced columns give the
+    oracle's parity bytes."""
     mod = _gen()
     rng = np.random.default_rng(5)
     for k, m in mod.SHAPES:
@@ -50,6 +51,7 @@ def test_xor_programs_compute_the_encode():
         shards = [bytearray(data[c].tobytes()) for c in range(k)] + [bytearray(32) for _ in range(m)]
         rs_oracle.encode(k, m, shards)
         want = [_planes(np.frombuffer(bytes(shards[k + r]), np.uint8)) for r in range(m)]
-        for y in mod.evaluate(k, m, [_planes(data[c]) for c in range(k)]):
+        for group in (1, 4):
+            y = mod.evaluate(k, m, [_planes(data[c]) for c in range(k)], group)
             got = [y[r * 8:(r + 1) * 8] for r in range(m)]
             assert got == want, (k, m)

@@ -82,10 +82,9 @@ def parity_rows(k: int, m: int):
 
 
 # ---- XOR programs ---------------------------------------------------------------
-# Group size of the grouped programs (bs_gstep): inputs C0..C0+G-1 transposed and live
-# together, their common pairs shared across the group (RS_BS_GROUP=4 in
-# rs_kernels.hip; the per-input bs_step programs are the default).
-GROUP = 4
+# Sharing pairs across groups of inputs (group size > 1: fewer XORs, more planes
+# live) was measured level or slower on the GPU (round 4,
+# profiles/r04r_ab_bitsliced_groups.log); program(..., cs) still takes a group.
 
 
 def group_rows(rows, m, cs):
@@ -132,38 +131,32 @@ def program(k, m, cs):
     return paar(group_rows(parity_rows(k, m), m, cs))
 
 
-def evaluate(k, m, planes_by_input):
-    """Reference evaluation of the per-input and the grouped programs (tests):
-    planes_by_input[c] = 8 plane words of input c; returns (per-input result,
-    grouped result), each 8m plane words."""
-    res = []
-    for size in (1, GROUP):
-        y = [0] * (8 * m)
-        for c0 in range(0, k, size):
-            cs = list(range(c0, min(k, c0 + size)))
-            temps, red = program(k, m, cs)
-            env = {f"x{ci * 8 + j}": planes_by_input[c][j] for ci, c in enumerate(cs) for j in range(8)}
-            for name, a, b in temps:
-                env[name] = env[a] ^ env[b]
-            for p, r in enumerate(red):
-                for o in r:
-                    y[p] ^= env[o]
-        res.append(y)
-    return res
+def evaluate(k, m, planes_by_input, group=1):
+    """Reference evaluation of the programs (tests): planes_by_input[c] = 8 plane
+    words of input c; returns the 8m parity plane words."""
+    y = [0] * (8 * m)
+    for c0 in range(0, k, group):
+        cs = list(range(c0, min(k, c0 + group)))
+        temps, red = program(k, m, cs)
+        env = {f"x{ci * 8 + j}": planes_by_input[c][j] for ci, c in enumerate(cs) for j in range(8)}
+        for name, a, b in temps:
+            env[name] = env[a] ^ env[b]
+        for p, r in enumerate(red):
+            for o in r:
+                y[p] ^= env[o]
+    return y
 
 
 def _operand(o):
     return f"x[{o[1:]}]" if o[0] == "x" else o
 
 
-def emit(k, m, cs, grouped):
-    """bs_step<k, m, c> (one input, cs = [c]) or bs_gstep<k, m, c0, n> (a group of n
-    inputs c0.. in the first 8n planes of x[8 * GROUP])."""
-    temps, red = program(k, m, cs)
-    head = (f"bs_gstep<{k}, {m}, {cs[0]}, {len(cs)}>(const uint32_t (&x)[{8 * GROUP}], " if grouped
-            else f"bs_step<{k}, {m}, {cs[0]}>(const uint32_t (&x)[8], ")
-    first = cs[0] == 0
-    lines = [f"template <> __device__ __forceinline__ void {head}uint32_t (&y)[{8 * m}]) {{"]
+def emit(k, m, c):
+    """bs_step<k, m, c>: input c's contribution to every parity plane."""
+    temps, red = program(k, m, [c])
+    first = c == 0
+    lines = [f"template <> __device__ __forceinline__ void bs_step<{k}, {m}, {c}>(const uint32_t (&x)[8], "
+             f"uint32_t (&y)[{8 * m}]) {{"]
     nx = 0
     for name, a, b in temps:
         lines.append(f"  const uint32_t {name} = {_operand(a)} ^ {_operand(b)};")
@@ -200,16 +193,11 @@ def main():
         out.append("};")
         total = 0
         for c in range(k):
-            lines, nx = emit(k, m, [c], False)
+            lines, nx = emit(k, m, c)
             out += lines
             total += nx
-        gtotal = 0
-        for c0 in range(0, k, GROUP):
-            lines, nx = emit(k, m, list(range(c0, min(k, c0 + GROUP))), True)
-            out += lines
-            gtotal += nx
         out.append("")
-        summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column ({gtotal} in groups of {GROUP})")
+        summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column")
     out.insert(3, "// " + "; ".join(summary))
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
