@@ -167,7 +167,9 @@ constexpr int out_cpol() {
 #endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
-  return RS_WAVE_ROWS_CPOL ? out_cpol<K, NR>() : out_cpol<K, E>();
+  return RS_WAVE_ROWS_CPOL == 2 ? (NR == 1 ? out_cpol<K, 1>() : kCpolNt)
+         : RS_WAVE_ROWS_CPOL    ? out_cpol<K, NR>()
+                                : out_cpol<K, E>();
 }
 
 // 16-B store at base + off, or nothing at all when !live: a raw buffer

@@ -88,6 +88,9 @@ WORKLOADS = {
     "rs104_64K_recmixh_out": (10, 4, 6554, 16384, "recmixh_out"),
     "rs84_64K_recmix_out": (8, 4, 8192, 16384, "recmix_out"),
     "rs84_64K_recmixh_out": (8, 4, 8192, 16384, "recmixh_out"),
+    # mixed 1..m erasures: no intact stripe (what the intact stripes' holes cost)
+    "rs104_64K_recmix1_out": (10, 4, 6554, 16384, "recmix1_out"),
+    "rs84_64K_recmix1_out": (8, 4, 8192, 16384, "recmix1_out"),
 }
 
 
@@ -180,6 +183,11 @@ def main():
             for j in rng.choice(t, size=int(ne), replace=False):
                 mix[i] &= ~np.uint32(1 << int(j))
         mixd = torch.from_numpy(mix.view(np.int32)).cuda()
+        mix1 = np.full(N, (1 << t) - 1, np.uint32)
+        for i, ne in enumerate(rng.integers(1, m + 1, N)):
+            for j in rng.choice(t, size=int(ne), replace=False):
+                mix1[i] &= ~np.uint32(1 << int(j))
+        mix1d = torch.from_numpy(mix1.view(np.int32)).cuda()
         m45 = torch.full((N,), 0b001111, dtype=torch.int32, device="cuda")
         m01 = torch.full((N,), ((1 << t) - 1) & ~3, dtype=torch.int32, device="cuda")
         m04 = torch.full((N,), ((1 << t) - 1) & ~0b10001, dtype=torch.int32, device="cuda")
@@ -188,8 +196,8 @@ def main():
         rows = bounded_rows[mode] if name.endswith("+dense") else m
         outs = [torch.empty((N, rows, P), dtype=torch.uint8, device="cuda") for _ in range(nb)] if "out" in mode else []
         alg = alg_bytes(name.split("+")[0])  # "+<pad>" / "+dense" variants move the same bytes
-        if mode in ("recmix_out", "recmixh_out"):  # K reads + one write per missing shard, complete stripes none
-            nmiss = np.array([bin(int(x) ^ ((1 << t) - 1)).count("1") for x in mix])
+        if mode in ("recmix_out", "recmixh_out", "recmix1_out"):  # K reads + one write per missing shard
+            nmiss = np.array([bin(int(x) ^ ((1 << t) - 1)).count("1") for x in (mix1 if mode == "recmix1_out" else mix)])
             alg = int(S * (k * np.count_nonzero(nmiss) + nmiss.sum()))
         bad = torch.empty(N, dtype=torch.int32, device="cuda")
 
@@ -233,6 +241,8 @@ def main():
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=masks_np[i % nb])
             elif mode == "recmix_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=mixd)
+            elif mode == "recmix1_out":
+                eng.reconstruct_out(d, p, outs[i % nb], S, N, masks_dev=mix1d)
             elif mode == "recmixh_out":
                 eng.reconstruct_out(d, p, outs[i % nb], S, N, present_masks=mix)
             elif mode == "encu_out":
