@@ -153,17 +153,24 @@ constexpr int out_cpol() {
 // Per-stripe kernels sized for E > 2 outputs (device masks without a caller bound:
 // E = M) compute only the rows a task's stripe(s) miss and then pick, in a
 // wave-uniform branch, the store sequence of that row count: 1 or 2 rows store with
-// the bounded E = 1 / 2 kernels' policy (out_cpol<K, 1 or 2>) and issue no dropped
-// stores for the other rows, more rows store E rows with out_cpol<K, E> (round 4).
+// their own policy (path_cpol below) and issue no dropped stores for the other rows,
+// more rows store E rows with out_cpol<K, E> (round 4).
 // Every store instruction has one policy for all its lanes and every 128-B output
 // line one writer instruction.  RS_WAVE_ROWS=0 builds the single-path kernels (A/B).
 #ifndef RS_WAVE_ROWS
 #define RS_WAVE_ROWS 1
 #endif
-// RS_WAVE_ROWS_CPOL=0: the 1- and 2-row paths store with out_cpol<K, E> too (A/B of
-// the dropped stores alone).
+// Store policy of those paths (RS_WAVE_ROWS_CPOL):
+//   2 (default): the 1-row path with out_cpol<K, 1> (SC1 for K >= 8), the 2-row path
+//     NT.  Interleaved A/B against 1 (profiles/r04t_ab_p2nt.log, RS(10+4) 64 KiB,
+//     >= 100 ms per point, 3 rounds): unbounded 2-erasure 69.5 -> 70.5 % (median),
+//     mixed 0..4 erasures 59.5-59.8 -> 60.6 % (host masks 56.9-57.0 -> 57.6-57.7 %),
+//     mixed 1..4 65.3-65.8 -> 66.7-66.9 %; the bounded E = 2 kernel keeps NT|SC1.
+//   1: out_cpol<K, 1 or 2>, the bounded kernels' policies.
+//   0: out_cpol<K, E> for every path (all NT: 1-erasure 4-7 points slower,
+//     profiles/r04s_ab_em_cpol_mix.log).
 #ifndef RS_WAVE_ROWS_CPOL
-#define RS_WAVE_ROWS_CPOL 1
+#define RS_WAVE_ROWS_CPOL 2
 #endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
