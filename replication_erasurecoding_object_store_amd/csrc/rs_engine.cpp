@@ -113,12 +113,6 @@ using rs::Matrix;
 using rs::PinnedBuf;
 using rs::round_up;
 
-// Default workgroups (256 threads) per CU for the batched kernels, measured with
-// tools/ab_bench.py on MI355X (profiles/r01_ab_occupancy.log): the streaming
-// pattern wants few waves (tools/hbm_probe2.hip: 1-2 WG/CU beat higher occupancy)
-// until the per-byte VALU work (K*E lookups) needs more waves to hide latency.
-int default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6 : 2; }
-
 // ---- plan construction -----------------------------------------------------
 // 3-chunk v_perm tables for coefficient f (see rs_kernels.hip):
 //   A[v] = f*v (v<8), B[v] = f*(v<<3) (v<8), C[v] = f*(v<<6) (v<4).
@@ -606,9 +600,9 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
       a.full_cols = static_cast<uint32_t>(s_eff / 16);
     }
   }
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e_out);
-  const char* name =
-      rs::launch_apply(a, e_out, per_stripe, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
+  // 0: each kernel's own default (rs::launch_apply)
+  const uint32_t bpc = e->blocks_per_cu > 0 ? static_cast<uint32_t>(e->blocks_per_cu) : 0u;
+  const char* name = rs::launch_apply(a, e_out, per_stripe, bpc, static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
   e->shared->note(s, name);
   RS_HIP(hipGetLastError());
@@ -617,7 +611,7 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
 
 int launch_verify_args(Engine* e, rs::KernelArgs& a, hipStream_t s) {
   a.plans = static_cast<const uint8_t*>(e->d_enc_plan.p);
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, e->m);
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : static_cast<int>(rs::default_blocks_per_cu(e->k, e->m));
   const char* name =
       rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
@@ -1181,7 +1175,7 @@ int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uin
   a.present_masks = masks_dev;
   a.shard_ptrs = shard_ptrs_dev;
   if (!(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : default_blocks_per_cu(e->k, bound);
+  const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : static_cast<int>(rs::default_blocks_per_cu(e->k, bound));
   const char* name = rs::launch_apply_ptrs(a, bound, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_NOT_SUPPORTED;
   e->shared->note(s, name);

@@ -1434,6 +1434,20 @@ static const void* pick_flat_ps(int k, int m, int e, const char** name) {
   return nullptr;
 }
 
+// Default workgroups per CU, measured with tools/ab_bench.py on MI355X
+// (profiles/r01_ab_occupancy.log, r04p_bpc_k8_k10.log): the streaming pattern wants
+// few waves (tools/hbm_probe2.hip: 1-2 WG/CU beat higher occupancy) until the
+// per-byte VALU work (K*E lookups) needs more waves to hide latency.
+uint32_t default_blocks_per_cu(int k, int e) { return k * e >= 24 ? 6u : 2u; }
+
+// The stripe-aligned per-stripe kernels sized for E > 2 (apply_kernel<K, M, M,
+// true>: occupancy 3) run as many short workgroups instead of a grid-stride loop over
+// 6 per CU (round 4, profiles/r04x_bpc_em.log, >= 100 ms per point): RS(8+4) 64 KiB
+// unbounded 1-erasure 75.1 -> 80.1 %, 2-erasure 71.4 -> 78.7 %, 4-erasure 69.7 ->
+// 70.8 %, mixed 0..4 66.0 -> 70.4 %; RS(10+4) at S = 6144 72.4 -> 75.8 %, 68.9 ->
+// 75.0 %, 67.8 -> 68.5 %.  The flat and bitsliced kernels do not gain (r04v, r04p).
+constexpr uint32_t kEmBlocksPerCu = 64;
+
 // Grid for `waves` wave-tasks: 4 waves per workgroup, at most blocks_per_cu
 // workgroups per CU (the kernels grid-stride over the rest).
 static dim3 grid_for(uint64_t waves, uint32_t blocks_per_cu, uint32_t cu_count) {
@@ -1460,7 +1474,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (fn) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 127u) / 128u;
       if (waves == 0) return name;
-      if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+      const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
+      if (hipLaunchKernel(fn, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
         return nullptr;
       return name;
     }
@@ -1471,7 +1486,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
       if (waves == 0) return name;
-      if (hipLaunchKernel(ff, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+      const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
+      if (hipLaunchKernel(ff, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
         return nullptr;
       return name;
     }
@@ -1484,7 +1500,9 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   }
   const uint64_t waves = static_cast<uint64_t>(a.n_stripes) * a.blocks_per_stripe;
   if (waves == 0) return name;
-  if (hipLaunchKernel(fn, grid_for(waves, blocks_per_cu, cu_count), dim3(256), args, 0, s) != hipSuccess)
+  uint32_t bpc = blocks_per_cu;
+  if (!bpc) bpc = (per_stripe && !generic && e > 2) ? kEmBlocksPerCu : default_blocks_per_cu(a.k, e);
+  if (hipLaunchKernel(fn, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
     return nullptr;
   return name;
 }

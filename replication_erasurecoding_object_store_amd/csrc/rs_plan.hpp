@@ -109,11 +109,15 @@ struct KernelArgs {
 // bitsliced kernel only if they equal its runtime encode matrix.
 const uint8_t* bitsliced_encode_rows(int k, int m);
 
+// Default workgroups (256 threads) per CU of the batched kernels with k inputs and
+// e outputs per stripe (blocks_per_cu = 0 in the launch helpers below).
+uint32_t default_blocks_per_cu(int k, int e);
+
 // Launch helpers implemented in rs_kernels.hip (host code; needs hip_runtime.h first).
 // e = outputs per stripe to compute (<= m): for per-stripe plans the launch's erasure
 // bound (stripes missing more are skipped and flagged, status bit 1).  Returns the
 // main kernel's name, or nullptr if the launch failed.  Any shard_len up to
-// 0xFFFFFFF0 (column windows).
+// 0xFFFFFFF0 (column windows).  blocks_per_cu = 0: the chosen kernel's default.
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);

@@ -52,6 +52,10 @@ WORKLOADS = {
     "rs42_4K_rec45u_out": (4, 2, 1024, 65536, "rec45u_out"),
     "rs84_64K_rec2p_out": (8, 4, 8192, 16384, "rec2p_out"),
     "rs63_64K_enc": (6, 3, 10923, 16384, "enc"),
+    # RS(6+3) per-stripe without a bound on whole-task shards (stripe-aligned E = M kernel)
+    "rs63_S8192_rec1p_out": (6, 3, 8192, 16384, "rec1p_out"),
+    "rs63_S8192_rec2p_out": (6, 3, 8192, 16384, "rec2p_out"),
+    "rs63_S8192_rec3p_out": (6, 3, 8192, 16384, "rec4p_out"),
     "rs42_64K_ver": (4, 2, 16384, 16384, "ver"),
     "rs104_64K_ver": (10, 4, 6554, 16384, "ver"),
     # tail-free shard lengths next to the real 64 KiB ones (S % 16 == 0)
