@@ -633,6 +633,14 @@ struct BsNet {
 };
 template <int K, int M, int C>
 __device__ __forceinline__ void bs_step(const uint32_t (&x)[8], uint32_t (&y)[8 * M]);
+// Pair programs of the 1 KiB-task encode (encode_bs16_kernel): shapes whose encode
+// matrix satisfies C[r ^ 1][c] = C[r][c ^ 1] (tools/gen_xor_networks.py).
+template <int K, int M>
+struct Bs16Net {
+  static constexpr bool kAvailable = false;
+};
+template <int K, int M, int P>
+__device__ __forceinline__ void bs16_step(const uint32_t (&x)[8], uint32_t (&ya)[4 * M], uint32_t (&yb)[4 * M]);
 
 #include "rs_xor_networks.inc"
 
@@ -784,6 +792,113 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       const uint32_t off = pb ? fb.poff : fa.poff;
 #pragma unroll
       for (int r = 0; r < M; ++r) store_part_rsrc(pout, off, r * pitch, pa || pb, part[r], nb);
+    }
+    c0 += step_c;
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bitsliced encode over 1 KiB-wide tasks (64 columns, 16 B of every shard per lane).
+//
+// Bitslicing needs 32 B per lane to fill 8 plane dwords; the 2 KiB rows of
+// encode_bitsliced_kernel give each lane two columns, and that task shape streams
+// about 3 points below 1 KiB rows at RS(8+4) (compute-free probe).  Here a
+// lane fills its planes from two INPUTS instead: 16 B of input c (even) in dwords
+// 0-3 and of input c ^ 1 in dwords 4-7, so after transpose8 plane j holds bit j of
+// input c in the low nibble of each byte and of input c ^ 1 in the high nibble.
+// The RS(8+4) and RS(10+4) encode matrices satisfy C[r ^ 1][c] = C[r][c ^ 1], so for
+// an even row r, A = C[r][c], B = C[r][c ^ 1]: A * P + B * nibswap(P) is row r of the
+// pair in the low nibbles and row r ^ 1 in the high nibbles.  The generated pair
+// program accumulates A * P (ya) and B * P (yb); nibswap is linear, so one
+// ya ^ nibswap(yb) per output plane and one transpose8 per packed row give 16 B of
+// rows r and r ^ 1 (dwords 0-3 and 4-7).  XORs per 32 B of every shard: RS(8+4) 532
+// (pair programs share the A / B terms) vs 564; the transposes: K / 2 + M / 2 per 16 B,
+// the same count per byte as the 2 KiB kernel, plus 4 VALU ops per packed plane.
+// Same flat column space, straddling and tail handling as encode_bitsliced_kernel.
+#ifndef RS_BS16
+#define RS_BS16 0
+#endif
+#ifndef RS_BS16_WINDOW
+#define RS_BS16_WINDOW 5
+#endif
+constexpr int kBs16Window = RS_BS16_WINDOW;  // input pairs with loads in flight
+
+template <int K, int M, int P>
+__device__ __forceinline__ void bs16_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off,
+                                          u32x4 (&xa)[kBs16Window], u32x4 (&xb)[kBs16Window],
+                                          uint32_t (&ya)[4 * M], uint32_t (&yb)[4 * M]) {
+  if constexpr (P < K / 2) {
+    constexpr int slot = P % kBs16Window;
+    uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
+                     xb[slot][0], xb[slot][1], xb[slot][2], xb[slot][3]};
+    if constexpr (P + kBs16Window < K / 2) {
+      xa[slot] = bload16(din, off, (2 * (P + kBs16Window)) * pitch);
+      xb[slot] = bload16(din, off, (2 * (P + kBs16Window) + 1) * pitch);
+    }
+    transpose8(d);
+    bs16_step<K, M, P>(d, ya, yb);
+    bs16_fold<K, M, P + 1>(din, pitch, off, xa, xb, ya, yb);
+  }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(256, RS_BS_OCC) void encode_bs16_kernel(const KernelArgs a) {
+  static_assert(K % 2 == 0 && M % 2 == 0, "pair programs need even K and M");
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_index();
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
+  const uint32_t cstride = (cols + 7u) & ~7u;
+  const uint64_t total = static_cast<uint64_t>(a.n_stripes) * cstride;
+  if (static_cast<uint64_t>(wave) * 64u >= total) return;
+  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
+  const uint64_t g0 = static_cast<uint64_t>(wave) * 64u;
+  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
+  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
+  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 64u;
+  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
+  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  while (s0 < a.n_stripes) {
+    const FlatCol f = flat_col(a, s0, c0 + lane, cstride, cols);
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pout = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                        0x7FFFFFFF, 0x00020000);
+    u32x4 xa[kBs16Window], xb[kBs16Window];
+#pragma unroll
+    for (int p = 0; p < kBs16Window && p < K / 2; ++p) {
+      xa[p] = bload16(din, f.doff, (2 * p) * pitch);
+      xb[p] = bload16(din, f.doff, (2 * p + 1) * pitch);
+    }
+    uint32_t ya[4 * M], yb[4 * M];
+    bs16_fold<K, M, 0>(din, pitch, f.doff, xa, xb, ya, yb);
+    const bool sf = f.live && f.col < a.full_cols;
+    const bool pf = nb != 0u && f.live && f.col == a.full_cols;  // this lane holds a partial column
+    u32x4 part[M];
+#pragma unroll
+    for (int q = 0; q < M / 2; ++q) {
+      uint32_t d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t b = yb[q * 8 + i];
+        d[i] = ya[q * 8 + i] ^ ((b >> 4) & 0x0F0F0F0Fu) ^ ((b << 4) & 0xF0F0F0F0u);
+      }
+      transpose8(d);
+      const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
+      __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sf ? f.poff : kDropOffset, (2 * q) * pitch, 2 /* nt */);
+      __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sf ? f.poff : kDropOffset, (2 * q + 1) * pitch, 2 /* nt */);
+      part[2 * q] = lo;
+      part[2 * q + 1] = hi;
+    }
+    if (nb != 0u && __builtin_amdgcn_ballot_w64(pf) != 0u) {  // wave-uniform
+#pragma unroll
+      for (int r = 0; r < M; ++r) store_part_rsrc(pout, f.poff, r * pitch, pf, part[r], nb);
     }
     c0 += step_c;
     s0 += step_s;
@@ -1404,7 +1519,28 @@ const uint8_t* bitsliced_encode_rows(int k, int m) {
   return nullptr;
 }
 
-static const void* pick_bitsliced(int k, int m, const char** name) {
+template <int K, int M>
+static const void* bs16_fn() {
+  if constexpr (Bs16Net<K, M>::kAvailable) return reinterpret_cast<const void*>(&encode_bs16_kernel<K, M>);
+  return nullptr;
+}
+
+// Bitsliced encode kernel of (k, m) and its task width in columns (128: 2 KiB rows,
+// 64: the 1 KiB-task pair kernel).  RS_BS16: 0 = 2 KiB kernel only, 1 = pair kernel
+// for RS(8+4), 2 = pair kernel for RS(8+4) and RS(10+4).
+static const void* pick_bitsliced(int k, int m, const char** name, uint32_t* task_cols) {
+  *task_cols = 128u;
+#define RS_BS16K(KK, MM)                                          \
+  if (k == KK && m == MM) {                                       \
+    if (const void* f = bs16_fn<KK, MM>()) {                      \
+      *name = "encode_bs16_kernel<" #KK "," #MM ">";              \
+      *task_cols = 64u;                                           \
+      return f;                                                   \
+    }                                                             \
+  }
+  if (RS_BS16 >= 1) RS_BS16K(8, 4)
+  if (RS_BS16 >= 2) RS_BS16K(10, 4)
+#undef RS_BS16K
 #define RS_BS(KK, MM)                                   \
   if (k == KK && m == MM) {                             \
     *name = "encode_bitsliced_kernel<" #KK "," #MM ">"; \
@@ -1470,9 +1606,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     // flat 128-column tasks straddle at most two stripes (cols >= 128) and address
     // with 32-bit offsets off one stripe base per region
     const bool flat_ok = cols >= 128u && a.data_sp + span < (1ull << 31) && a.parity_sp + span < (1ull << 31);
-    const void* fn = flat_ok ? pick_bitsliced(a.k, a.m, &name) : nullptr;
+    uint32_t tc = 128u;
+    const void* fn = flat_ok ? pick_bitsliced(a.k, a.m, &name, &tc) : nullptr;
     if (fn) {
-      const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 127u) / 128u;
+      const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + tc - 1u) / tc;
       if (waves == 0) return name;
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
       if (hipLaunchKernel(fn, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)

@@ -26,6 +26,7 @@ import os
 from collections import Counter
 
 SHAPES = [(4, 2), (8, 4), (10, 4), (6, 3)]
+PAIR_SHAPES = [(8, 4), (10, 4)]  # 1 KiB-task pair programs (encode_bs16_kernel)
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "replication_erasurecoding_object_store_amd", "csrc", "rs_xor_networks.inc")
 
@@ -178,6 +179,86 @@ def emit(k, m, c):
     return lines, nx
 
 
+# ---- 1 KiB-task programs on input pairs ----------------------------------------
+# The encode matrices of RS(8+4) and RS(10+4) satisfy C[r ^ 1][c] = C[r][c ^ 1].  A
+# lane holding 16 B of inputs c (even) and c ^ 1 transposes them together: plane j,
+# low nibble of every byte = bit j of 4 bytes of input c, high nibble = of input c ^ 1.
+# For an even row r, A = C[r][c] and B = C[r][c ^ 1]:  A * P + B * nibswap(P) carries
+# row r's terms of both inputs in the low nibbles and row r ^ 1's in the high nibbles.
+# The kernel accumulates A * P (ya) and B * P (yb) and combines ya ^ nibswap(yb) once
+# per column, so one program over M / 2 packed rows serves all M rows.
+
+
+def pair_symmetric(k: int, m: int) -> bool:
+    rows = parity_rows(k, m)
+    return k % 2 == 0 and m % 2 == 0 and all(
+        rows[r ^ 1][c] == rows[r][c ^ 1] for r in range(m) for c in range(k))
+
+
+def pair_program(k, m, p):
+    """Program of input pair (2p, 2p+1): output planes 0..4m-1 = ya (A terms of the
+    packed rows 0, 2, ..), 4m..8m-1 = yb (B terms)."""
+    rows = parity_rows(k, m)
+    coefs = [rows[r][2 * p] for r in range(0, m, 2)] + [rows[r][2 * p + 1] for r in range(0, m, 2)]
+    subsets = []
+    for f in coefs:
+        for i in range(8):
+            subsets.append(frozenset(j for j in range(8) if (mul(f, 1 << j) >> i) & 1))
+    return paar(subsets)
+
+
+def evaluate_pairs(k, m, planes_by_input):
+    """Reference evaluation of the pair programs on 32-bit planes whose low 16 bits
+    hold the input of the pair's even member and high 16 bits its odd member (the
+    kernel's nibbles, spread for the test): returns the 8m parity planes, row r's
+    plane i in the low 16 bits of y[(r // 2) * 8 + i] when r is even, high when odd."""
+    half = 4 * m
+    ya, yb = [0] * half, [0] * half
+    for p in range(k // 2):
+        P = [(planes_by_input[2 * p][j] & 0xFFFF) | ((planes_by_input[2 * p + 1][j] & 0xFFFF) << 16)
+             for j in range(8)]
+        temps, red = pair_program(k, m, p)
+        env = {f"x{j}": P[j] for j in range(8)}
+        for name, a, b in temps:
+            env[name] = env[a] ^ env[b]
+        for q, r in enumerate(red):
+            for o in r:
+                if q < half:
+                    ya[q] ^= env[o]
+                else:
+                    yb[q - half] ^= env[o]
+    swap = [((v >> 16) | (v << 16)) & 0xFFFFFFFF for v in yb]
+    return [a ^ b for a, b in zip(ya, swap)]
+
+
+def emit_pair(k, m, p):
+    """bs16_step<k, m, p>: input pair p's contribution to ya / yb."""
+    temps, red = pair_program(k, m, p)
+    half = 4 * m
+    first = p == 0
+    lines = [f"template <> __device__ __forceinline__ void bs16_step<{k}, {m}, {p}>(const uint32_t (&x)[8], "
+             f"uint32_t (&ya)[{half}], uint32_t (&yb)[{half}]) {{"]
+    nx = 0
+    for name, a, b in temps:
+        lines.append(f"  const uint32_t {name} = {_operand(a)} ^ {_operand(b)};")
+        nx += 1
+    for q, r in enumerate(red):
+        dst = f"ya[{q}]" if q < half else f"yb[{q - half}]"
+        ops = [_operand(o) for o in sorted(r)]
+        if not ops:
+            if first:
+                lines.append(f"  {dst} = 0u;")
+            continue
+        nx += len(ops) - 1
+        if first:
+            lines.append(f"  {dst} = {' ^ '.join(ops)};")
+        else:
+            lines.append(f"  {dst} ^= {' ^ '.join(ops)};")
+            nx += 1
+    lines.append("}")
+    return lines, nx
+
+
 def main():
     out = ["// rs_xor_networks.inc -- GENERATED by tools/gen_xor_networks.py; do not edit.",
            "// Bitsliced encode XOR programs for the fixed RS(K, M) encode matrices",
@@ -198,6 +279,18 @@ def main():
             total += nx
         out.append("")
         summary.append(f"RS({k}+{m}): {total} v_xor_b32 per 32-byte column")
+        if (k, m) in PAIR_SHAPES:
+            assert pair_symmetric(k, m), (k, m)
+            out.append(f"template <> struct Bs16Net<{k}, {m}> {{")
+            out.append("  static constexpr bool kAvailable = true;")
+            out.append("};")
+            total = 0
+            for p in range(k // 2):
+                lines, nx = emit_pair(k, m, p)
+                out += lines
+                total += nx
+            out.append("")
+            summary.append(f"RS({k}+{m}) pairs: {total} v_xor_b32 per 16-byte column")
     out.insert(3, "// " + "; ".join(summary))
     with open(OUT, "w") as f:
         f.write("\n".join(out) + "\n")
