@@ -55,3 +55,24 @@ def test_xor_programs_compute_the_encode():
             y = mod.evaluate(k, m, [_planes(data[c]) for c in range(k)], group)
             got = [y[r * 8:(r + 1) * 8] for r in range(m)]
             assert got == want, (k, m)
+
+
+def test_pair_programs_compute_the_encode():
+    """The 1 KiB-task pair programs (encode_bs16_kernel): the shapes they are emitted
+    for satisfy C[r ^ 1][c] = C[r][c ^ 1], and ya ^ swap(yb) over 16-byte columns (one
+    input of each pair per half-word) gives the oracle's parity bytes of both rows of
+    every packed row."""
+    mod = _gen()
+    rng = np.random.default_rng(6)
+    for k, m in mod.PAIR_SHAPES:
+        assert mod.pair_symmetric(k, m), (k, m)
+        data = rng.integers(0, 256, (k, 16), dtype=np.uint8)
+        shards = [bytearray(data[c].tobytes()) for c in range(k)] + [bytearray(16) for _ in range(m)]
+        rs_oracle.encode(k, m, shards)
+        planes = [[sum(((int(data[c][b]) >> j) & 1) << b for b in range(16)) for j in range(8)] for c in range(k)]
+        y = mod.evaluate_pairs(k, m, planes)
+        for r in range(m):
+            want = _planes(np.concatenate([np.frombuffer(bytes(shards[k + r]), np.uint8), np.zeros(16, np.uint8)]))
+            got = [(v >> (16 * (r & 1))) & 0xFFFF for v in y[(r // 2) * 8:(r // 2) * 8 + 8]]
+            assert got == want, (k, m, r)
+    assert not mod.pair_symmetric(6, 3) and not mod.pair_symmetric(4, 3)
