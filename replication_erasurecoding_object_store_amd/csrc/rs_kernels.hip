@@ -820,11 +820,17 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
 // (pair programs share the A / B terms) vs 564; the transposes: K / 2 + M / 2 per 16 B,
 // the same count per byte as the 2 KiB kernel, plus 4 VALU ops per packed plane.
 // Same flat column space, straddling and tail handling as encode_bitsliced_kernel.
+// Interleaved A/B against the 2 KiB kernel (round 4, profiles/r04zb_ab_bs16.log, 64 KiB
+// objects, >= 100 ms per point, 3 rounds): RS(8+4) 69.4-70.4 -> 72.0-73.1 % of 8 TB/s,
+// RS(10+4) 66.6-67.6 -> 67.5-68.2 %; a window of 3 pairs and 8 workgroups per CU level.
 #ifndef RS_BS16
-#define RS_BS16 0
+#define RS_BS16 2
 #endif
 #ifndef RS_BS16_WINDOW
 #define RS_BS16_WINDOW 5
+#endif
+#ifndef RS_BS16_OCC
+#define RS_BS16_OCC 3
 #endif
 constexpr int kBs16Window = RS_BS16_WINDOW;  // input pairs with loads in flight
 
@@ -847,7 +853,7 @@ __device__ __forceinline__ void bs16_fold(__amdgpu_buffer_rsrc_t din, uint32_t p
 }
 
 template <int K, int M>
-__global__ __launch_bounds__(256, RS_BS_OCC) void encode_bs16_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const KernelArgs a) {
   static_assert(K % 2 == 0 && M % 2 == 0, "pair programs need even K and M");
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
@@ -1527,7 +1533,7 @@ static const void* bs16_fn() {
 
 // Bitsliced encode kernel of (k, m) and its task width in columns (128: 2 KiB rows,
 // 64: the 1 KiB-task pair kernel).  RS_BS16: 0 = 2 KiB kernel only, 1 = pair kernel
-// for RS(8+4), 2 = pair kernel for RS(8+4) and RS(10+4).
+// for RS(8+4), 2 (default) = pair kernel for RS(8+4) and RS(10+4).
 static const void* pick_bitsliced(int k, int m, const char** name, uint32_t* task_cols) {
   *task_cols = 128u;
 #define RS_BS16K(KK, MM)                                          \
