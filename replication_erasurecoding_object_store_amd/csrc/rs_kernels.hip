@@ -1645,8 +1645,19 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   if (waves == 0) return name;
   uint32_t bpc = blocks_per_cu;
   if (!bpc) bpc = (per_stripe && !generic && e > 2) ? kEmBlocksPerCu : default_blocks_per_cu(a.k, e);
-  if (hipLaunchKernel(fn, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
-    return nullptr;
+  dim3 grid = grid_for(waves, bpc, cu_count);
+  if (!blocks_per_cu && !generic && !(per_stripe && e > 2)) {
+    // The specialised E <= 2 and encode kernels run one task per wave: a grid over
+    // every task instead of a grid-stride loop over 2 workgroups per CU (round 4,
+    // profiles/r04zf_bpc_bounded.log, >= 100 ms per point, 3 rounds): RS(4+2) 4 KiB
+    // per-stripe 2-erasure 74.5 -> 78.8 % of 8 TB/s, encode 76.8 -> 79.1 %, uniform
+    // 2-erasure 72.6 -> 76.5 %; 64 KiB 2-erasure 74.8 -> 79.8 %, encode 77.1 -> 80.8 %;
+    // RS(8+4) 1-/2-erasure 77.6 / 75.2 -> 79.8 / 78.2 %; RS(4+2) 1-erasure 77.2 ->
+    // 76.4 %.  Partial grids (32 or 64 per CU, still looping) were slower than both.
+    const uint64_t need = (waves + 3) / 4;
+    grid = dim3(static_cast<uint32_t>(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
+  }
+  if (hipLaunchKernel(fn, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
 }
 
