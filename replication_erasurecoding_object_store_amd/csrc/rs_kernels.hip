@@ -1599,6 +1599,13 @@ static dim3 grid_for(uint64_t waves, uint32_t blocks_per_cu, uint32_t cu_count) 
   return dim3(static_cast<uint32_t>(g > 0 ? g : 1));
 }
 
+// Grid with one wave per task (4 waves per workgroup), capped at 2^31 - 1 workgroups
+// (the kernels grid-stride over anything beyond).
+static dim3 full_grid(uint64_t waves) {
+  const uint64_t need = (waves + 3) / 4;
+  return dim3(static_cast<uint32_t>(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
+}
+
 // One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
 // the dropped-store descriptors cover 2 GiB from the shard base).
 static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
@@ -1617,9 +1624,11 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (fn) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + tc - 1u) / tc;
       if (waves == 0) return name;
-      const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
-      if (hipLaunchKernel(fn, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
-        return nullptr;
+      // default: one task per wave (profiles/r04zi_bpc_flat.log, >= 100 ms per point:
+      // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
+      // against a grid-stride loop over 6 workgroups per CU)
+      const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
+      if (hipLaunchKernel(fn, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
       return name;
     }
   }
@@ -1629,9 +1638,11 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
       if (waves == 0) return name;
+      // E <= 2: one task per wave (r04zi: RS(10+4) 64 KiB 1-/2-erasure +0.9 / +2.5
+      // points); E = M keeps its grid-stride loop (a full grid lost 10 points there)
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
-      if (hipLaunchKernel(ff, grid_for(waves, bpc, cu_count), dim3(256), args, 0, s) != hipSuccess)
-        return nullptr;
+      const dim3 grid = (!blocks_per_cu && e <= 2) ? full_grid(waves) : grid_for(waves, bpc, cu_count);
+      if (hipLaunchKernel(ff, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
       return name;
     }
   }
@@ -1654,8 +1665,7 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     // 2-erasure 72.6 -> 76.5 %; 64 KiB 2-erasure 74.8 -> 79.8 %, encode 77.1 -> 80.8 %;
     // RS(8+4) 1-/2-erasure 77.6 / 75.2 -> 79.8 / 78.2 %; RS(4+2) 1-erasure 77.2 ->
     // 76.4 %.  Partial grids (32 or 64 per CU, still looping) were slower than both.
-    const uint64_t need = (waves + 3) / 4;
-    grid = dim3(static_cast<uint32_t>(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
+    grid = full_grid(waves);
   }
   if (hipLaunchKernel(fn, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
