@@ -50,7 +50,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: "6.29 TB/s measured (float4 copy, 79%)"
 # Compute-free ceilings of the RS access patterns on MI355X (tools/pattern_probe.hip,
 # profiles/r02_pattern_probe.log): the best the split layout's traffic reaches with no
-# arithmetic at all, fraction of 8 TB/s.
+# arithmetic at all, fraction of 8 TB/s.  The probes grid-strided over a few workgroups
+# per CU; since round 4 the kernels launch one wave per task and can exceed these
+# figures (profiles/r04zi_bpc_flat.log).
 PATTERN_CEILING = {(4, 2, 1024): 0.797, (4, 2, 16384): 0.774, (8, 4, 8192): 0.778, (10, 4, 6554): 0.712}
 
 
