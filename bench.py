@@ -75,7 +75,94 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--json-out", default="")
+    p.add_argument("--dry-run", action="store_true",
+                   help="no GPU: run the rank launcher and the control collectives on gloo only and print a "
+                        "line with n_gpus (tests/test_bench_launch.py)")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`--gpus N > 1` with no torchrun environment: one fresh process per GPU.
+
+    The parent touches no GPU (no torch import at all): it starts N children of this
+    same command with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set,
+    as torch.distributed.run would, waits for all of them and returns a non-zero
+    code if any fails -- terminating the others, which would otherwise wait forever
+    at the next barrier.  Rank 0 prints the JSON line (its stdout is this process's).
+    The reference likewise runs one codec per process (cmd/api/main.go:206)."""
+    import signal
+    import subprocess
+
+    procs = []
+
+    def stop(live):
+        for q in live:
+            try:
+                os.killpg(q.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+
+    def on_signal(signum, _frame):  # a time limit on this launcher reaches the ranks too
+        stop([p for p in procs if p.poll() is None])
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
+    port = str(_free_port())
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                stop(live)
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+def dry_run(args):
+    """GPU-free rehearsal of the N-rank path: the same env, gloo control
+    collectives (barrier, max over ranks, AND) and the line's n_gpus field."""
+    from replication_erasurecoding_object_store_amd import dist as rdist
+
+    rank, _, world = rdist.world()
+    if os.environ.get("RSGPU_BENCH_DRY_FAIL_RANK") == str(rank):
+        sys.exit(3)  # tests/test_bench_launch.py: a rank that dies before the rendezvous
+    rdist.init("gloo")
+    rdist.barrier()
+    t0 = time.perf_counter()
+    rdist.barrier()
+    dt = rdist.max_over_ranks(time.perf_counter() - t0 + 1e-3 * rank)
+    ok = rdist.all_true(True)
+    pids = rdist.distinct_count(os.getpid())  # a collective: every rank calls it
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no GPU): rank launcher + control collectives", "value": None,
+                          "n_gpus": world, "physical_gpus": 0, "ranks_ok": ok, "max_rank_s": dt,
+                          "pids_distinct": pids}), flush=True)
+    rdist.shutdown()
 
 
 def two_erasure_masks(rng, n, t):
@@ -679,6 +766,16 @@ def committed_profile(workload):
 
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (launched by torchrun with another "
+                 f"--nproc-per-node?); refusing to time a different number of ranks than asked for")
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if args.dry_run:
+        return dry_run(args)
     import torch
 
     from replication_erasurecoding_object_store_amd import dist as rdist
@@ -690,6 +787,9 @@ def main():
         # runs them on the CPU instead, so the N>1 path can be rehearsed with several
         # ranks sharing one GPU (the driver's multi-GPU runs use the default).
         backend = os.environ.get("RSGPU_BENCH_BACKEND", "nccl")
+        if backend == "nccl" and local >= torch.cuda.device_count():
+            sys.exit(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} are visible "
+                     f"(RSGPU_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs)")
         if backend == "gloo":
             torch.cuda.set_device(local % torch.cuda.device_count())
         rdist.init(backend)

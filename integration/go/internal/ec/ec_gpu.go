@@ -53,58 +53,81 @@ type Service struct {
 
 	mu      sync.Mutex
 	nextTag uint64
-	waiting map[uint64]chan C.int
+	waiting map[uint64]chan int // result codes (Go ints: the tests cannot name cgo types)
 
 	// back-pressure: a submit that finds no free staging batch (RS_ERR_BUSY) waits
-	// for the next reap instead of spinning
+	// for the next reaper round instead of spinning.  Every round bumps epoch and
+	// wakes the waiters, timeouts included: batches also come free without a reap
+	// (rs_co_reconstruct_many's synchronous calls), so a waiter retries at least
+	// every reapTimeoutUs.
 	freeMu   sync.Mutex
 	freeCond *sync.Cond
-	reaped   uint64 // reap rounds so far (freeMu)
+	epoch    uint64 // reaper rounds so far (freeMu)
 
+	// broken: a reaper failed; the calls it left waiting got its error and every
+	// later call runs on klauspost (enc).  Set before waiting is flushed (mu).
+	broken  atomic.Bool
 	closing atomic.Bool
 	reapers sync.WaitGroup
 }
+
+// errGPUUnavailable: the call was not submitted (the engine is broken); the caller
+// runs it on the CPU codec instead.
+var errGPUUnavailable = errors.New("EC Driver: GPU engine unavailable")
 
 // reapTimeoutUs bounds one rs_co_reap wait so a reaper notices Close.
 const reapTimeoutUs = 100000
 
 // call runs one asynchronous coalescer call: submit(tag) stages it; the result
 // arrives from a reaper.  The caller keeps its shard buffers pinned until then.
+// errGPUUnavailable means nothing was submitted: run the call on the CPU.
 func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
-	ch := make(chan C.int, 1)
+	ch := make(chan int, 1) // buffered: a reaper never blocks on a send
 	s.mu.Lock()
+	if s.broken.Load() {
+		s.mu.Unlock()
+		return errGPUUnavailable
+	}
 	s.nextTag++
 	tag := s.nextTag
 	s.waiting[tag] = ch
 	s.mu.Unlock()
+	forget := func() {
+		s.mu.Lock()
+		delete(s.waiting, tag)
+		s.mu.Unlock()
+	}
 	for {
 		s.freeMu.Lock()
-		seen := s.reaped
+		seen := s.epoch
 		s.freeMu.Unlock()
 		rc := submit(C.uint64_t(tag))
 		if rc == C.RS_OK {
-			return toErr(<-ch)
+			return toErr(C.int(<-ch)) // a reaper's result, or the error of a reaper that failed
 		}
 		if rc != C.RS_ERR_BUSY || s.closing.Load() { // rejected: never reaped
-			s.mu.Lock()
-			delete(s.waiting, tag)
-			s.mu.Unlock()
+			forget()
 			return toErr(rc)
 		}
 		// no staging batch is free: batches still executing, or finished ones whose
-		// calls are not reaped yet -- sleep until a reaper has released some (a reap
-		// since `seen` means slots came back), then submit again
+		// calls are not reaped yet -- sleep until the next reaper round, then submit
+		// again
 		s.freeMu.Lock()
-		for s.reaped == seen && !s.closing.Load() {
+		for s.epoch == seen && !s.closing.Load() && !s.broken.Load() {
 			s.freeCond.Wait()
 		}
 		s.freeMu.Unlock()
+		if s.broken.Load() {
+			forget()
+			return errGPUUnavailable
+		}
 	}
 }
 
 // reap delivers finished calls to their goroutines; several run per Service.
 // rs_co_reap returns 0 on its timeout (or when the coalescer stops) and a negative
-// code on bad arguments, which ends this reaper.
+// code on bad arguments: then this reaper fails every waiting call with that code
+// and switches the Service to the CPU codec (fail, never hang a caller).
 func (s *Service) reap() {
 	defer s.reapers.Done()
 	const max = 256
@@ -115,23 +138,48 @@ func (s *Service) reap() {
 	for !s.closing.Load() {
 		n := int(C.rs_co_reap(s.co, &tags[0], &rcs[0], max, reapTimeoutUs))
 		if n < 0 {
-			log.Printf("EC Driver: rs_co_reap failed: %v; reaper stops", toErr(C.int(-n)))
+			s.fail(-n)
 			return
 		}
 		for i := 0; i < n; i++ {
 			s.mu.Lock()
-			ch := s.waiting[uint64(tags[i])]
+			ch, ok := s.waiting[uint64(tags[i])]
 			delete(s.waiting, uint64(tags[i]))
 			s.mu.Unlock()
-			ch <- rcs[i]
+			if ok { // a tag already failed by fail() has no waiter left
+				ch <- int(rcs[i])
+			}
 		}
-		if n > 0 {
-			s.freeMu.Lock()
-			s.reaped++
-			s.freeCond.Broadcast()
-			s.freeMu.Unlock()
-		}
+		s.tick()
 	}
+}
+
+// tick ends a reaper round: BUSY submitters wake and try again.
+func (s *Service) tick() {
+	s.freeMu.Lock()
+	s.epoch++
+	s.freeCond.Broadcast()
+	s.freeMu.Unlock()
+}
+
+// fail completes every waiting call with rc and sends later calls to the CPU codec.
+func (s *Service) fail(rc int) {
+	log.Printf("EC Driver: rs_co_reap failed: %v; failing %d waiting calls, using klauspost/reedsolomon on the CPU from now on",
+		toErr(C.int(rc)), s.pending())
+	s.broken.Store(true) // before the flush: no call registers after it
+	s.mu.Lock()
+	for tag, ch := range s.waiting {
+		ch <- rc
+		delete(s.waiting, tag)
+	}
+	s.mu.Unlock()
+	s.tick()
+}
+
+func (s *Service) pending() int {
+	s.mu.Lock()
+	defer s.mu.Unlock()
+	return len(s.waiting)
 }
 
 // Close stops the reapers and frees the engine.  No call may be in flight (an
@@ -199,7 +247,7 @@ func NewService() interfaces.IEcDriver {
 		log.Fatalf("Failed to create Reed-Solomon batch coalescer: %v", toErr(rc))
 	}
 	log.Printf("EC Driver loaded (k=%d, m=%d) on %s\n", config.K, config.M, C.GoString(C.rs_backend(ctx)))
-	s := &Service{ctx: ctx, co: co, enc: enc, gpu: true, waiting: make(map[uint64]chan C.int)}
+	s := &Service{ctx: ctx, co: co, enc: enc, gpu: true, waiting: make(map[uint64]chan int)}
 	s.freeCond = sync.NewCond(&s.freeMu)
 	// reapers share rs_co_reap's output copies: one per 4 Ps, 1..8
 	n := min(max(runtime.GOMAXPROCS(0)/4, 1), 8)
@@ -236,7 +284,7 @@ func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, fu
 
 // Encode fills shards[K:] in place (ec.go:54-56).
 func (s *Service) Encode(shards [][]byte) error {
-	if !s.gpu {
+	if !s.gpu || s.broken.Load() {
 		return s.enc.Encode(shards)
 	}
 	if len(shards) != config.K+config.M {
@@ -246,13 +294,17 @@ func (s *Service) Encode(shards [][]byte) error {
 	defer pin.Unpin() // after the call completed: the engine writes parity until then
 	p, l, free := shardArgs(shards, &pin)
 	defer free()
-	return s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_encode(s.co, p, l, tag) })
+	err := s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_encode(s.co, p, l, tag) })
+	if err == errGPUUnavailable {
+		return s.enc.Encode(shards)
+	}
+	return err
 }
 
 // Reconstruct fills every empty entry, data and parity (ec.go:59-61;
 // readservice.go:285 and poller.go:282 rely on all nil entries being filled).
 func (s *Service) Reconstruct(shards [][]byte) error {
-	if !s.gpu {
+	if !s.gpu || s.broken.Load() {
 		return s.enc.Reconstruct(shards)
 	}
 	if len(shards) != config.K+config.M {
@@ -289,7 +341,13 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 	defer pin.Unpin()
 	p, l, free := shardArgs(shards, &pin)
 	defer free()
-	if err := s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_reconstruct(s.co, p, l, tag) }); err != nil {
+	err := s.call(func(tag C.uint64_t) C.int { return C.rs_co_submit_reconstruct(s.co, p, l, tag) })
+	if err == errGPUUnavailable {
+		// nothing was submitted; the entries made above have len 0, so klauspost
+		// sees the same missing set and reuses their capacity
+		return s.enc.Reconstruct(shards)
+	}
+	if err != nil {
 		return err
 	}
 	for i := range shards { // every missing entry was filled
@@ -353,7 +411,7 @@ func (s *Service) EncodeHash(shards [][]byte, valueLen int) (sum [32]byte, err e
 func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 	t := config.K + config.M
 	errs = make([]error, len(objects))
-	if !s.gpu {
+	if !s.gpu || s.broken.Load() {
 		for i, shards := range objects {
 			errs[i] = s.enc.Reconstruct(shards)
 		}
