@@ -48,12 +48,22 @@ sys.path.insert(0, ROOT)
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: "6.29 TB/s measured (float4 copy, 79%)"
-# Compute-free ceilings of the RS access patterns on MI355X (tools/pattern_probe.hip,
-# profiles/r02_pattern_probe.log): the best the split layout's traffic reaches with no
-# arithmetic at all, fraction of 8 TB/s.  The probes grid-strided over a few workgroups
-# per CU; since round 4 the kernels launch one wave per task and can exceed these
-# figures (profiles/r04zi_bpc_flat.log).
-PATTERN_CEILING = {(4, 2, 1024): 0.797, (4, 2, 16384): 0.774, (8, 4, 8192): 0.778, (10, 4, 6554): 0.712}
+
+
+def committed_ceilings():
+    """Per-leg compute-free ceilings of the shipped kernels (fraction of 8 TB/s):
+    the newest committed profiles/*_pattern_ceilings.json written by
+    tools/ceiling_probe.sh -- the same sweep run with the RS_PATTERN_ONLY twin of the
+    library (same launches, loads and stores, no GF arithmetic) on one box."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pattern_ceilings.json")), reverse=True):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except Exception:
+            continue
+        doc["_path"] = os.path.relpath(path, ROOT)
+        return doc
+    return None
 
 
 def parse():
@@ -577,6 +587,7 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
     from replication_erasurecoding_object_store_amd.batch import BatchEngine
 
     _, _, world = rdist.world()
+    ceilings = committed_ceilings()
     sweep = {}
     for kk, mm in [(4, 2), (8, 4), (10, 4)]:
         e2 = BatchEngine(kk, mm, torch.cuda.current_device())
@@ -624,10 +635,16 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
         ent["kernels"] = kern
         w.close()
         e2.close()
-        ceiling = PATTERN_CEILING.get((kk, mm, SS))
-        if ceiling:
-            ent["pattern_ceiling_frac"] = ceiling
-        sweep[f"rs{kk}{mm}_64KiB"] = ent
+        name = f"rs{kk}{mm}_64KiB"
+        if ceilings:
+            # the compute-free twin of each leg's kernel (tools/ceiling_probe.sh), when
+            # the committed probe ran the kernel this leg launched
+            for key, kname in kern.items():
+                c = ceilings["legs"].get(name, {}).get(key)
+                if c and c["kernel"] == kname:
+                    ent[f"{key}_pattern_ceiling_frac"] = c["ceiling_frac"]
+            ent["pattern_ceilings_from"] = ceilings["_path"]
+        sweep[name] = ent
     return sweep
 
 
@@ -805,6 +822,16 @@ def main():
         res = {"kmsweep_64KiB_device": kmsweep(torch, rdist, rotate)}
         if world == 1:
             res["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
+            # the headline step's two kernels (configs[1] / configs[2]), same timing
+            w = RSWorkload(torch, eng, k, m, S, N, rotate, seed=0x5EED0002)
+            alg = w.alg_bytes()
+            head = {}
+            for key, fn, b in (("encode", w.enc, alg["encode"]), ("reconstruct", w.rec, alg["reconstruct"])):
+                ms, reps = sustained_kernel_ms(torch, fn, 100.0)
+                head[key] = {"kernel": eng.last_kernel(), "hbm_frac": round(b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                             "launches": reps}
+            w.close()
+            res["headline_rs42_4KiB"] = head
         if rank == 0:
             line = json.dumps(res)
             print(line, flush=True)
@@ -839,6 +866,12 @@ def main():
 
     dom = max(km, key=km.get)
     achieved = alg[dom] / (km[dom] * 1e-3) / 1e9
+    ceilings = committed_ceilings()
+    ceiling = None
+    if ceilings:
+        c = ceilings["legs"].get(f"rs{k}{m}_{args.stripe_kib}KiB", {}).get(dom)
+        if c and kernel_key(c["kernel"]) == kernel_key(kernel_names.get(dom, "")):
+            ceiling = {"frac": c["ceiling_frac"], "from": ceilings["_path"]}
     workload_key = f"rs{k}{m}_{args.stripe_kib}KiB_N{N}_split"
     prof = committed_profile(workload_key)
     frac_rocprof, traffic, rocprof_ns = None, None, None
@@ -891,7 +924,10 @@ def main():
             "frac_rocprof": frac_rocprof,  # from the committed profile of this kernel, not this run
             "rocprof_avg_ns": rocprof_ns,
             "rocprof_summary": prof["_path"] if prof else None,
-            "pattern_ceiling_frac": PATTERN_CEILING.get((k, m, S)),
+            # the dominant kernel's compute-free twin on the same launch shape
+            # (tools/ceiling_probe.sh), when the committed probe ran this very kernel
+            "pattern_ceiling_frac": ceiling["frac"] if ceiling else None,
+            "pattern_ceiling_from": ceiling["from"] if ceiling else None,
             "kernel_ms": {kk: round(v, 5) for kk, v in km.items()},
             "alg_bytes_per_launch": alg,
         },

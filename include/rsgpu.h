@@ -324,7 +324,10 @@ int rs_sha256_batch_var(rs_ctx *ctx, const uint8_t *base, const uint64_t *offset
  * call is using them; rs_destroy frees any left (after every queued kernel). */
 int rs_host_alloc(rs_ctx *ctx, size_t bytes, void **out);
 int rs_host_free(rs_ctx *ctx, void *ptr);
-/* Records [ptr, ptr + bytes) as caller memory and nothing more: the library never
+/* DEPRECATED -- a range recorder that never pins (the name is historical; do not
+ * call it expecting faster transfers: registered and unregistered caller memory
+ * take exactly the same staged path).
+ * Records [ptr, ptr + bytes) as caller memory and nothing more: the library never
  * pins, maps or addresses caller memory in place (round 4).  amdgpu maps
  * hipHostRegister'ed pageable memory as a user-pointer range whose pages may still
  * be migrated, compacted or collapsed into huge pages while a kernel runs, which is
@@ -332,7 +335,9 @@ int rs_host_free(rs_ctx *ctx, void *ptr);
  * buffers are staged like any pageable buffer; use rs_host_alloc for in-place
  * work.  Kept for ABI compatibility: RS_ERR_INVALID_ARG for a range overlapping a
  * known one; rs_host_unregister(ptr) forgets the range starting at ptr
- * (RS_ERR_INVALID_ARG if there is none, or it is rs_host_free's). */
+ * (RS_ERR_INVALID_ARG if there is none, or it is rs_host_free's).  A recorded range
+ * that rs_host_alloc later gets memory inside (the caller freed it without
+ * unregistering) is dropped, never an allocation failure. */
 int rs_host_register(rs_ctx *ctx, void *ptr, size_t bytes);
 int rs_host_unregister(rs_ctx *ctx, void *ptr);
 

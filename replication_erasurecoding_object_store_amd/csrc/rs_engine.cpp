@@ -251,20 +251,35 @@ struct StatusChunk {
 // "What ran last" (measurement and fault diagnostics): context-wide, and per launch
 // stream -- a device fault surfaces asynchronously, and only the stream's own record
 // names the launch that preceded it when other threads launch on the context too.
+// The per-stream record is sharded by stream handle (one
+// context-wide mutex on every launch made concurrent launchers queue on it); a
+// shard's entry stays until rs_stream_release(stream) forgets it.
 struct Shared {
+  static constexpr size_t kShards = 64;
+  struct Shard {
+    std::mutex mu;
+    std::unordered_map<hipStream_t, const char*> by_stream;
+  };
   std::atomic<const char*> last_kernel{"none"};
   std::atomic<const char*> last_host_path{"none"};
-  std::mutex stream_mu;
-  std::unordered_map<hipStream_t, const char*> by_stream;
+  Shard shards[kShards];
+  Shard& shard(hipStream_t s) { return shards[(reinterpret_cast<uintptr_t>(s) >> 4) % kShards]; }
   void note(hipStream_t s, const char* name) {
-    last_kernel.store(name);
-    std::lock_guard<std::mutex> g(stream_mu);
-    by_stream[s] = name;
+    last_kernel.store(name, std::memory_order_relaxed);
+    Shard& sh = shard(s);
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.by_stream[s] = name;
   }
   const char* on(hipStream_t s) {
-    std::lock_guard<std::mutex> g(stream_mu);
-    auto it = by_stream.find(s);
-    return it == by_stream.end() ? "none" : it->second;
+    Shard& sh = shard(s);
+    std::lock_guard<std::mutex> g(sh.mu);
+    auto it = sh.by_stream.find(s);
+    return it == sh.by_stream.end() ? "none" : it->second;
+  }
+  void forget(hipStream_t s) {
+    Shard& sh = shard(s);
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.by_stream.erase(s);
   }
 };
 
@@ -318,6 +333,7 @@ struct Engine {
   std::mutex host_mu;                     // host-resident batches: one at a time per engine
   hipStream_t pipe_st[kHostStreams] = {};
   DevBuf pipe_buf[kHostStreams];
+  PinnedBuf pipe_host[kHostStreams];      // staged per-stripe reconstruct: dense output rows (D2H)
   DevBuf d_bad;                           // zero-copy verify: per-stripe result before D2H
 
   std::atomic<int> inflight{0};           // calls running on this engine (dispatch)
@@ -911,6 +927,105 @@ int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_
   return RS_OK;
 }
 
+// The first k present shards of a mask: the survivors a per-stripe plan reads
+// (klauspost's choice, make_decode_plan).
+uint32_t first_present(uint32_t present, int k) {
+  uint32_t r = 0;
+  for (int c = 0; c < k && present; ++c) {
+    r |= present & (0u - present);
+    present &= present - 1u;
+  }
+  return r;
+}
+
+// Staged per-stripe reconstruct (round 5): only the bytes the codec needs cross
+// PCIe, and the caller's present shards are never written.
+//  * H2D: the slots some stripe of the share reads -- the union of every stripe's
+//    first k present shards (a 1-erasure healer mix of RS(4+2) never reads slot 5).
+//  * The kernel writes out of place into a dense slab, the r-th missing shard of
+//    stripe i at row i*e_out + r (what the healer writes back, poller.go:288-302).
+//  * D2H: that slab (e_out rows per stripe, not k+m), into pinned memory, from which
+//    the host scatters each row into the caller's missing slot -- on the calling
+//    thread, while the other pipeline streams' chunks are in flight.
+// Round 4 moved every slot both ways and wrote the present ones back unchanged:
+// config 5 (50/50 encode / 1-erasure) 25.7 GiB/s.
+int host_batch_ps(Engine* e, const Layout& hl, size_t S, size_t N, const uint32_t* masks, int e_out) {
+  const int k = e->k, m = e->m, t = k + m;
+  const uint32_t full = static_cast<uint32_t>(full_mask64(t));  // t <= 16: per-stripe host masks need the LUT
+  std::vector<uint8_t> seen(size_t(1) << t, 0);
+  uint32_t need = 0;
+  for (size_t i = 0; i < N; ++i) {
+    const uint32_t pm = masks[i] & full;
+    if (!seen[pm]) {
+      seen[pm] = 1;
+      need |= first_present(pm, k);
+    }
+  }
+  std::vector<int> in_slots;
+  for (int s = 0; s < t; ++s)
+    if ((need >> s) & 1u) in_slots.push_back(s);
+  const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
+  const size_t slab = P * static_cast<size_t>(t), outb = P * static_cast<size_t>(e_out);
+  const size_t per_stripe = slab + outb + 4;
+  const size_t chunk = std::min(N, std::max<size_t>(1, kHostChunkBytes / per_stripe));
+  const size_t in_bytes = round_up(chunk * slab, 256), out_bytes = round_up(chunk * outb, 256);
+  std::lock_guard<std::mutex> g(e->host_mu);
+  for (int i = 0; i < kHostStreams; ++i) {
+    int rc = ensure_pipe_stream(e, i);
+    if (rc) return rc;
+    e->pipe_host[i].numa = e->numa;
+    if (e->pipe_buf[i].ensure(std::max(kHostChunkBytes, in_bytes + out_bytes + chunk * 4) + per_stripe + 256) ||
+        e->pipe_host[i].ensure(chunk * static_cast<size_t>(e_out) * S))
+      return RS_ERR_DEVICE;
+  }
+  size_t pend_s0[kHostStreams] = {}, pend_n[kHostStreams] = {};
+  auto scatter = [&](int i) {  // chunk on stream i is complete: its rows into the missing slots
+    const uint8_t* h = static_cast<const uint8_t*>(e->pipe_host[i].p);
+    for (size_t q = 0; q < pend_n[i]; ++q) {
+      const size_t s = pend_s0[i] + q;
+      uint32_t miss = ~masks[s] & full;
+      for (size_t r = 0; miss; ++r) {
+        const int j = __builtin_ctz(miss);
+        miss &= miss - 1u;
+        std::memcpy(hl.slot(k, s, j), h + (q * static_cast<size_t>(e_out) + r) * S, S);
+      }
+    }
+    pend_n[i] = 0;
+  };
+  int j = 0;
+  for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
+    const int i = j % kHostStreams;
+    hipStream_t st = e->pipe_st[i];
+    if (pend_n[i]) {  // the stream's previous chunk: its pinned rows are about to be reused
+      RS_HIP(hipStreamSynchronize(st));
+      scatter(i);
+    }
+    const size_t n = std::min(chunk, N - s0);
+    uint8_t* d = static_cast<uint8_t*>(e->pipe_buf[i].p);
+    const Layout dl{d, P * k, d + chunk * P * k, P * m, P};
+    int rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
+    if (rc) return rc;
+    uint8_t* o = d + in_bytes;
+    uint32_t* aux = reinterpret_cast<uint32_t*>(o + out_bytes);
+    RS_HIP(hipMemcpyAsync(aux, masks + s0, n * 4, hipMemcpyHostToDevice, st));
+    rs::KernelArgs a = make_args(e, dl, S, n);
+    a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+    a.present_masks = aux;
+    a.out = o;
+    a.out_sp = outb;
+    rc = launch(e, a, e_out, true, st);
+    if (rc) return rc;
+    RS_HIP(copy2d(e->pipe_host[i].p, S, o, P, S, n * static_cast<size_t>(e_out), hipMemcpyDeviceToHost, st));
+    pend_s0[i] = s0;
+    pend_n[i] = n;
+  }
+  for (int i = 0; i < kHostStreams; ++i) {
+    RS_HIP(hipStreamSynchronize(e->pipe_st[i]));
+    if (pend_n[i]) scatter(i);
+  }
+  return RS_OK;
+}
+
 // One engine's share of a host-resident batch (caller holds its DeviceScope).
 int host_batch(Engine* e, const Layout& hl, const std::vector<int>& in_slots, const std::vector<int>& out_slots,
                size_t S, size_t N, const uint8_t* plan_dev, const uint32_t* masks_host, int e_out,
@@ -921,6 +1036,7 @@ int host_batch(Engine* e, const Layout& hl, const std::vector<int>& in_slots, co
     if (rc != RS_ERR_NOT_SUPPORTED) return rc;
   }
   e->shared->last_host_path.store("staged");
+  if (masks_host && !bad_host) return host_batch_ps(e, hl, S, N, masks_host, e_out);
   const int k = e->k, m = e->m;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t per_stripe = P * static_cast<size_t>(k + m) + ((masks_host || bad_host) ? 4 : 0);
@@ -1446,12 +1562,7 @@ int rs_reconstruct_batch(rs_ctx* c, uint8_t* data, size_t data_sp, uint8_t* pari
         out_slots.push_back(i);
       }
     }
-  } else {
-    // per-stripe patterns: every slot travels both ways on the staged path (present
-    // slots come back unchanged); the zero-copy path touches only what it needs
-    for (int i = 0; i < t; ++i) in_slots.push_back(i);
-    out_slots = in_slots;
-  }
+  }  // per-stripe patterns: host_batch_ps picks the slots from the masks
   return fan_out(c, N, static_cast<size_t>(c->k) * S, [&](Engine* e, size_t s0, size_t n) {
     const uint8_t* plan = static_cast<const uint8_t*>(e->d_plans.p);
     const uint32_t* mk = nullptr;
@@ -1565,10 +1676,7 @@ static int sync_stream(rs_ctx* c, void* stream, bool release) {
     e->status_idx.erase(s);
     e->status_free.push_back(idx);
   }
-  if (release) {
-    std::lock_guard<std::mutex> g(c->shared.stream_mu);
-    c->shared.by_stream.erase(s);
-  }
+  if (release) c->shared.forget(s);
   if (word & 1u) return RS_ERR_TOO_FEW_SHARDS;
   if (word & 2u) return RS_ERR_INVALID_ARG;
   return RS_OK;
@@ -1587,6 +1695,15 @@ uint32_t count_owned(const rs_ctx* c) {
 // Inserts r unless it overlaps a known range (false then).
 bool reg_insert(rs_ctx* c, const RegRange& r) {
   std::unique_lock<std::shared_mutex> g(c->reg_mu);
+  if (r.owned) {
+    // Memory the allocator just handed out cannot be live caller memory: a caller
+    // range recorded over it is stale (freed without rs_host_unregister -- harmless
+    // since round 4, nothing is pinned) and gives way instead of failing the
+    // allocation.
+    c->reg.erase(std::remove_if(c->reg.begin(), c->reg.end(),
+                                [&](const RegRange& q) { return !q.owned && q.lo < r.hi && r.lo < q.hi; }),
+                 c->reg.end());
+  }
   auto it = std::lower_bound(c->reg.begin(), c->reg.end(), r.lo,
                              [](const RegRange& a, uintptr_t lo) { return a.lo < lo; });
   if (it != c->reg.end() && it->lo < r.hi) return false;
@@ -1645,8 +1762,8 @@ int rs_host_alloc(rs_ctx* c, size_t bytes, void** out) {
   }
   if (!reg_insert(c, RegRange{reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p) + n,
                               static_cast<uint8_t*>(dev), true})) {
-    rs::pinned_free(p);  // a caller range recorded over memory that was not the caller's
-    return RS_ERR_DEVICE;
+    rs::pinned_free(p);  // overlaps a live owned range: the allocator's bookkeeping is broken
+    return RS_ERR_INVALID_ARG;
   }
   *out = p;
   return RS_OK;

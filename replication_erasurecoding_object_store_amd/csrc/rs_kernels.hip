@@ -48,6 +48,14 @@ namespace rs {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// RS_PATTERN_ONLY=1 builds the compute-free twin of every reconstruct / encode
+// kernel (tools/ceiling_probe.sh): the same launches, tasks, loads and stores, with
+// the GF(2^8) arithmetic replaced by one XOR per input dword -- the ceiling of each
+// kernel's memory pattern on its shipped launch shape.  Its bytes are NOT codewords.
+#ifndef RS_PATTERN_ONLY
+#define RS_PATTERN_ONLY 0
+#endif
+
 struct Idx3 {
   uint32_t a, b, c;
 };
@@ -272,6 +280,15 @@ __device__ __forceinline__ uint32_t pop_low(uint32_t& bits) {
 // e.g. 100 for RS(10+4) x 2 rows -> SGPR spills through VGPR lanes).
 template <int K, int M, int R0, int NR>
 __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K], u32x4 (&y)[NR]) {
+  if constexpr (RS_PATTERN_ONLY) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      y[r] = x[0] + static_cast<uint32_t>(R0 + r);
+#pragma unroll
+      for (int c = 1; c < K; ++c) y[r] ^= x[c];
+    }
+    return;
+  }
   u32x4 pend[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
@@ -312,6 +329,13 @@ __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K]
 template <int K, int M>
 __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)[K][4], int r) {
   u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+  if constexpr (RS_PATTERN_ONLY) {
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) y[d] ^= ix[c][d].a + static_cast<uint32_t>(r);
+    return y;
+  }
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     const uint8_t* tcol = plan;
@@ -462,9 +486,10 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       const uint32_t loff = work ? off : kDropOffset;
 #pragma unroll
       for (int c = 0; c < K; ++c) {
+        // range: the slot's columns (cols * 16 <= 1 GiB + 16 per column window), never
+        // the pitch, which may exceed 32 bits in plane-major layouts
         const auto r = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(uniform_ptr(slot_ptr(a, K, stripe, pv.in_idx(c)))), 0,
-            static_cast<uint32_t>(a.shard_pitch), 0x00020000);
+            const_cast<uint8_t*>(uniform_ptr(slot_ptr(a, K, stripe, pv.in_idx(c)))), 0, cols * 16u, 0x00020000);
         x[c] = bload16(r, loff, 0);
       }
     } else {
@@ -694,8 +719,13 @@ __device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pit
       xa[slot] = bload16(din, off_a, (C + kBsWindow) * pitch);
       xb[slot] = bload16(din, off_b, (C + kBsWindow) * pitch);
     }
-    transpose8(d);
-    bs_step<K, M, C>(d, y);
+    if constexpr (RS_PATTERN_ONLY) {
+#pragma unroll
+      for (int i = 0; i < 8 * M; ++i) y[i] = (C == 0 ? 0u : y[i]) ^ d[i & 7];
+    } else {
+      transpose8(d);
+      bs_step<K, M, C>(d, y);
+    }
     bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, y);
   }
 }
@@ -782,7 +812,7 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
       uint32_t d[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
-      transpose8(d);
+      if constexpr (!RS_PATTERN_ONLY) transpose8(d);
       const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
       __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
       __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
@@ -846,8 +876,16 @@ __device__ __forceinline__ void bs16_fold(__amdgpu_buffer_rsrc_t din, uint32_t p
       xa[slot] = bload16(din, off, (2 * (P + kBs16Window)) * pitch);
       xb[slot] = bload16(din, off, (2 * (P + kBs16Window) + 1) * pitch);
     }
-    transpose8(d);
-    bs16_step<K, M, P>(d, ya, yb);
+    if constexpr (RS_PATTERN_ONLY) {
+#pragma unroll
+      for (int i = 0; i < 4 * M; ++i) {
+        ya[i] = (P == 0 ? 0u : ya[i]) ^ d[i & 7];
+        yb[i] = (P == 0 ? 0u : yb[i]) ^ d[(i + 3) & 7];
+      }
+    } else {
+      transpose8(d);
+      bs16_step<K, M, P>(d, ya, yb);
+    }
     bs16_fold<K, M, P + 1>(din, pitch, off, xa, xb, ya, yb);
   }
 }
@@ -895,7 +933,7 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
         const uint32_t b = yb[q * 8 + i];
         d[i] = ya[q * 8 + i] ^ ((b >> 4) & 0x0F0F0F0Fu) ^ ((b << 4) & 0xF0F0F0F0u);
       }
-      transpose8(d);
+      if constexpr (!RS_PATTERN_ONLY) transpose8(d);
       const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
       __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sf ? f.poff : kDropOffset, (2 * q) * pitch, 2 /* nt */);
       __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sf ? f.poff : kDropOffset, (2 * q + 1) * pitch, 2 /* nt */);
@@ -933,6 +971,7 @@ template <int K, int M>
 __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t* planB, bool inB,
                                             const Idx3 (&ix)[K][4], int r) {
   u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+  if constexpr (RS_PATTERN_ONLY) return gf_row_ix<K, M>(planA, ix, r);
   const uint32_t selB = inB ? 0xFFFFFFFFu : 0u;
 #pragma unroll
   for (int c = 0; c < K; ++c) {
@@ -969,6 +1008,10 @@ __device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t*
 template <int K, int M, int NR, int R0 = 0>
 __device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* planB, bool inB, const u32x4 (&x)[K],
                                          u32x4 (&y)[NR]) {
+  if constexpr (RS_PATTERN_ONLY) {
+    gf_rows<K, M, R0, NR>(planA, x, y);
+    return;
+  }
   u32x4 pend[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
@@ -1160,6 +1203,237 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
     }
     next_task();
+  }
+  if (bad && lane == 0u) atomicOr(a.status, bad);
+}
+
+// ---------------------------------------------------------------------------
+// Flat per-stripe reconstruct, segmented (round 5).  The same flat 64-column tasks
+// as apply_flat_ps_kernel, but a task whose two stripes have different erasure
+// patterns runs as two passes of the single-plan code -- the lanes of stripe s0
+// with plan A, then the lanes of stripe s0+1 with plan B -- in which the other
+// stripe's lanes load nothing (out-of-range offsets: no fetch) and store nothing.
+// No per-lane plan selection (gf_rows2 / gf_row_ix2) is compiled in, so the kernel
+// holds one plan's working set; the price is a second pass of VALU work on the one
+// task in 13 that straddles two stripes (RS(10+4) at 64 KiB objects: 6.5 tasks per
+// stripe).  A pass over an intact (or skipped) stripe is not run at all.
+// RS_FLAT_EM_ROWS: rows of the E > 2 launches -- 0: every input's chunk indices
+// kept (ix[K][4], 12 VGPRs per input) and one row at a time, as apply_flat_ps_kernel;
+// 1: each row re-splits its inputs (only x[K] live); 2: input-outer passes of <= 2
+// rows (rows 0-1, then 2-3 only for a stripe missing more than 2).
+#ifndef RS_FLAT_SEG
+#define RS_FLAT_SEG 0
+#endif
+#ifndef RS_FLAT_EM_ROWS
+#define RS_FLAT_EM_ROWS 0
+#endif
+// RS_FLAT_EM_FULL: the E > 2 flat launches take one task per wave (a full grid) like
+// the E <= 2 ones, instead of a grid-stride loop over default_blocks_per_cu.
+#ifndef RS_FLAT_EM_FULL
+#define RS_FLAT_EM_FULL 0
+#endif
+
+// Makes the inputs' registers opaque to the compiler: chunk indices computed from
+// them before cannot be reused after (it would otherwise keep every split live
+// across rows -- the ix[K][4] array this is meant to avoid).
+template <int K>
+__device__ __forceinline__ void launder(u32x4 (&x)[K]) {
+#pragma unroll
+  for (int c = 0; c < K; ++c)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(x[c][d]));
+}
+
+// One row r from the inputs' bytes, split on the fly (no chunk-index array).
+template <int K, int M>
+__device__ __forceinline__ u32x4 gf_row_x(const uint8_t* plan, const u32x4 (&x)[K], int r) {
+  u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
+  if constexpr (RS_PATTERN_ONLY) {
+#pragma unroll
+    for (int c = 0; c < K; ++c) y ^= x[c] + static_cast<uint32_t>(r);
+    return y;
+  }
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    const uint8_t* tcol = plan;
+    asm volatile("" : "+s"(tcol));  // one opaque base per input: tables never all in SGPRs
+    const PlanView pc(tcol, K, M);
+    const RS_CONST uint32_t* tb = pc.quad(r, c);
+    const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(r, c);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t prod = lookup3(split3(x[c][d]), q0, q1, q2, q3, q4);
+      if (c & 1)
+        y[d] = xor3(y[d], pend[d], prod);
+      else if (c == K - 1)
+        y[d] ^= prod;
+      else
+        pend[d] = prod;
+    }
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+  }
+  return y;
+}
+
+template <int K, int M, int E>
+__global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = wave_index();
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t N = a.n_stripes;
+  const uint32_t cols = (a.shard_len + 15u) >> 4;
+  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
+  const uint32_t cstride = (cols + 7u) & ~7u;
+  if (static_cast<uint64_t>(wave) * 64u >= static_cast<uint64_t>(N) * cstride) return;
+  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
+  const uint32_t full = a.full_mask;
+  const uint64_t g0 = static_cast<uint64_t>(wave) * 64u;
+  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
+  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
+  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 64u;
+  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
+  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
+  uint32_t bad = 0u;
+
+  // stripe s's present mask (a skipped one: all present) and plan
+  auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
+    const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
+    uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
+    bad |= (pid == kPlanInvalid) ? 1u : 0u;
+    bool skip = pid == kPlanInvalid;
+    if constexpr (E < M) {  // more erasures than this launch's bound: skip, flag
+      const bool over = static_cast<uint32_t>(__builtin_popcount((~present) & full)) > static_cast<uint32_t>(E);
+      bad |= over ? 2u : 0u;
+      skip = skip || over;
+    }
+    m = skip ? full : present;
+    pid = skip ? 0u : pid;  // plan 0 = nothing missing
+    const uint8_t* p = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
+    nout = PlanView(p, K, M).n_out();
+    return p;
+  };
+
+  while (s0 < N) {
+    const uint32_t cl = c0 + lane;
+    const bool inB = cl >= cstride;
+    const uint32_t colr = inB ? cl - cstride : cl;
+    const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
+    const bool live = !inB || straddle;                         // past the batch end: dead
+    const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
+    uint32_t mA, nA, mB, nB;
+    const uint8_t* planA = plan_of(s0, mA, nA);
+    const uint8_t* planB = planA;
+    mB = mA;
+    nB = nA;
+    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
+    const bool two = planA != planB;  // wave-uniform: two passes, one per stripe
+    const bool lb = live && inB;
+    const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
+    const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
+    const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
+    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
+                                                        0x7FFFFFFF, 0x00020000);
+    const bool fullc = live && colr < a.full_cols;
+    const bool part = nb != 0u && live && colr == a.full_cols;
+    for (uint32_t seg = 0; seg < (two ? 2u : 1u); ++seg) {
+      const bool sb = seg != 0u;
+      const uint8_t* plan = sb ? planB : planA;
+      uint32_t bits = sb ? mB : mA;
+      const uint32_t nout = sb ? nB : nA;  // wave-uniform
+      if (nout == 0u) continue;           // an intact (or skipped) stripe: no loads, no stores
+      const bool mine = !two || inB == sb;
+      const uint32_t oD = mine ? offD : kDropOffset, oP = mine ? offP : kDropOffset;
+      u32x4 x[K];
+#pragma unroll
+      for (int c = 0; c < K; ++c) {
+        const uint32_t s = pop_low(bits);
+        x[c] = s < static_cast<uint32_t>(K) ? bload16(din, oD, s * pitch)
+                                            : bload16(pin, oP, (s - static_cast<uint32_t>(K)) * pitch);
+      }
+      const uint32_t nl = mine ? nout : 0u;
+      // stores rows [0, NR) with cache policy CPOL, dropped per lane past its stripe's outputs
+      auto emit = [&](auto nr_tag, auto cpol_tag, const auto& yy) {
+        constexpr int NR = decltype(nr_tag)::value;
+        constexpr int CPOL = decltype(cpol_tag)::value;
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          __builtin_amdgcn_raw_buffer_store_b128(yy[r], oout,
+                                                 fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
+                                                 r * pitch, CPOL);
+        if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            store_part_rsrc<CPOL>(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, yy[r], nb);
+        }
+      };
+      if constexpr (E <= 2) {
+        u32x4 y[E];
+        gf_rows<K, M, 0, E>(plan, x, y);
+        emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+      } else {
+        u32x4 y[E];
+        if constexpr (RS_FLAT_EM_ROWS == 2) {
+          u32x4 y01[2];
+          if (nout <= 1u) {
+            u32x4 y0[1];
+            gf_rows<K, M, 0, 1>(plan, x, y0);
+            y01[0] = y01[1] = y0[0];
+          } else {
+            gf_rows<K, M, 0, 2>(plan, x, y01);
+          }
+          y[0] = y01[0];
+          y[1] = y01[1];
+          u32x4 yh[E - 2];
+#pragma unroll
+          for (int r = 0; r < E - 2; ++r) yh[r] = y01[0];
+          if (nout > 2u) {
+            launder(x);
+            gf_rows<K, M, 2, E - 2>(plan, x, yh);
+          }
+#pragma unroll
+          for (int r = 2; r < E; ++r) y[r] = yh[r - 2];
+        } else if constexpr (RS_FLAT_EM_ROWS == 1) {
+          y[0] = gf_row_x<K, M>(plan, x, 0);
+#pragma unroll
+          for (int r = 1; r < E; ++r) {
+            y[r] = y[0];  // dropped unless computed
+            if (static_cast<uint32_t>(r) < nout) {
+              launder(x);
+              y[r] = gf_row_x<K, M>(plan, x, r);
+            }
+          }
+        } else {
+          Idx3 ix[K][4];
+#pragma unroll
+          for (int c = 0; c < K; ++c)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+#pragma unroll
+          for (int r = 1; r < E; ++r) {
+            y[r] = y[0];  // dropped unless computed
+            if (static_cast<uint32_t>(r) < nout) y[r] = gf_row_ix<K, M>(plan, ix, r);
+          }
+        }
+        if (RS_WAVE_ROWS && nout <= 1u)  // wave-uniform: the bounded kernels' store policy
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
+        else if (RS_WAVE_ROWS && nout == 2u)
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+        else
+          emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+      }
+    }
+    c0 += step_c;  // grid stride in the flat column space
+    s0 += step_s;
+    if (c0 >= cstride) {
+      c0 -= cstride;
+      ++s0;
+    }
   }
   if (bad && lane == 0u) atomicOr(a.status, bad);
 }
@@ -1563,10 +1837,14 @@ static const void* pick_bitsliced(int k, int m, const char** name, uint32_t* tas
 // or the bound a caller (host masks: their maximum; device masks: max_missing)
 // gives -- E <= 2 runs input-outer with x[K] as the only per-input state.
 static const void* pick_flat_ps(int k, int m, int e, const char** name) {
-#define RS_PSFLAT(KK, MM, EE)                                                 \
-  if (k == KK && m == MM && e == EE) {                                        \
-    *name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                  \
-    return reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>); \
+#define RS_PSFLAT(KK, MM, EE)                                                   \
+  if (k == KK && m == MM && e == EE) {                                          \
+    if (RS_FLAT_SEG) {                                                          \
+      *name = "apply_flat_seg_kernel<" #KK "," #MM "," #EE ">";                 \
+      return reinterpret_cast<const void*>(&apply_flat_seg_kernel<KK, MM, EE>); \
+    }                                                                           \
+    *name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                    \
+    return reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>);   \
   }
   RS_PSFLAT(4, 2, 1) RS_PSFLAT(4, 2, 2)
   RS_PSFLAT(8, 4, 1) RS_PSFLAT(8, 4, 2) RS_PSFLAT(8, 4, 4)
@@ -1641,7 +1919,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // E <= 2: one task per wave (r04zi: RS(10+4) 64 KiB 1-/2-erasure +0.9 / +2.5
       // points); E = M keeps its grid-stride loop (a full grid lost 10 points there)
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
-      const dim3 grid = (!blocks_per_cu && e <= 2) ? full_grid(waves) : grid_for(waves, bpc, cu_count);
+      const dim3 grid = (!blocks_per_cu && (e <= 2 || RS_FLAT_EM_FULL)) ? full_grid(waves)
+                                                                         : grid_for(waves, bpc, cu_count);
       if (hipLaunchKernel(ff, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
       return name;
     }

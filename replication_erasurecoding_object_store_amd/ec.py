@@ -187,7 +187,11 @@ class Arena:
     (rs_host_alloc).  Alloc(n) hands out writable memoryviews, 16-B aligned; a
     coalesced call whose shards all come from an arena runs in place on the GPU (no
     staging copies, parity written straight into the views).  A bump allocator:
-    Alloc until full, Reset when no view is in use, Close to free."""
+    Alloc until full, Reset when no view is in use, Close to free.
+
+    A view re-exported by the caller (numpy.frombuffer(view), ...) cannot be revoked:
+    Reset and Close raise BufferError while such an export is alive instead of
+    handing its memory out again or freeing it under it."""
 
     def __init__(self, svc: "Service", size: int):
         n = (size + 4095) // 4096 * 4096
@@ -195,7 +199,8 @@ class Arena:
         _check(_lib.lib().rs_host_alloc(svc.ctx, n, ctypes.byref(p)))
         self._svc, self._base, self._size, self._off = svc, p.value, n, 0
         self._mem = (ctypes.c_uint8 * n).from_address(p.value)
-        self._views: List[memoryview] = []  # released when the memory goes away
+        self._root: Optional[memoryview] = memoryview(self._mem).cast("B")  # one per arena
+        self._views: List[memoryview] = []  # slices handed out, released with the memory
         svc._arenas.add(self)
 
     def Alloc(self, n: int) -> Optional[memoryview]:
@@ -203,36 +208,53 @@ class Arena:
         if n <= 0 or self._base is None or off + n > self._size:
             return None
         self._off = off + n
-        root = memoryview(self._mem).cast("B")
-        v = root[off:off + n]
-        self._views += [v, root]
+        v = self._root[off:off + n]
+        self._views.append(v)
         return v
 
     def Reset(self) -> None:
         """Makes the whole arena free again (no view may be in use): the views handed
         out so far are released."""
-        self._release_views()
+        if self._release_views():
+            raise BufferError("Arena.Reset: views are still exported (e.g. numpy arrays over them); "
+                              "their memory would be handed out again")
         self._off = 0
 
-    def _release_views(self) -> None:
-        for v in reversed(self._views):
+    def _release_views(self) -> int:
+        """Releases every view handed out; returns how many are still exported."""
+        stuck = []
+        for v in self._views:
             try:
                 v.release()
-            except BufferError:  # re-exported by the caller (e.g. numpy): cannot be revoked
-                pass
-        self._views = []
+            except BufferError:  # re-exported by the caller: cannot be revoked
+                stuck.append(v)
+        self._views = stuck
+        return len(stuck)
 
     def _invalidate(self) -> None:
         """The memory is about to be freed: every view handed out is released (using
         one afterwards raises ValueError instead of touching freed memory) and Alloc
-        returns None."""
-        self._release_views()
-        self._base, self._mem = None, None
+        returns None.  Views still exported when the service closes cannot be
+        revoked: a warning names them."""
+        if self._release_views():
+            import warnings
+
+            warnings.warn(f"Arena freed with {len(self._views)} view(s) still exported", RuntimeWarning)
+        if self._root is not None:
+            try:
+                self._root.release()
+            except BufferError:
+                pass
+        self._base, self._mem, self._root = None, None, None
 
     def Close(self) -> None:
         """Frees the memory (no view may be in use); after the service closed,
-        rs_destroy has freed it already."""
+        rs_destroy has freed it already.  BufferError (nothing freed) while a view
+        is still exported."""
         if self._base is not None and self._svc.ctx:
+            if self._release_views():
+                raise BufferError("Arena.Close: views are still exported (e.g. numpy arrays over them); "
+                                  "drop them first")
             base = self._base
             self._invalidate()
             _check(_lib.lib().rs_host_free(self._svc.ctx, base))

@@ -371,6 +371,51 @@ def test_batch_host_paths_match_device(engines, zero_copy, mem):
         _host_mem_free(eng, mem, host)
 
 
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4)])
+def test_staged_per_stripe_never_writes_present_slots(engines, k, m):
+    """Staged per-stripe host reconstruct (round 5, host_batch_ps): every present
+    slot of the caller's memory is read-only (mprotect) during the call -- a write by
+    DMA or by the host scatter would fail the call or fault -- and the missing slots
+    come back equal to the oracle's codewords.  Intact stripes, 1..m erasures and
+    slack bytes past S in every slot (guard pattern, never written) included."""
+    import ctypes
+    import mmap
+
+    eng = eng_for(engines, k, m)
+    t = k + m
+    S, P, N = 4000, 4096, 48  # one page per slot: each present slot protected on its own
+    mm = mmap.mmap(-1, N * t * P)
+    host = np.frombuffer(mm, np.uint8).reshape(N, t, P)
+    rng = np.random.default_rng(21)
+    want = np.zeros((N, t, S), np.uint8)
+    want[:, :k] = rng.integers(0, 256, (N, k, S), dtype=np.uint8)
+    rs_oracle.encode_batch_scalar(k, m, want.reshape(-1), t * S, S, S, N)
+    host[:, :, :S] = want
+    host[:, :, S:] = 0xA5  # guard bytes past S
+    masks = np.full(N, (1 << t) - 1, np.uint32)
+    for i in range(N):
+        ne = i % (m + 1)  # 0 (intact) .. m erasures
+        for j in rng.choice(t, size=ne, replace=False):
+            masks[i] &= ~np.uint32(1 << int(j))
+            host[i, j, :S] = 0
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    base = host.ctypes.data
+    present = [(i, j) for i in range(N) for j in range(t) if (masks[i] >> j) & 1]
+    for i, j in present:
+        assert libc.mprotect(base + (i * t + j) * P, P, mmap.PROT_READ) == 0
+    try:
+        eng.reconstruct_host_unified(host, S, P, N, masks)
+        assert eng.last_host_path() == "staged"
+    finally:
+        for i, j in present:
+            libc.mprotect(base + (i * t + j) * P, P, mmap.PROT_READ | mmap.PROT_WRITE)
+    assert not _host_diff(host[:, :, :S], want), _host_diff(host[:, :, :S], want)
+    assert (host[:, :, S:] == 0xA5).all(), "bytes past S were written"
+    del host
+    mm.close()
+
+
 def test_config2_full_size_roundtrip(engines):
     """BASELINE config 2/3 at full size (65 536 x 4 KiB stripes): encode, check a
     sample of stripes against the oracle, then erase 2 shards per stripe (seeded

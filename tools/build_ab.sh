@@ -8,9 +8,10 @@ NAME=$1; SRC=$2; shift 2
 C=replication_erasurecoding_object_store_amd/csrc
 make -s -C $C >/dev/null
 mkdir -p abx
-cp "$SRC" $C/_ab_kernels.hip
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result "$@" -c $C/_ab_kernels.hip -o /tmp/_ab_$NAME.o
-rm -f $C/_ab_kernels.hip
+# a copy next to the sources (their includes), one per variant: builds may run in parallel
+cp "$SRC" $C/_ab_$NAME.hip
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result "$@" -c $C/_ab_$NAME.hip -o /tmp/_ab_$NAME.o
+rm -f $C/_ab_$NAME.hip
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -o abx/$NAME.so /tmp/_ab_$NAME.o \
   $C/build/rs_sha256.hip.o $C/build/rs_engine.cpp.o $C/build/rs_coalescer.cpp.o $C/build/gf256.cpp.o \
   $C/build/rs_host_copy.cpp.o

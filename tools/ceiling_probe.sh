@@ -1,0 +1,20 @@
+#!/bin/bash
+# Compute-free ceilings of every K/M-sweep and config-3 leg on the shipped launch
+# shapes: bench.py --sweep-only runs twice on the same box, once
+# with the shipped librsgpu.so and once with its RS_PATTERN_ONLY=1 twin
+# (abx/pattern.so, built on the CPU by tools/build_ab.sh pattern ... -DRS_PATTERN_ONLY=1):
+# the same kernels, launches, tasks, loads and stores with the GF(2^8) arithmetic
+# replaced by one XOR per input dword.  tools/ceiling_summary.py pairs the legs.
+# Usage: tools/ceiling_probe.sh <tag>
+set -euo pipefail
+TAG=$1
+LIB=replication_erasurecoding_object_store_amd/librsgpu.so
+OUT=gpurun_out/ceiling_${TAG}
+mkdir -p "$OUT"
+cp $LIB /tmp/_librsgpu_keep.so
+trap 'cp /tmp/_librsgpu_keep.so $LIB' EXIT
+timeout -k 10 400 python3 bench.py --sweep-only --json-out "$OUT/shipped.json" > "$OUT/shipped.log" 2>&1
+cp abx/pattern.so $LIB
+timeout -k 10 400 python3 bench.py --sweep-only --json-out "$OUT/pattern.json" > "$OUT/pattern.log" 2>&1
+cp /tmp/_librsgpu_keep.so $LIB
+python3 tools/ceiling_summary.py "$OUT" "$TAG"

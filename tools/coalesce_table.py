@@ -1,8 +1,9 @@
-"""Markdown table of tools/run_coalesce_sizes.sh output: per object size, user
-GiB/s (and calls/s) of the CPU codec on 1 core and on the CPU quota, the coalesced
-GPU drop-in with blocking callers and with asynchronous calls.
+"""Markdown table of tools/run_drop_in.sh output: per object size, user GiB/s (and
+calls/s) of the CPU codec on 1 core and on the CPU quota, and of the coalesced GPU
+drop-in with blocking callers and with asynchronous calls, staged (caller memory)
+and in place (rs_host_alloc arena).
 
-Usage: python tools/coalesce_table.py <run_coalesce_sizes log>
+Usage: python tools/coalesce_table.py <run_drop_in log>
 """
 import json
 import sys
@@ -17,14 +18,15 @@ def main():
             continue
         r = json.loads(line)
         mode = r["mode"]
+        where = ", in place" if r.get("registered") == 2 else (", staged" if mode != "cpu" else "")
         if mode == "cpu":
             key = f"CPU codec, {r['threads']} thread{'s' if r['threads'] > 1 else ''}"
         elif mode == "coalesced":
-            key = f"GPU coalesced, {r['threads']} blocking callers"
+            key = f"GPU coalesced, {r['threads']} blocking callers{where}"
         elif mode == "async":
-            key = f"GPU async, {r['threads']} loops x {r['depth']} in flight"
+            key = f"GPU async, {r['threads']} loops x {r['depth']} in flight{where}"
         else:
-            key = f"{mode} {r['threads']}"
+            key = f"{mode} {r['threads']}{where}"
         if key not in cols:
             cols.append(key)
         rows[r["obj_bytes"]][key] = (r["user_GiBps"], r["calls_per_s"])
