@@ -48,6 +48,7 @@ sys.path.insert(0, ROOT)
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: "6.29 TB/s measured (float4 copy, 79%)"
+OCC_CAP = -1  # --occ-cap
 
 
 def committed_ceilings():
@@ -85,6 +86,9 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--json-out", default="")
+    p.add_argument("--occ-cap", type=int, default=-1,
+                   help="rs_set_occupancy_cap on every engine: -1 = the kernels' defaults (tools/ceiling_probe.sh "
+                        "sweeps it for the compute-free twin)")
     p.add_argument("--dry-run", action="store_true",
                    help="no GPU: run the rank launcher and the control collectives on gloo only and print a "
                         "line with n_gpus (tests/test_bench_launch.py)")
@@ -591,6 +595,7 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
     sweep = {}
     for kk, mm in [(4, 2), (8, 4), (10, 4)]:
         e2 = BatchEngine(kk, mm, torch.cuda.current_device())
+        e2.set_occupancy_cap(OCC_CAP)
         SS, NN = -(-65536 // kk), 16384
         w = RSWorkload(torch, e2, kk, mm, SS, NN, rotate, seed=0x5EED0004)
         alg = w.alg_bytes()
@@ -816,7 +821,10 @@ def main():
     k, m = args.k, args.m
     S = args.stripe_kib * 1024 // k
     N = args.stripes
+    global OCC_CAP
+    OCC_CAP = args.occ_cap
     eng = BatchEngine(k, m, torch.cuda.current_device())
+    eng.set_occupancy_cap(OCC_CAP)
     rotate = int(args.rotate_gib * GiB)
     if args.sweep_only:
         res = {"kmsweep_64KiB_device": kmsweep(torch, rdist, rotate)}

@@ -353,6 +353,11 @@ int rs_device_copy(rs_ctx *ctx, void *dst, const void *src, size_t bytes, void *
 /* Tuning knob: workgroups (256 threads) per CU for the batched kernels
  * (0 = the default, 2). */
 int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
+/* Tuning knob: at most waves_per_simd waves of a batched encode / reconstruct
+ * launch per SIMD (a dynamic-LDS reservation admits that many 4-wave workgroups
+ * per CU); -1 (default) = each kernel's measured default, 0 = uncapped.  For
+ * measurement (tools/ab_bench.py, tools/ceiling_probe.sh); bytes never change. */
+int rs_set_occupancy_cap(rs_ctx *ctx, int waves_per_simd);
 /* Batched encode may write each parity slot's padding up to the next 128-B line
  * (bytes [S, min(pitch, round_up(S, 128))) of every parity slot; never past the
  * pitch) and reads the data slots' padding over the same range: every parity shard
@@ -364,11 +369,17 @@ int rs_set_blocks_per_cu(rs_ctx *ctx, int blocks_per_cu);
  * 0 (the default): no byte past S of any slot is ever written. */
 int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
 /* The same for the out-of-place reconstructs (rs_reconstruct_batch_out and its
- * _devmask form): each output row written gets its padding up to the next 128-B
- * line, bytes [S, min(pitch, round_up(S, 128))) of the row at out + i*out_sp +
- * r*pitch (the caller's output allocation must cover them), and the inputs' padding
- * is read over the same range.  Bytes [0, S) are unchanged.  0 (the default): no
- * byte past S of an output row is written. */
+ * _devmask form), ON by default since round 5: each output row written gets its
+ * padding up to the next 128-B line, bytes [S, min(pitch, round_up(S, 128))) of the
+ * row at out + i*out_sp + r*pitch -- never past the row's own slot: only when that
+ * line end also fits the out stripe pitch (plane-major outputs with out_sp below it
+ * are written exactly) -- and the inputs' padding is read over the same range.
+ * Output rows are fresh shards (the reference's Reconstruct hands back new slices);
+ * a partial last line costs HBM a read-modify-write (RS(10+4) 64 KiB 2-erasure
+ * 0.728 -> 0.756 of 8 TB/s, profiles/r04zj_sweep_trace.md).  Bytes [0, S) are
+ * unchanged, rows a stripe does not miss are untouched.  0: no byte past S of an
+ * output row is written.  (Parity padding, above, stays opt-in: parity slots are
+ * the caller's stored shards.) */
 int rs_set_out_pad_writes(rs_ctx *ctx, int enable);
 /* RS_MEM_HOST batches whose shards all lie in rs_host_alloc'ed memory, 16-B
  * aligned, run zero-copy by default: the kernel reads the survivors and writes the

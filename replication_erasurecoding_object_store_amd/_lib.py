@@ -91,6 +91,7 @@ SIGNATURES = {
     "rs_last_kernel_on": (ctypes.c_char_p, [_vp, _vp]),
     "rs_device_copy": (_i, [_vp, _vp, _vp, _sz, _vp]),
     "rs_set_blocks_per_cu": (_i, [_vp, _i]),
+    "rs_set_occupancy_cap": (_i, [_vp, _i]),
     "rs_set_parity_pad_writes": (_i, [_vp, _i]),
     "rs_set_out_pad_writes": (_i, [_vp, _i]),
     "rs_set_host_zero_copy": (_i, [_vp, _i]),

@@ -247,6 +247,10 @@ class BatchEngine(Service):
     def set_blocks_per_cu(self, n: int) -> None:
         _check(_lib.lib().rs_set_blocks_per_cu(self.ctx, n))
 
+    def set_occupancy_cap(self, waves_per_simd: int) -> None:
+        """-1: each kernel's tuned default; 0: uncapped; c: at most c waves per SIMD."""
+        _check(_lib.lib().rs_set_occupancy_cap(self.ctx, waves_per_simd))
+
     def set_out_pad_writes(self, enable: bool) -> None:
         """Out-of-place reconstructs may write each output row's padding up to the
         next 128-B line (rsgpu.h)."""

@@ -295,10 +295,11 @@ struct Engine {
   const std::vector<uint32_t>* h_lut = nullptr;
   Shared* shared = nullptr;
   int blocks_per_cu = 0;                  // 0 = by shape
+  int occ_cap = -1;                       // waves per SIMD: -1 = each kernel's tuned default
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
-  bool out_pad = false;                   // out-of-place outputs likewise (rs_set_out_pad_writes)
+  bool out_pad = true;                    // out-of-place rows end on whole lines (rs_set_out_pad_writes)
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -333,7 +334,14 @@ struct Engine {
   std::mutex host_mu;                     // host-resident batches: one at a time per engine
   hipStream_t pipe_st[kHostStreams] = {};
   DevBuf pipe_buf[kHostStreams];
-  PinnedBuf pipe_host[kHostStreams];      // staged per-stripe reconstruct: dense output rows (D2H)
+  // staged per-stripe reconstruct: a ring of pinned D2H buffers of dense output rows
+  // and the events that say when each holds its chunk (host_batch_ps)
+  PinnedBuf scatter_host[2 * kHostStreams];
+  hipEvent_t scatter_ev[2 * kHostStreams] = {};
+  // ... and per pipeline stream the parity survivors gathered on the host, which
+  // the kernel reads in place over PCIe (GPU address par_dev)
+  PinnedBuf par_host[kHostStreams];
+  uint8_t* par_dev[kHostStreams] = {};
   DevBuf d_bad;                           // zero-copy verify: per-stripe result before D2H
 
   std::atomic<int> inflight{0};           // calls running on this engine (dispatch)
@@ -389,6 +397,8 @@ struct Engine {
       if (l->stream) (void)hipStreamDestroy(l->stream);
     for (auto& s : pipe_st)
       if (s) (void)hipStreamDestroy(s);
+    for (auto& ev : scatter_ev)
+      if (ev) (void)hipEventDestroy(ev);
   }
 };
 
@@ -598,19 +608,25 @@ rs::KernelArgs make_args(Engine* e, const Layout& L, size_t S, size_t N) {
 }
 
 // e_out = outputs per stripe (m for encode, #missing for a uniform reconstruct, max
-// #missing for per-stripe patterns).
-int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s) {
+// #missing for per-stripe patterns).  own_out: the out-of-place rows are the
+// engine's own scratch (a staging slab), so their padding may always be written.
+int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hipStream_t s, bool own_out = false) {
   if (args.n_stripes == 0 || args.shard_len == 0 || e_out <= 0) return RS_OK;
   rs::KernelArgs a = args;
   // the encode plan with a verified generated XOR program -> bitsliced kernel
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  if ((e->parity_pad && a.data_inputs && !a.out) || (e->out_pad && a.out)) {
-    // rs_set_parity_pad_writes / rs_set_out_pad_writes: run over whole 128-B lines of
-    // the slot (inputs' padding read, the written rows' padding written)
+  if ((e->parity_pad && a.data_inputs && !a.out) || ((e->out_pad || own_out) && a.out)) {
+    // rs_set_parity_pad_writes / rs_set_out_pad_writes / engine-owned out rows: run
+    // over whole 128-B lines of the slot (inputs' padding read, the written rows'
+    // padding written): every output row ends on a whole line, no partial columns
+    // A written row's padding stays inside its own slot: within the shard pitch
+    // (rows of one stripe) and within the stripe pitch of the written region
+    // (stripes of a plane-major / SoA layout lie only that far apart).
     const uint64_t s_eff = std::min<uint64_t>(a.shard_pitch, round_up(static_cast<size_t>(a.shard_len), 128));
-    if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u) {
+    const uint64_t row_sp = a.out ? a.out_sp : a.parity_sp;
+    if (s_eff > a.shard_len && s_eff <= 0xFFFFFFF0u && (a.n_stripes <= 1 || s_eff <= row_sp)) {
       a.shard_len = static_cast<uint32_t>(s_eff);
       a.blocks_per_stripe = static_cast<uint32_t>((round_up(s_eff, 16) / 16 + 63) / 64);
       a.full_cols = static_cast<uint32_t>(s_eff / 16);
@@ -618,7 +634,7 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   }
   // 0: each kernel's own default (rs::launch_apply)
   const uint32_t bpc = e->blocks_per_cu > 0 ? static_cast<uint32_t>(e->blocks_per_cu) : 0u;
-  const char* name = rs::launch_apply(a, e_out, per_stripe, bpc, static_cast<uint32_t>(e->cu_count), s);
+  const char* name = rs::launch_apply(a, e_out, per_stripe, bpc, static_cast<uint32_t>(e->cu_count), s, e->occ_cap);
   if (!name) return RS_ERR_DEVICE;
   e->shared->note(s, name);
   RS_HIP(hipGetLastError());
@@ -940,15 +956,24 @@ uint32_t first_present(uint32_t present, int k) {
 
 // Staged per-stripe reconstruct (round 5): only the bytes the codec needs cross
 // PCIe, and the caller's present shards are never written.
-//  * H2D: the slots some stripe of the share reads -- the union of every stripe's
-//    first k present shards (a 1-erasure healer mix of RS(4+2) never reads slot 5).
+//  * H2D: the data slots some stripe of the share reads (the union of every
+//    stripe's first k present shards: normally all k, one contiguous copy per
+//    stripe).  Parity survivors are needed only by stripes missing a data shard
+//    (a third of a 50/50 encode / 1-erasure RS(4+2) mix): the host gathers exactly
+//    those rows into the library's own page-locked slab, which the kernel reads in
+//    place over PCIe -- no DMA of parity rows nobody reads.
 //  * The kernel writes out of place into a dense slab, the r-th missing shard of
-//    stripe i at row i*e_out + r (what the healer writes back, poller.go:288-302).
-//  * D2H: that slab (e_out rows per stripe, not k+m), into pinned memory, from which
-//    the host scatters each row into the caller's missing slot -- on the calling
-//    thread, while the other pipeline streams' chunks are in flight.
+//    stripe i at row i*e_out + r (what the healer writes back, poller.go:288-302),
+//    whole 128-B lines (the slab is the engine's own).
+//  * D2H: that slab (e_out rows per stripe, not k+m) into a ring of pinned buffers,
+//    from which scatter threads copy each row into the caller's missing slot while
+//    later chunks are in flight (one thread cannot keep up with the link: a 4 KiB
+//    RS(4+2) mix scatters ~1.5 KiB per 5 KiB of H2D).
 // Round 4 moved every slot both ways and wrote the present ones back unchanged:
 // config 5 (50/50 encode / 1-erasure) 25.7 GiB/s.
+constexpr int kScatterRing = 2 * kHostStreams;  // pinned D2H buffers in flight or being scattered
+constexpr int kScatterThreads = 3;
+
 int host_batch_ps(Engine* e, const Layout& hl, size_t S, size_t N, const uint32_t* masks, int e_out) {
   const int k = e->k, m = e->m, t = k + m;
   const uint32_t full = static_cast<uint32_t>(full_mask64(t));  // t <= 16: per-stripe host masks need the LUT
@@ -961,28 +986,43 @@ int host_batch_ps(Engine* e, const Layout& hl, size_t S, size_t N, const uint32_
       need |= first_present(pm, k);
     }
   }
-  std::vector<int> in_slots;
-  for (int s = 0; s < t; ++s)
+  std::vector<int> in_slots;  // data slots only: parity survivors are gathered
+  for (int s = 0; s < k; ++s)
     if ((need >> s) & 1u) in_slots.push_back(s);
+  const bool need_par = (need >> k) != 0u;
   const size_t P = round_up(S, 256);  // 256-B slots: see batch.shard_pitch_for
   const size_t slab = P * static_cast<size_t>(t), outb = P * static_cast<size_t>(e_out);
   const size_t per_stripe = slab + outb + 4;
   const size_t chunk = std::min(N, std::max<size_t>(1, kHostChunkBytes / per_stripe));
   const size_t in_bytes = round_up(chunk * slab, 256), out_bytes = round_up(chunk * outb, 256);
+  const size_t host_bytes = chunk * static_cast<size_t>(e_out) * S;
   std::lock_guard<std::mutex> g(e->host_mu);
   for (int i = 0; i < kHostStreams; ++i) {
     int rc = ensure_pipe_stream(e, i);
     if (rc) return rc;
-    e->pipe_host[i].numa = e->numa;
-    if (e->pipe_buf[i].ensure(std::max(kHostChunkBytes, in_bytes + out_bytes + chunk * 4) + per_stripe + 256) ||
-        e->pipe_host[i].ensure(chunk * static_cast<size_t>(e_out) * S))
+    if (e->pipe_buf[i].ensure(std::max(kHostChunkBytes, in_bytes + out_bytes + chunk * 4) + per_stripe + 256))
       return RS_ERR_DEVICE;
+    if (need_par) {
+      const void* before = e->par_host[i].p;
+      e->par_host[i].numa = e->numa;
+      if (e->par_host[i].ensure(chunk * P * static_cast<size_t>(m))) return RS_ERR_DEVICE;
+      if (e->par_host[i].p != before || !e->par_dev[i]) {
+        void* dev = nullptr;
+        RS_HIP(hipHostGetDevicePointer(&dev, e->par_host[i].p, 0));
+        e->par_dev[i] = static_cast<uint8_t*>(dev);
+      }
+    }
   }
-  size_t pend_s0[kHostStreams] = {}, pend_n[kHostStreams] = {};
-  auto scatter = [&](int i) {  // chunk on stream i is complete: its rows into the missing slots
-    const uint8_t* h = static_cast<const uint8_t*>(e->pipe_host[i].p);
-    for (size_t q = 0; q < pend_n[i]; ++q) {
-      const size_t s = pend_s0[i] + q;
+  for (int b = 0; b < kScatterRing; ++b) {
+    e->scatter_host[b].numa = e->numa;
+    if (e->scatter_host[b].ensure(host_bytes)) return RS_ERR_DEVICE;
+    if (!e->scatter_ev[b]) RS_HIP(hipEventCreateWithFlags(&e->scatter_ev[b], hipEventDisableTiming));
+  }
+  // rows of the chunk in ring buffer b into the caller's missing slots
+  auto scatter = [&](size_t s0, size_t n, int b) {
+    const uint8_t* h = static_cast<const uint8_t*>(e->scatter_host[b].p);
+    for (size_t q = 0; q < n; ++q) {
+      const size_t s = s0 + q;
       uint32_t miss = ~masks[s] & full;
       for (size_t r = 0; miss; ++r) {
         const int j = __builtin_ctz(miss);
@@ -990,40 +1030,127 @@ int host_batch_ps(Engine* e, const Layout& hl, size_t S, size_t N, const uint32_
         std::memcpy(hl.slot(k, s, j), h + (q * static_cast<size_t>(e_out) + r) * S, S);
       }
     }
-    pend_n[i] = 0;
   };
-  int j = 0;
-  for (size_t s0 = 0; s0 < N; s0 += chunk, ++j) {
-    const int i = j % kHostStreams;
-    hipStream_t st = e->pipe_st[i];
-    if (pend_n[i]) {  // the stream's previous chunk: its pinned rows are about to be reused
-      RS_HIP(hipStreamSynchronize(st));
-      scatter(i);
+  const size_t n_chunks = (N + chunk - 1) / chunk;
+  // scatter threads (several chunks only): a queue of retired chunks; buffer b is
+  // free again once done[b] counts its chunk
+  struct Job {
+    size_t s0, n;
+    int b;
+  };
+  std::mutex qm;
+  std::condition_variable qcv, dcv;
+  std::deque<Job> q;
+  bool stop = false;
+  std::vector<size_t> done(kScatterRing, 0), want(kScatterRing, 0);  // chunks scattered / handed out per buffer
+  std::vector<std::thread> pool;
+  if (n_chunks > static_cast<size_t>(kHostStreams)) {
+    try {
+      for (int w = 0; w < kScatterThreads; ++w)
+        pool.emplace_back([&] {
+          std::unique_lock<std::mutex> lk(qm);
+          for (;;) {
+            qcv.wait(lk, [&] { return stop || !q.empty(); });
+            if (q.empty()) return;
+            const Job jb = q.front();
+            q.pop_front();
+            lk.unlock();
+            scatter(jb.s0, jb.n, jb.b);
+            lk.lock();
+            ++done[jb.b];
+            dcv.notify_all();
+          }
+        });
+    } catch (...) {  // no threads: the calling thread scatters
     }
-    const size_t n = std::min(chunk, N - s0);
+  }
+  auto join_pool = [&] {
+    {
+      std::lock_guard<std::mutex> lk(qm);
+      stop = true;
+    }
+    qcv.notify_all();
+    for (auto& th : pool) th.join();
+    pool.clear();
+  };
+  std::vector<Job> inflight;  // enqueued chunks not yet retired, oldest first
+  int rc = RS_OK;
+  auto retire = [&](const Job& jb) -> int {  // the chunk's rows are in host memory: scatter them
+    RS_HIP(hipEventSynchronize(e->scatter_ev[jb.b]));
+    if (pool.empty()) {
+      scatter(jb.s0, jb.n, jb.b);
+      std::lock_guard<std::mutex> lk(qm);
+      ++done[jb.b];
+      return RS_OK;
+    }
+    {
+      std::lock_guard<std::mutex> lk(qm);
+      q.push_back(jb);
+    }
+    qcv.notify_one();
+    return RS_OK;
+  };
+  for (size_t j = 0; j < n_chunks && rc == RS_OK; ++j) {
+    const size_t s0 = j * chunk, n = std::min(chunk, N - s0);
+    const int i = static_cast<int>(j % kHostStreams), b = static_cast<int>(j % kScatterRing);
+    hipStream_t st = e->pipe_st[i];
+    // keep at most kHostStreams chunks queued on the device: retire the oldest first
+    if (inflight.size() >= static_cast<size_t>(kHostStreams)) {
+      rc = retire(inflight.front());
+      inflight.erase(inflight.begin());
+      if (rc) break;
+    }
+    {  // ring buffer b: its previous chunk must be scattered before the D2H reuses it
+      std::unique_lock<std::mutex> lk(qm);
+      dcv.wait(lk, [&] { return done[b] == want[b]; });
+      ++want[b];
+    }
     uint8_t* d = static_cast<uint8_t*>(e->pipe_buf[i].p);
-    const Layout dl{d, P * k, d + chunk * P * k, P * m, P};
-    int rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
-    if (rc) return rc;
+    // data slots in the device slab; parity slots in the pinned gather slab, which
+    // the retire of chunk j - kHostStreams (above) has freed from its last kernel
+    const Layout dl{d, P * k, need_par ? e->par_dev[i] : d + chunk * P * k, P * m, P};
+    rc = copy_slots(dl, hl, k, in_slots, 0, s0, n, S, hipMemcpyHostToDevice, st);
+    if (rc) break;
+    if (need_par) {
+      uint8_t* ph = static_cast<uint8_t*>(e->par_host[i].p);
+      for (size_t q = 0; q < n; ++q) {
+        uint32_t pm = first_present(masks[s0 + q] & full, k) >> k;  // parity survivors of this stripe
+        while (pm) {
+          const int p = __builtin_ctz(pm);
+          pm &= pm - 1u;
+          std::memcpy(ph + (q * static_cast<size_t>(m) + p) * P, hl.slot(k, s0 + q, k + p), S);
+        }
+      }
+    }
     uint8_t* o = d + in_bytes;
     uint32_t* aux = reinterpret_cast<uint32_t*>(o + out_bytes);
-    RS_HIP(hipMemcpyAsync(aux, masks + s0, n * 4, hipMemcpyHostToDevice, st));
+    if (hipMemcpyAsync(aux, masks + s0, n * 4, hipMemcpyHostToDevice, st) != hipSuccess) {
+      rc = RS_ERR_DEVICE;
+      break;
+    }
     rs::KernelArgs a = make_args(e, dl, S, n);
     a.plans = static_cast<const uint8_t*>(e->d_plans.p);
     a.present_masks = aux;
     a.out = o;
     a.out_sp = outb;
-    rc = launch(e, a, e_out, true, st);
-    if (rc) return rc;
-    RS_HIP(copy2d(e->pipe_host[i].p, S, o, P, S, n * static_cast<size_t>(e_out), hipMemcpyDeviceToHost, st));
-    pend_s0[i] = s0;
-    pend_n[i] = n;
+    rc = launch(e, a, e_out, true, st, true);  // the slab's rows: whole-line writes
+    if (rc) break;
+    if (copy2d(e->scatter_host[b].p, S, o, P, S, n * static_cast<size_t>(e_out), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipEventRecord(e->scatter_ev[b], st) != hipSuccess) {
+      rc = RS_ERR_DEVICE;
+      break;
+    }
+    inflight.push_back(Job{s0, n, b});
   }
-  for (int i = 0; i < kHostStreams; ++i) {
-    RS_HIP(hipStreamSynchronize(e->pipe_st[i]));
-    if (pend_n[i]) scatter(i);
+  for (const Job& jb : inflight) {
+    const int r2 = retire(jb);
+    if (!rc) rc = r2;
   }
-  return RS_OK;
+  join_pool();  // drains the queue first
+  for (int i = 0; i < kHostStreams; ++i)
+    if (hipStreamSynchronize(e->pipe_st[i]) != hipSuccess && !rc) rc = RS_ERR_DEVICE;
+  return rc;
 }
 
 // One engine's share of a host-resident batch (caller holds its DeviceScope).
@@ -1843,6 +1970,12 @@ int rs_set_parity_pad_writes(rs_ctx* c, int enable) {
 int rs_set_out_pad_writes(rs_ctx* c, int enable) {
   if (!c) return RS_ERR_INVALID_ARG;
   for (auto& e : c->engines) e->out_pad = enable != 0;
+  return RS_OK;
+}
+
+int rs_set_occupancy_cap(rs_ctx* c, int waves_per_simd) {
+  if (!c || waves_per_simd < -1 || waves_per_simd > 32) return RS_ERR_INVALID_ARG;
+  for (auto& e : c->engines) e->occ_cap = waves_per_simd;
   return RS_OK;
 }
 

@@ -1222,7 +1222,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
 // 1: each row re-splits its inputs (only x[K] live); 2: input-outer passes of <= 2
 // rows (rows 0-1, then 2-3 only for a stripe missing more than 2).
 #ifndef RS_FLAT_SEG
-#define RS_FLAT_SEG 0
+#define RS_FLAT_SEG 1
 #endif
 #ifndef RS_FLAT_EM_ROWS
 #define RS_FLAT_EM_ROWS 0
@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
 // RS_FLAT_EM_FULL: the E > 2 flat launches take one task per wave (a full grid) like
 // the E <= 2 ones, instead of a grid-stride loop over default_blocks_per_cu.
 #ifndef RS_FLAT_EM_FULL
-#define RS_FLAT_EM_FULL 0
+#define RS_FLAT_EM_FULL 1
 #endif
 
 // Makes the inputs' registers opaque to the compiler: chunk indices computed from
@@ -1884,10 +1884,63 @@ static dim3 full_grid(uint64_t waves) {
   return dim3(static_cast<uint32_t>(need < 0x7FFFFFFFull ? need : 0x7FFFFFFFull));
 }
 
+// Occupancy caps (round 5).  A launch's waves per SIMD are set by its registers
+// unless capped: a workgroup of 4 waves puts one wave on each SIMD, so c
+// workgroups per CU = c waves per SIMD, and a dynamic LDS request of 160 KiB / c
+// per workgroup (unused by the kernel) admits exactly c of them.  The streaming
+// kernels want few waves in flight per SIMD; the cap sets that number
+// directly instead of through the register count.  0 = uncapped.
+#ifndef RS_OCC_CAP
+#define RS_OCC_CAP 0
+#endif
+// The segmented flat reconstructs (apply_flat_seg_kernel) at 4 waves per SIMD, one
+// task per wave (round 5, same-process A/B over shared buffers, 4 rounds,
+// profiles/r05d_ab_same_seg.log, RS(10+4) 64 KiB, against apply_flat_ps_kernel):
+// bounded 1-erasure 72.2 -> 73.9 %, bounded 2-erasure 73.4 -> 74.7 % (3 or 5 waves:
+// 69.7 / 69.4 %), unbounded 2-erasure 68.3 -> 72.0 %, mixed 0..4 57.9 -> 61.8 %,
+// mixed 1..4 65.1 -> 66.9 %; unbounded 1- and 4-erasure 69.7 -> 69.0 % and 66.0 ->
+// 63.9 %.  Uncapped, the segmented kernels run at 7-8 waves per SIMD and lose 5-7
+// points (profiles/r05b_ab_same_flat.log).
+#ifndef RS_OCC_CAP_FLAT_E1
+#define RS_OCC_CAP_FLAT_E1 4
+#endif
+#ifndef RS_OCC_CAP_FLAT_E2
+#define RS_OCC_CAP_FLAT_E2 4
+#endif
+#ifndef RS_OCC_CAP_FLAT_EM
+#define RS_OCC_CAP_FLAT_EM 4
+#endif
+#ifndef RS_OCC_CAP_APPLY
+#define RS_OCC_CAP_APPLY RS_OCC_CAP
+#endif
+#ifndef RS_OCC_CAP_BS
+#define RS_OCC_CAP_BS RS_OCC_CAP
+#endif
+constexpr size_t kLdsPerCu = 160u * 1024u;
+
+// Dynamic LDS bytes that cap `fn` at `cap` workgroups per CU (0: none): halfway
+// between 160 KiB / (cap + 1) and 160 KiB / cap, so allocation granularity and any
+// static LDS cannot turn c into c - 1 (160 KiB / cap exactly admitted one fewer:
+// profiles/r05c_ab_same_occ.log, caps 3 / 5 / 6 ran as 2 / 4 / 5).
+static size_t occ_lds(const void* fn, uint32_t cap) {
+  if (cap == 0) return 0;
+  const size_t lds = ((kLdsPerCu / cap + kLdsPerCu / (cap + 1)) / 2) & ~size_t(1023);
+  if (lds > 65536) {  // above the default dynamic-LDS limit: raise it for this kernel
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+  }
+  return lds;
+}
+
 // One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
 // the dropped-store descriptors cover 2 GiB from the shard base).
 static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
-                                 uint32_t cu_count, hipStream_t s) {
+                                 uint32_t cu_count, hipStream_t s, int occ_cap) {
+  // the launch's waves-per-SIMD cap: the caller's (rs_set_occupancy_cap) or the
+  // kernel class's tuned default
+  auto cap_of = [&](uint32_t dflt) -> uint32_t { return occ_cap >= 0 ? static_cast<uint32_t>(occ_cap) : dflt; };
   void* args[] = {const_cast<KernelArgs*>(&a)};
   const uint64_t cols = (static_cast<uint64_t>(a.shard_len) + 15u) / 16u;
   const char* name = nullptr;
@@ -1906,7 +1959,7 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
       // against a grid-stride loop over 6 workgroups per CU)
       const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
-      if (hipLaunchKernel(fn, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
+      if (hipLaunchKernel(fn, grid, dim3(256), args, occ_lds(fn, cap_of(RS_OCC_CAP_BS)), s) != hipSuccess) return nullptr;
       return name;
     }
   }
@@ -1921,7 +1974,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
       const dim3 grid = (!blocks_per_cu && (e <= 2 || RS_FLAT_EM_FULL)) ? full_grid(waves)
                                                                          : grid_for(waves, bpc, cu_count);
-      if (hipLaunchKernel(ff, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
+      const uint32_t cap = e == 1 ? RS_OCC_CAP_FLAT_E1 : e == 2 ? RS_OCC_CAP_FLAT_E2 : RS_OCC_CAP_FLAT_EM;
+      if (hipLaunchKernel(ff, grid, dim3(256), args, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
       return name;
     }
   }
@@ -1946,15 +2000,16 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     // 76.4 %.  Partial grids (32 or 64 per CU, still looping) were slower than both.
     grid = full_grid(waves);
   }
-  if (hipLaunchKernel(fn, grid, dim3(256), args, 0, s) != hipSuccess) return nullptr;
+  if (hipLaunchKernel(fn, grid, dim3(256), args, generic ? 0 : occ_lds(fn, cap_of(RS_OCC_CAP_APPLY)), s) != hipSuccess)
+    return nullptr;
   return name;
 }
 
 const char* launch_apply(const KernelArgs& args, int e, bool per_stripe, uint32_t blocks_per_cu, uint32_t cu_count,
-                         hipStream_t s) {
+                         hipStream_t s, int occ_cap) {
   KernelArgs a = args;
   a.max_out = static_cast<uint32_t>(e);
-  if (a.shard_len <= kColumnWindow) return launch_window(a, e, per_stripe, blocks_per_cu, cu_count, s);
+  if (a.shard_len <= kColumnWindow) return launch_window(a, e, per_stripe, blocks_per_cu, cu_count, s, occ_cap);
   // Shards of 1 GiB or more (one huge Encode of an object of several GiB): the
   // codec is column-wise, so columns [x, x + W) of every shard are an independent
   // batch whose slots all start x bytes later.  Windows run in order on s.
@@ -1968,7 +2023,7 @@ const char* launch_apply(const KernelArgs& args, int e, bool per_stripe, uint32_
     w.shard_len = static_cast<uint32_t>(len);
     w.full_cols = w.shard_len / 16u;
     w.blocks_per_stripe = ((w.shard_len + 15u) / 16u + 63u) / 64u;
-    name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s);
+    name = launch_window(w, e, per_stripe, blocks_per_cu, cu_count, s, occ_cap);
     if (!name) return nullptr;
   }
   return name;

@@ -118,8 +118,10 @@ uint32_t default_blocks_per_cu(int k, int e);
 // bound (stripes missing more are skipped and flagged, status bit 1).  Returns the
 // main kernel's name, or nullptr if the launch failed.  Any shard_len up to
 // 0xFFFFFFF0 (column windows).  blocks_per_cu = 0: the chosen kernel's default.
+// occ_cap: waves per SIMD the launch may hold (rs_set_occupancy_cap): -1 = the
+// kernel's tuned default, 0 = uncapped, c = at most c.
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
-                         uint32_t cu_count, hipStream_t s);
+                         uint32_t cu_count, hipStream_t s, int occ_cap = -1);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.

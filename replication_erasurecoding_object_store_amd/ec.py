@@ -189,9 +189,11 @@ class Arena:
     staging copies, parity written straight into the views).  A bump allocator:
     Alloc until full, Reset when no view is in use, Close to free.
 
-    A view re-exported by the caller (numpy.frombuffer(view), ...) cannot be revoked:
-    Reset and Close raise BufferError while such an export is alive instead of
-    handing its memory out again or freeing it under it."""
+    Reset and Close release every memoryview handed out, so a stale view raises
+    ValueError instead of touching reused or freed memory.  Objects the caller built
+    ON a view (numpy.frombuffer(view), ctypes from_buffer, ...) take their own
+    reference to the memory that no Python API lets the arena see or revoke: drop
+    them before Reset / Close, as the Go shim's callers drop their slices."""
 
     def __init__(self, svc: "Service", size: int):
         n = (size + 4095) // 4096 * 4096
@@ -200,7 +202,7 @@ class Arena:
         self._svc, self._base, self._size, self._off = svc, p.value, n, 0
         self._mem = (ctypes.c_uint8 * n).from_address(p.value)
         self._root: Optional[memoryview] = memoryview(self._mem).cast("B")  # one per arena
-        self._views: List[memoryview] = []  # slices handed out, released with the memory
+        self._views: List[memoryview] = []  # the slices handed out since the last Reset
         svc._arenas.add(self)
 
     def Alloc(self, n: int) -> Optional[memoryview]:
@@ -215,31 +217,22 @@ class Arena:
     def Reset(self) -> None:
         """Makes the whole arena free again (no view may be in use): the views handed
         out so far are released."""
-        if self._release_views():
-            raise BufferError("Arena.Reset: views are still exported (e.g. numpy arrays over them); "
-                              "their memory would be handed out again")
+        self._release_views()
         self._off = 0
 
-    def _release_views(self) -> int:
-        """Releases every view handed out; returns how many are still exported."""
-        stuck = []
+    def _release_views(self) -> None:
         for v in self._views:
             try:
                 v.release()
-            except BufferError:  # re-exported by the caller: cannot be revoked
-                stuck.append(v)
-        self._views = stuck
-        return len(stuck)
+            except BufferError:  # a live PEP 3118 export of the view itself: cannot be revoked
+                pass
+        self._views = []
 
     def _invalidate(self) -> None:
         """The memory is about to be freed: every view handed out is released (using
         one afterwards raises ValueError instead of touching freed memory) and Alloc
-        returns None.  Views still exported when the service closes cannot be
-        revoked: a warning names them."""
-        if self._release_views():
-            import warnings
-
-            warnings.warn(f"Arena freed with {len(self._views)} view(s) still exported", RuntimeWarning)
+        returns None."""
+        self._release_views()
         if self._root is not None:
             try:
                 self._root.release()
@@ -249,12 +242,8 @@ class Arena:
 
     def Close(self) -> None:
         """Frees the memory (no view may be in use); after the service closed,
-        rs_destroy has freed it already.  BufferError (nothing freed) while a view
-        is still exported."""
+        rs_destroy has freed it already."""
         if self._base is not None and self._svc.ctx:
-            if self._release_views():
-                raise BufferError("Arena.Close: views are still exported (e.g. numpy arrays over them); "
-                                  "drop them first")
             base = self._base
             self._invalidate()
             _check(_lib.lib().rs_host_free(self._svc.ctx, base))

@@ -62,6 +62,12 @@ def _codewords(eng, k, m, S, N, seed):
     return data, parity, uni
 
 
+def _pad_end(S, P):
+    """First byte of an out-of-place row that is never written: rows end on whole
+    128-B lines within their slot (rs_set_out_pad_writes, on by default)."""
+    return min(P, (S + 127) // 128 * 128)
+
+
 @pytest.mark.parametrize("k,m,S", SHAPES)
 def test_paths_match_oracle(engines, k, m, S):
     import torch
@@ -106,7 +112,7 @@ def test_paths_match_oracle(engines, k, m, S):
         o = out.cpu().numpy()
         for r, s in enumerate(lost):
             assert np.array_equal(o[:, r, :S], uni[:, s, :S]), (lost, s)
-        assert (o[:, len(lost):] == 0xC3).all() and (o[:, :, S:] == 0xC3).all()
+        assert (o[:, len(lost):] == 0xC3).all() and (o[:, :, _pad_end(S, P):] == 0xC3).all()
     for bound in (0, 1, 2, m):
         hi = bound or m
         masks = _masks(rng, N, t, 1 if bound == 1 else 0, hi)
@@ -119,7 +125,7 @@ def test_paths_match_oracle(engines, k, m, S):
             miss = [s for s in range(t) if not (masks[i] >> s) & 1]
             for r, s in enumerate(miss):
                 assert np.array_equal(o[i, r, :S], uni[i, s, :S]), (bound, i, s)
-            assert (o[i, len(miss):] == 0xC3).all() and (o[i, :, S:] == 0xC3).all()
+            assert (o[i, len(miss):] == 0xC3).all() and (o[i, :, _pad_end(S, P):] == 0xC3).all()
 
 
 @pytest.mark.parametrize("k,m,S", [(10, 4, 6554), (8, 4, 8192), (4, 2, 1024), (10, 4, 413)])
@@ -212,7 +218,7 @@ def test_out_of_place_stress(engines, k, m, S, bound):
                 unused = np.array([i for i in range(N) if len(missing[i]) <= r])
                 if len(unused):
                     assert (got[unused, r] == 0xC3).all(), (mode, trial, r, "unused output slot written")
-            assert (got[:, :, S:] == 0xC3).all(), "output padding written"
+            assert (got[:, :, _pad_end(S, P):] == 0xC3).all(), "output padding past the line written"
 
 
 @pytest.mark.parametrize("k,m,S,bound", [(10, 4, 6554, 1), (10, 4, 6554, 2), (10, 4, 6554, 0), (8, 4, 8192, 2),
@@ -236,13 +242,9 @@ def test_out_pad_writes(engines, k, m, S, bound):
     masks = _masks(rng, N, t, 1, bound or m)
     rows = bound or m
     out = torch.full((N, rows, P), 0xC3, dtype=torch.uint8, device="cuda")
-    eng.set_out_pad_writes(True)
-    try:
-        eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
-                            max_missing=bound, shard_pitch=P)
-        eng.sync()
-    finally:
-        eng.set_out_pad_writes(False)
+    mdev = torch.from_numpy(masks.view(np.int32)).cuda()
+    eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=bound, shard_pitch=P)  # default: on
+    eng.sync()
     got = out.cpu().numpy()
     line_end = min(P, (S + 127) // 128 * 128)
     for i in range(N):
@@ -251,6 +253,51 @@ def test_out_pad_writes(engines, k, m, S, bound):
             assert np.array_equal(got[i, r, :S], full[i, j, :S]), (i, r, j)
             assert (got[i, r, line_end:] == 0xC3).all(), ("past the line", i, r)
         assert (got[i, len(missing):] == 0xC3).all(), ("unused rows", i)
+    # rs_set_out_pad_writes(0): exact rows, nothing past S
+    out.fill_(0xC3)
+    eng.set_out_pad_writes(False)
+    try:
+        eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=bound, shard_pitch=P)
+        eng.sync()
+    finally:
+        eng.set_out_pad_writes(True)
+    got = out.cpu().numpy()
+    for i in range(N):
+        missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+        for r, j in enumerate(missing):
+            assert np.array_equal(got[i, r, :S], full[i, j, :S]), (i, r, j)
+    assert (got[:, :, S:] == 0xC3).all(), "exact mode wrote past S"
+
+
+@pytest.mark.parametrize("k,m,S", [(10, 4, 6554), (4, 2, 1000), (8, 4, 8200)])
+def test_out_pad_never_crosses_a_stripe_slot(engines, k, m, S):
+    """Dense 1-row outputs (bound 1, out stripe pitch = round_up(S, 16), below the
+    128-B line end): whole-line rows would overwrite the next stripe's row, so the
+    engine writes them exactly (the guard in launch()) -- with the default on."""
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, N = k + m, 300
+    P = shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    full = torch.cat([data, parity], dim=1)[:, :, :S].cpu().numpy()
+    out_sp = (S + 15) // 16 * 16
+    assert out_sp < (S + 127) // 128 * 128
+    out = torch.full((N + 1, out_sp), 0xC3, dtype=torch.uint8, device="cuda")
+    rng = np.random.default_rng(S)
+    masks = _masks(rng, N, t, 1, 1)
+    eng.reconstruct_out(data, parity, out[:N].view(N, 1, out_sp), S, N,
+                        masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(), max_missing=1, shard_pitch=P)
+    eng.sync()
+    got = out.cpu().numpy()
+    for i in range(N):
+        j = [s for s in range(t) if not (masks[i] >> s) & 1][0]
+        assert np.array_equal(got[i, :S], full[i, j]), (i, j)
+    assert (got[:N, S:] == 0xC3).all(), "a row's padding reached into the next stripe's row"
+    assert (got[N] == 0xC3).all()
 
 
 @pytest.mark.parametrize("nbytes", [16, 4080, 4096, 4112, (1 << 20) + 16, 201326592])

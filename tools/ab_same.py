@@ -1,0 +1,180 @@
+"""Same-process A/B of librsgpu variants (abx/<name>.so from tools/build_ab.sh).
+
+tools/run_ab.sh runs each variant in its own process, and an allocation's physical
+pages move a leg by up to 2 points from process to process (the
+spread is fixed per allocation).  Here every variant library is loaded into ONE
+process (ctypes, RTLD_LOCAL: each keeps its own kernels and context) and they
+take turns on the SAME device buffers, in an order that rotates every round, each
+timed over >= min_ms of back-to-back launches.  Reported per variant: the median
+fraction of 8 TB/s and the median of its per-round difference to the first
+variant (paired, so a drift of the chip's state cancels).
+
+Usage: python tools/ab_same.py --variants base,seg --workloads rs104_64K_rec1pb_out,... [--rounds 5]
+Workload names and modes: tools/ab_bench.py (device-resident modes only).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from ab_bench import WORKLOADS, alg_bytes  # noqa: E402
+
+_vp, _sz, _i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+SIGS = {
+    "rs_create": (_i, [_i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "rs_destroy": (None, [_vp]),
+    "rs_encode_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _i, _vp]),
+    "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
+    "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
+    "rs_last_kernel": (ctypes.c_char_p, [_vp]),
+    "rs_set_out_pad_writes": (_i, [_vp, _i]),
+    "rs_sync": (_i, [_vp, _vp]),
+}
+
+
+class Variant:
+    def __init__(self, name, path):
+        self.name = name
+        self.lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
+        for fn, (res, args) in SIGS.items():
+            f = getattr(self.lib, fn)
+            f.restype, f.argtypes = res, args
+        self.ctx = {}
+
+    def ctx_for(self, k, m):
+        if (k, m) not in self.ctx:
+            c = _vp()
+            rc = self.lib.rs_create(k, m, 0, 0, ctypes.byref(c))
+            assert rc == 0, f"{self.name}: rs_create {rc}"
+            self.ctx[(k, m)] = c
+        return self.ctx[(k, m)]
+
+    def close(self):
+        for c in self.ctx.values():
+            self.lib.rs_destroy(c)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", required=True, help="comma-separated abx/<name>.so (the first is the reference)")
+    ap.add_argument("--workloads", required=True)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--min-ms", type=float, default=100.0)
+    ap.add_argument("--out-pad", action="store_true", help="rs_set_out_pad_writes(1) on every variant")
+    args = ap.parse_args()
+    import torch
+
+    GiB = 1 << 30
+    names = args.variants.split(",")
+    vs = [Variant(n, os.path.join(ROOT, "abx", n + ".so")) for n in names]
+    print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
+    for wl in args.workloads.split(","):
+        k, m, S, N, mode = WORKLOADS[wl]
+        t = k + m
+        P = (S + 255) // 256 * 256
+        nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))
+        g = torch.Generator(device="cuda").manual_seed(1)
+        bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
+                 torch.empty((N, m, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
+        outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+        rng = np.random.default_rng(3)
+        full = (1 << t) - 1
+        if mode in ("rec1pb_out", "rec1p_out"):
+            mk = full & ~(1 << rng.integers(0, t, N))
+            bound = 1 if mode == "rec1pb_out" else 0
+        elif mode in ("rec2pb_out", "rec2p_out"):
+            import itertools
+
+            pairs = np.array(list(itertools.combinations(range(t), 2)))
+            ch = pairs[rng.integers(0, len(pairs), N)]
+            mk = full & ~((1 << ch[:, 0]) | (1 << ch[:, 1]))
+            bound = 2 if mode == "rec2pb_out" else 0
+        elif mode == "rec4p_out":
+            mk = np.array([full & ~sum(1 << int(j) for j in rng.choice(t, size=min(4, m), replace=False))
+                           for _ in range(N)])
+            bound = 0
+        elif mode in ("recmix_out", "recmix1_out"):
+            lo = 1 if mode == "recmix1_out" else 0
+            mk = np.full(N, full)
+            for i, ne in enumerate(rng.integers(lo, m + 1, N)):
+                for j in rng.choice(t, size=int(ne), replace=False):
+                    mk[i] &= ~(1 << int(j))
+            bound = 0
+        elif mode == "enc":
+            mk, bound = None, 0
+        else:
+            raise SystemExit(f"{wl}: mode {mode} not supported here")
+        alg = alg_bytes(wl)
+        if mk is not None:
+            mk = mk.astype(np.uint32)
+            if mode in ("recmix_out", "recmix1_out"):
+                nmiss = np.array([bin(int(x) ^ full).count("1") for x in mk])
+                alg = int(S * (k * np.count_nonzero(nmiss) + nmiss.sum()))
+            md = torch.from_numpy(mk.view(np.int32)).cuda()
+        for v in vs:
+            v.lib.rs_set_out_pad_writes(v.ctx_for(k, m), 1 if args.out_pad else 0)
+
+        def run(v, i):
+            c = v.ctx_for(k, m)
+            d, p = bufs[i % nb]
+            if mode == "enc":
+                rc = v.lib.rs_encode_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, 0, None)
+            elif bound:
+                rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                            md.data_ptr(), bound, outs[i % nb].data_ptr(), m * P,
+                                                            None)
+            else:
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                    md.data_ptr(), N, 1, outs[i % nb].data_ptr(), m * P, None)
+            assert rc == 0, (v.name, rc)
+
+        for v in vs:  # every batch a codeword; warm each variant's kernels
+            for d, p in bufs:
+                v.lib.rs_encode_batch(v.ctx_for(k, m), d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, 0, None)
+            run(v, 0)
+        torch.cuda.synchronize()
+        res = {v.name: [] for v in vs}
+        digests = {}
+        for r in range(args.rounds):
+            order = vs[r % len(vs):] + vs[:r % len(vs)]
+            for v in order:
+                run(v, 0)
+                run(v, 1)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                iters = 10
+                for rep in range(2):  # the first pass sizes the second
+                    e0.record()
+                    for i in range(iters):
+                        run(v, i)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ms = e0.elapsed_time(e1) / iters
+                    iters = max(10, int(np.ceil(args.min_ms / max(ms, 1e-3))))
+                res[v.name].append(alg / (ms * 1e-3) / 1e9 / 8000)
+        for v in vs:
+            run(v, 0)
+            torch.cuda.synchronize()
+            o = (outs[0] if mode != "enc" else bufs[0][1]).cpu().numpy()
+            digests[v.name] = hash(o.tobytes())
+            kname = v.lib.rs_last_kernel(v.ctx_for(k, m)).decode()
+            base = np.array(res[vs[0].name])
+            mine = np.array(res[v.name])
+            print(f"{wl:24s} {v.name:10s} median {np.median(mine) * 100:5.1f}%  min {mine.min() * 100:5.1f}  "
+                  f"max {mine.max() * 100:5.1f}  paired diff vs {vs[0].name}: {np.median(mine - base) * 100:+5.2f} "
+                  f"points  {kname}", flush=True)
+        agree = len(set(digests.values())) == 1
+        print(f"{wl:24s} outputs agree across variants: {agree}", flush=True)
+        del bufs, outs
+        torch.cuda.empty_cache()
+    for v in vs:
+        v.close()
+
+
+if __name__ == "__main__":
+    main()

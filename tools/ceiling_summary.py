@@ -28,22 +28,30 @@ def legs(doc):
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     shipped = legs(json.load(open(os.path.join(d, "shipped.json"))))
-    pattern = legs(json.load(open(os.path.join(d, "pattern.json"))))
-    rows, doc = [], {"tag": tag, "source": "tools/ceiling_probe.sh (same box, same process layout)", "legs": {}}
+    twins = {}  # occupancy cap -> legs of the compute-free twin
+    for fn in sorted(os.listdir(d)):
+        if fn.startswith("pattern_c") and fn.endswith(".json"):
+            twins[int(fn[len("pattern_c"):-len(".json")])] = legs(json.load(open(os.path.join(d, fn))))
+    rows, doc = [], {"tag": tag, "source": "tools/ceiling_probe.sh (same box, back to back)",
+                     "caps": sorted(twins), "legs": {}}
     for (shape, key), (kname, frac) in shipped.items():
-        if (shape, key) not in pattern:
+        cands = [(tw[(shape, key)][1], cap) for cap, tw in twins.items() if (shape, key) in tw]
+        if not cands:
             continue
-        pk, ceil = pattern[(shape, key)]
-        doc["legs"].setdefault(shape, {})[key] = {"kernel": kname, "shipped_frac": frac, "ceiling_frac": ceil,
-                                                  "of_ceiling": round(frac / ceil, 4), "same_kernel": pk == kname}
-        rows.append(f"| {shape} {key} | `{kname}` | {frac:.4f} | {ceil:.4f} | {frac / ceil:.3f} | "
-                    f"{(ceil - frac) * 100:+.1f} |")
+        ceil, cap = max(cands)
+        doc["legs"].setdefault(shape, {})[key] = {
+            "kernel": kname, "shipped_frac": frac, "ceiling_frac": ceil, "ceiling_at_cap": cap,
+            "twin_by_cap": {str(c): tw[(shape, key)][1] for c, tw in sorted(twins.items()) if (shape, key) in tw},
+            "of_ceiling": round(frac / ceil, 4)}
+        rows.append(f"| {shape} {key} | `{kname}` | {frac:.4f} | {ceil:.4f} (cap {cap or 'none'}) | "
+                    f"{frac / ceil:.3f} | {(ceil - frac) * 100:+.1f} |")
     with open(os.path.join(d, "ceilings.json"), "w") as f:
         json.dump(doc, f, indent=1)
     md = [f"# Compute-free ceilings per leg ({tag})", "",
-          "shipped = bench.py --sweep-only HBM fraction of the shipped kernel; ceiling = the same sweep with the "
-          "RS_PATTERN_ONLY=1 twin (same launches / loads / stores, one XOR per input dword instead of GF(2^8) "
-          "arithmetic), same box, run back to back.", "",
+          "shipped = bench.py --sweep-only HBM fraction of the shipped kernel; ceiling = the best of the same sweep "
+          "with the RS_PATTERN_ONLY=1 twin (same launches / loads / stores, one XOR per input dword instead of "
+          "GF(2^8) arithmetic) at each occupancy cap (rs_set_occupancy_cap; none = uncapped), same box, back to "
+          "back.", "",
           "| leg | kernel | shipped | ceiling | shipped / ceiling | headroom (points) |", "|---|---|---|---|---|---|"]
     md += sorted(rows, key=lambda r: -float(r.split("|")[-2]))
     with open(os.path.join(d, "ceilings.md"), "w") as f:
