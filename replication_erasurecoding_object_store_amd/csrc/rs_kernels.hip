@@ -1232,6 +1232,11 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
 #ifndef RS_FLAT_EM_FULL
 #define RS_FLAT_EM_FULL 1
 #endif
+// RS_FLAT_LIST: the E = m launches run over a list of the damaged stripes
+// (compact_damaged_kernel) instead of skipping intact stripes task by task.
+#ifndef RS_FLAT_LIST
+#define RS_FLAT_LIST 0
+#endif
 
 // Makes the inputs' registers opaque to the compiler: chunk indices computed from
 // them before cannot be reused after (it would otherwise keep every split live
@@ -1280,7 +1285,10 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t N = a.n_stripes;
+  // list mode (E = m launches over a scan's batch): the tasks cover only the damaged
+  // stripes, listed by compact_damaged_kernel; logical stripe s is list[s]
+  const bool listed = a.stripe_list != nullptr;
+  const uint32_t N = listed ? wave_uniform(*as_const<uint32_t>(a.list_count)) : a.n_stripes;
   const uint32_t cols = (a.shard_len + 15u) >> 4;
   const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
   const uint32_t cstride = (cols + 7u) & ~7u;
@@ -1296,6 +1304,7 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
   uint32_t bad = 0u;
 
   // stripe s's present mask (a skipped one: all present) and plan
+  auto phys = [&](uint32_t s) -> uint32_t { return listed ? as_const<uint32_t>(a.stripe_list)[s] : s; };
   auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
     const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
     uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
@@ -1320,28 +1329,31 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
     const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
     const bool live = !inB || straddle;                         // past the batch end: dead
     const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
+    const uint32_t pA = phys(s0), pB = straddle ? phys(s0 + 1u) : pA;  // wave-uniform
     uint32_t mA, nA, mB, nB;
-    const uint8_t* planA = plan_of(s0, mA, nA);
+    const uint8_t* planA = plan_of(pA, mA, nA);
     const uint8_t* planB = planA;
     mB = mA;
     nB = nA;
-    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
-    const bool two = planA != planB;  // wave-uniform: two passes, one per stripe
-    const bool lb = live && inB;
+    if (straddle) planB = plan_of(pB, mB, nB);
+    // wave-uniform: two passes, one per stripe -- when the stripes' patterns differ,
+    // and in list mode whenever the task straddles (listed stripes are not adjacent
+    // in memory, so each pass addresses its own stripe's base)
+    const bool two = listed ? straddle : planA != planB;
+    const bool lb = live && inB && !listed;  // B lanes addressed off stripe s0's base
     const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
     const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
     const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
-    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
-                                                       0x7FFFFFFF, 0x00020000);
-    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
-                                                       0x7FFFFFFF, 0x00020000);
-    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
-    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
-                                                        0x7FFFFFFF, 0x00020000);
     const bool fullc = live && colr < a.full_cols;
     const bool part = nb != 0u && live && colr == a.full_cols;
     for (uint32_t seg = 0; seg < (two ? 2u : 1u); ++seg) {
       const bool sb = seg != 0u;
+      const uint64_t base_s = (listed && sb) ? pB : pA;  // stripe whose base this pass addresses
+      const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + base_s * a.data_sp, 0, 0x7FFFFFFF, 0x00020000);
+      const auto pin =
+          __builtin_amdgcn_make_buffer_rsrc(a.parity + base_s * a.parity_sp, 0, 0x7FFFFFFF, 0x00020000);
+      // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
+      const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + base_s * a.out_sp, 0, 0x7FFFFFFF, 0x00020000);
       const uint8_t* plan = sb ? planB : planA;
       uint32_t bits = sb ? mB : mA;
       const uint32_t nout = sb ? nB : nA;  // wave-uniform
@@ -1763,6 +1775,28 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ s
 }
 
 // ---------------------------------------------------------------------------
+// List of the damaged stripes of a per-stripe batch (round 5): list[1 + j] = the
+// j-th stripe whose mask misses a shard, list[0] = how many.  One thread per stripe,
+// one atomic per wave (a vector atomic, from lane 0); the order across waves is
+// whatever the atomics give (each stripe is computed on its own, so the bytes do not
+// depend on it).  The flat E = m kernel then runs over damaged stripes only: a scan's
+// batch of intact and damaged stripes reads the damaged ones back to back instead of
+// leaving a hole in the read stream for every intact stripe.
+__global__ __launch_bounds__(256) void compact_damaged_kernel(const uint32_t* __restrict__ masks, uint32_t n,
+                                                               uint32_t full, uint32_t* __restrict__ list) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const bool dmg = i < n && (masks[i] & full) != full;
+  const uint64_t b = __builtin_amdgcn_ballot_w64(dmg);
+  if (b == 0) return;  // wave-uniform
+  uint32_t base = 0;
+  if ((threadIdx.x & 63u) == 0u) base = atomicAdd(list, static_cast<uint32_t>(__builtin_popcountll(b)));
+  base = __builtin_amdgcn_readfirstlane(base);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
+  if (dmg) list[1u + base + rank] = i;
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launch dispatch.
 template <int K, int M, int E>
 static const void* spec_fn(bool per_stripe) {
@@ -1969,13 +2003,23 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
       if (waves == 0) return name;
+      KernelArgs la = a;
+      if (RS_FLAT_LIST && RS_FLAT_SEG && e == a.m && a.list_scratch && a.present_masks) {
+        // E = m (no caller bound: a scan's batch): list the damaged stripes first
+        if (hipMemsetAsync(a.list_scratch, 0, 4, s) != hipSuccess) return nullptr;
+        hipLaunchKernelGGL(compact_damaged_kernel, dim3((a.n_stripes + 255u) / 256u), dim3(256), 0, s,
+                           a.present_masks, a.n_stripes, a.full_mask, a.list_scratch);
+        la.list_count = a.list_scratch;
+        la.stripe_list = a.list_scratch + 1;
+      }
+      void* largs[] = {&la};
       // E <= 2: one task per wave (r04zi: RS(10+4) 64 KiB 1-/2-erasure +0.9 / +2.5
       // points); E = M keeps its grid-stride loop (a full grid lost 10 points there)
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
       const dim3 grid = (!blocks_per_cu && (e <= 2 || RS_FLAT_EM_FULL)) ? full_grid(waves)
                                                                          : grid_for(waves, bpc, cu_count);
       const uint32_t cap = e == 1 ? RS_OCC_CAP_FLAT_E1 : e == 2 ? RS_OCC_CAP_FLAT_E2 : RS_OCC_CAP_FLAT_EM;
-      if (hipLaunchKernel(ff, grid, dim3(256), args, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
+      if (hipLaunchKernel(ff, grid, dim3(256), largs, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
       return name;
     }
   }
