@@ -313,9 +313,6 @@ struct Engine {
   // rs_stream_release(stream) returns the stream's word to status_free.
   std::mutex status_mu;
   std::unordered_map<hipStream_t, uint32_t> status_idx;
-  // per stream: the damaged-stripe list of E = m flat launches (stream-ordered, so
-  // one buffer per stream serves every launch on it; freed by rs_stream_release)
-  std::unordered_map<hipStream_t, std::unique_ptr<DevBuf>> list_scratch;
   std::vector<uint32_t> status_free;
   std::unique_ptr<StatusChunk> status_chunks[kStatusChunks];  // fixed slots: read without the mutex
   uint32_t status_next = 0;  // words handed out from the chunks so far
@@ -555,23 +552,6 @@ int fan_out(rs_ctx* c, size_t N, size_t user_bytes_per_stripe, Fn&& fn) {
   return RS_OK;
 }
 
-// The stream's damaged-stripe list buffer with room for n + 1 words, or nullptr
-// (the launch then skips intact stripes task by task).  Growing it waits for the
-// stream first: a queued kernel may still read the old buffer.
-uint32_t* list_scratch_for(Engine* e, hipStream_t s, size_t n) {
-  std::lock_guard<std::mutex> g(e->status_mu);
-  auto& b = e->list_scratch[s];
-  if (!b) b = std::make_unique<DevBuf>();
-  if (b->n < (n + 1) * 4) {
-    if (b->p && hipStreamSynchronize(s) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    if (b->ensure((n + 1) * 4)) return nullptr;
-  }
-  return static_cast<uint32_t*>(b->p);
-}
-
 uint32_t* status_dev(Engine* e, uint32_t idx) {
   return static_cast<uint32_t*>(e->status_chunks[idx / kStatusChunk]->dev.p) + idx % kStatusChunk;
 }
@@ -637,8 +617,6 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   a.encode_net = (e->bitsliced && !per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   a.data_inputs = (!per_stripe && a.plans == e->d_enc_plan.p) ? 1u : 0u;
   if (per_stripe && !(a.status = status_word(e, s))) return RS_ERR_DEVICE;
-  if (per_stripe && a.out && e_out == e->m && e->m > 2 && !a.stripe_plans)
-    a.list_scratch = list_scratch_for(e, s, a.n_stripes);
   if ((e->parity_pad && a.data_inputs && !a.out) || ((e->out_pad || own_out) && a.out)) {
     // rs_set_parity_pad_writes / rs_set_out_pad_writes / engine-owned out rows: run
     // over whole 128-B lines of the slot (inputs' padding read, the written rows'
@@ -1824,7 +1802,6 @@ static int sync_stream(rs_ctx* c, void* stream, bool release) {
     std::lock_guard<std::mutex> g(e->status_mu);
     e->status_idx.erase(s);
     e->status_free.push_back(idx);
-    e->list_scratch.erase(s);
   }
   if (release) c->shared.forget(s);
   if (word & 1u) return RS_ERR_TOO_FEW_SHARDS;

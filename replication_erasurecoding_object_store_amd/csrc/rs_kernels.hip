@@ -954,101 +954,35 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
 }
 
 // ---------------------------------------------------------------------------
-// Per-stripe reconstruct over flat 64-column tasks (out of place, LUT plans).
+// Per-stripe out-of-place reconstruct over flat 64-column tasks (LUT plans),
+// segmented (round 5).
 //
-// The same flat column space as the flat encode / scrub (each stripe's columns
-// rounded up to whole 128-B lines), so RS(10+4) at 64 KiB objects runs 6.5 tasks
-// per stripe instead of 7 stripe-aligned ones, with every wave access split at a
-// line boundary.  A task that straddles stripes s0 / s0+1 whose erasure patterns
-// differ selects per lane: input slots (the first K present of each mask), table
-// dwords (v_cndmask between the two plans' SGPR tables) and the rows to store.
-// Input loads of such a task come from both regions with one buffer load each;
-// a lane whose slot lies in the other region gets an out-of-range offset, which
-// fetches nothing and returns zeros, so OR-ing the two loads gives its bytes.
+// For ragged shard lengths (columns not a multiple of 64, e.g. RS(10+4) at 64 KiB
+// objects: S = 6 554, 410 columns) the batch's columns -- each stripe rounded up to
+// whole 128-B lines, so a wave access splits only at a line boundary -- are cut into
+// 64-column tasks that may straddle two stripes: 6.5 tasks per RS(10+4) stripe
+// instead of 7 stripe-aligned ones.  A task whose two stripes have different
+// erasure patterns runs as two passes of the single-plan code: the lanes of stripe
+// s0 with plan A, then the lanes of stripe s0 + 1 with plan B, the other stripe's
+// lanes loading nothing (out-of-range offsets: no fetch) and storing nothing.  The
+// kernel so holds one plan's working set (RS(10+4): 58 / 65 / 164 VGPRs for E = 1 /
+// 2 / 4); round 2's form selected table dwords per lane between the two plans
+// (141 / 129 / 195 VGPRs).  The price is a second pass of VALU work on the one task
+// in 13 that straddles two stripes.  A pass over an intact (or skipped) stripe is
+// not run at all.  E is the launch's erasure bound: M for device masks without a
+// bound and for mixed coalescer batches, the masks' maximum for host masks, the
+// caller's max_missing for device masks.  E <= 2 runs input-outer with x[K] as the
+// only per-input state; E > 2 splits every input into chunk indices once and then
+// computes only the rows the stripe misses, one at a time.
+// RS_FLAT_EM_FULL: the E > 2 flat launches take one task per wave (a full grid) like
+// the E <= 2 ones, instead of a grid-stride loop over default_blocks_per_cu.
+#ifndef RS_FLAT_EM_FULL
+#define RS_FLAT_EM_FULL 1
+#endif
 
-// One row r from chunk indices, table dwords chosen per lane between two plans.
-template <int K, int M>
-__device__ __forceinline__ u32x4 gf_row_ix2(const uint8_t* planA, const uint8_t* planB, bool inB,
-                                            const Idx3 (&ix)[K][4], int r) {
-  u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
-  if constexpr (RS_PATTERN_ONLY) return gf_row_ix<K, M>(planA, ix, r);
-  const uint32_t selB = inB ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    const uint8_t* pa = planA;
-    const uint8_t* pb = planB;
-    asm volatile("" : "+s"(pa));
-    asm volatile("" : "+s"(pb));
-    const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(r, c);
-    const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(r, c);
-    uint32_t q[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      q[i] = __builtin_amdgcn_bitop3_b32(selB, tb[i], ta[i], 0xCA);  // selB ? tb : ta, bitwise
-      asm volatile("" : "+v"(q[i]));                                // one input's tables at a time
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t prod = lookup3(ix[c][d], q[0], q[1], q[2], q[3], q[4]);
-      if (c & 1)
-        y[d] = xor3(y[d], pend[d], prod);
-      else if (c == K - 1)
-        y[d] ^= prod;
-      else
-        pend[d] = prod;
-    }
-    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
-  }
-  return y;
-}
-
-// Rows 0..NR-1 input-outer (as gf_rows) with table dwords chosen per lane between
-// two plans: no chunk-index array (K x 12 VGPRs) is kept, each input is split and
-// used once.  For flat per-stripe launches bounded to E <= 2 erasures.
-template <int K, int M, int NR, int R0 = 0>
-__device__ __forceinline__ void gf_rows2(const uint8_t* planA, const uint8_t* planB, bool inB, const u32x4 (&x)[K],
-                                         u32x4 (&y)[NR]) {
-  if constexpr (RS_PATTERN_ONLY) {
-    gf_rows<K, M, R0, NR>(planA, x, y);
-    return;
-  }
-  u32x4 pend[NR];
-#pragma unroll
-  for (int r = 0; r < NR; ++r) y[r] = u32x4{0u, 0u, 0u, 0u};
-  const uint32_t selB = inB ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    Idx3 ix[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) ix[d] = split3(x[c][d]);
-    const uint8_t* pa = planA;
-    const uint8_t* pb = planB;
-    asm volatile("" : "+s"(pa));
-    asm volatile("" : "+s"(pb));
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const RS_CONST uint32_t* ta = PlanView(pa, K, M).quad(R0 + r, c);
-      const RS_CONST uint32_t* tb = PlanView(pb, K, M).quad(R0 + r, c);
-      uint32_t q[5];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) q[i] = __builtin_amdgcn_bitop3_b32(selB, tb[i], ta[i], 0xCA);  // selB ? tb : ta
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const uint32_t prod = lookup3(ix[d], q[0], q[1], q[2], q[3], q[4]);
-        if (c & 1)
-          y[r][d] = xor3(y[r][d], pend[r][d], prod);
-        else if (c == K - 1)
-          y[r][d] ^= prod;
-        else
-          pend[r][d] = prod;
-      }
-    }
-    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
-  }
-}
 
 template <int K, int M, int E>
-__global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -1067,244 +1001,7 @@ __global__ __launch_bounds__(256) void apply_flat_ps_kernel(const KernelArgs a) 
   const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
   uint32_t bad = 0u;
 
-  // stripe s's present mask (an invalid one reads slots 0..K-1) and plan
-  auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
-    const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
-    uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
-    bad |= (pid == kPlanInvalid) ? 1u : 0u;
-    bool skip = pid == kPlanInvalid;
-    if constexpr (E < M) {  // more erasures than this launch's bound: skip, flag
-      const bool over = static_cast<uint32_t>(__builtin_popcount((~present) & full)) > static_cast<uint32_t>(E);
-      bad |= over ? 2u : 0u;
-      skip = skip || over;
-    }
-    m = skip ? full : present;
-    pid = skip ? 0u : pid;  // plan 0 = nothing missing -> every store dropped
-    const uint8_t* p = uniform_ptr(a.plans + static_cast<uint64_t>(pid) * a.plan_bytes);
-    nout = PlanView(p, K, M).n_out();
-    return p;
-  };
-
-  auto next_task = [&] {  // grid stride in the flat column space
-    c0 += step_c;
-    s0 += step_s;
-    if (c0 >= cstride) {
-      c0 -= cstride;
-      ++s0;
-    }
-  };
-  while (s0 < N) {
-    const uint32_t cl = c0 + lane;
-    const bool inB = cl >= cstride;
-    const uint32_t colr = inB ? cl - cstride : cl;
-    const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
-    const bool live = !inB || straddle;                         // past the batch end: dead
-    const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
-    uint32_t mA, nA, mB, nB;
-    const uint8_t* planA = plan_of(s0, mA, nA);
-    const uint8_t* planB = planA;
-    mB = mA;
-    nB = nA;
-    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
-    const bool diff = planA != planB;  // wave-uniform: the two stripes' patterns differ
-    if ((nA | nB) == 0u) {  // complete (or skipped) stripes: no loads, no stores (round 4)
-      next_task();
-      continue;
-    }
-    const bool lb = live && inB;
-    const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
-    const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
-    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
-                                                       0x7FFFFFFF, 0x00020000);
-    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
-                                                       0x7FFFFFFF, 0x00020000);
-    u32x4 x[K];
-    uint32_t bitsA = mA, bitsB = mB;
-    if (!diff) {
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const uint32_t s = pop_low(bitsA);
-        x[c] = s < static_cast<uint32_t>(K) ? bload16(din, offD, s * pitch)
-                                            : bload16(pin, offP, (s - static_cast<uint32_t>(K)) * pitch);
-      }
-    } else {
-      // E = M launches (a scan's mixed batch): the lanes of an intact stripe next to a
-      // damaged one fetch nothing either (their stores are dropped anyway)
-      const bool need = E <= 2 || (inB ? nB : nA) != 0u;
-#pragma unroll
-      for (int c = 0; c < K; ++c) {
-        const uint32_t sa = pop_low(bitsA), sb = pop_low(bitsB);
-        const uint32_t s = inB ? sb : sa;
-        const bool par = s >= static_cast<uint32_t>(K);
-        const uint32_t so = (par ? s - static_cast<uint32_t>(K) : s) * pitch;
-        const u32x4 xd = bload16(din, par || !need ? kDropOffset : offD + so, 0);
-        const u32x4 xp = bload16(pin, par && need ? offP + so : kDropOffset, 0);
-        x[c] = xd | xp;
-      }
-    }
-    const uint32_t nmax = nA > nB ? nA : nB;
-    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
-    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
-                                                        0x7FFFFFFF, 0x00020000);
-    const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
-    const uint32_t nl = inB ? nB : nA;
-    const bool fullc = live && colr < a.full_cols;
-    const bool part = nb != 0u && live && colr == a.full_cols;
-    // stores rows [0, NR) with cache policy CPOL, dropped per lane past its stripe's outputs
-    auto emit = [&](auto nr_tag, auto cpol_tag, const auto& yy) {
-      constexpr int NR = decltype(nr_tag)::value;
-      constexpr int CPOL = decltype(cpol_tag)::value;
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-        __builtin_amdgcn_raw_buffer_store_b128(yy[r], oout, fullc && static_cast<uint32_t>(r) < nl ? offO : kDropOffset,
-                                               r * pitch, CPOL);
-      if (__builtin_amdgcn_ballot_w64(part) != 0u) {  // wave-uniform
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-          store_part_rsrc<CPOL>(oout, offO, r * pitch, part && static_cast<uint32_t>(r) < nl, yy[r], nb);
-      }
-    };
-    if constexpr (E <= 2) {
-      // input-outer, every row of the bound computed (a 1-erasure stripe in an E = 2
-      // launch computes a row it does not store): x[K] only, no index array
-      u32x4 y[E];
-      if (!diff)
-        gf_rows<K, M, 0, E>(planA, x, y);
-      else
-        gf_rows2<K, M, E>(planA, planB, inB, x, y);
-      emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-    } else {
-      u32x4 y[E];
-      Idx3 ix[K][4];
-#pragma unroll
-      for (int c = 0; c < K; ++c)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
-      if (!diff) {
-        y[0] = gf_row_ix<K, M>(planA, ix, 0);
-#pragma unroll
-        for (int r = 1; r < E; ++r) {
-          y[r] = y[0];
-          if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix<K, M>(planA, ix, r);
-        }
-      } else {
-        y[0] = gf_row_ix2<K, M>(planA, planB, inB, ix, 0);
-#pragma unroll
-        for (int r = 1; r < E; ++r) {
-          y[r] = y[0];
-          if (static_cast<uint32_t>(r) < nmax) y[r] = gf_row_ix2<K, M>(planA, planB, inB, ix, r);
-        }
-      }
-      if (RS_WAVE_ROWS && nmax <= 1u)  // wave-uniform: the bounded kernels' store policy
-        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
-      else if (RS_WAVE_ROWS && nmax == 2u)
-        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-      else
-        emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-    }
-    next_task();
-  }
-  if (bad && lane == 0u) atomicOr(a.status, bad);
-}
-
-// ---------------------------------------------------------------------------
-// Flat per-stripe reconstruct, segmented (round 5).  The same flat 64-column tasks
-// as apply_flat_ps_kernel, but a task whose two stripes have different erasure
-// patterns runs as two passes of the single-plan code -- the lanes of stripe s0
-// with plan A, then the lanes of stripe s0+1 with plan B -- in which the other
-// stripe's lanes load nothing (out-of-range offsets: no fetch) and store nothing.
-// No per-lane plan selection (gf_rows2 / gf_row_ix2) is compiled in, so the kernel
-// holds one plan's working set; the price is a second pass of VALU work on the one
-// task in 13 that straddles two stripes (RS(10+4) at 64 KiB objects: 6.5 tasks per
-// stripe).  A pass over an intact (or skipped) stripe is not run at all.
-// RS_FLAT_EM_ROWS: rows of the E > 2 launches -- 0: every input's chunk indices
-// kept (ix[K][4], 12 VGPRs per input) and one row at a time, as apply_flat_ps_kernel;
-// 1: each row re-splits its inputs (only x[K] live); 2: input-outer passes of <= 2
-// rows (rows 0-1, then 2-3 only for a stripe missing more than 2).
-#ifndef RS_FLAT_SEG
-#define RS_FLAT_SEG 1
-#endif
-#ifndef RS_FLAT_EM_ROWS
-#define RS_FLAT_EM_ROWS 0
-#endif
-// RS_FLAT_EM_FULL: the E > 2 flat launches take one task per wave (a full grid) like
-// the E <= 2 ones, instead of a grid-stride loop over default_blocks_per_cu.
-#ifndef RS_FLAT_EM_FULL
-#define RS_FLAT_EM_FULL 1
-#endif
-// RS_FLAT_LIST: the E = m launches run over a list of the damaged stripes
-// (compact_damaged_kernel) instead of skipping intact stripes task by task.
-#ifndef RS_FLAT_LIST
-#define RS_FLAT_LIST 0
-#endif
-
-// Makes the inputs' registers opaque to the compiler: chunk indices computed from
-// them before cannot be reused after (it would otherwise keep every split live
-// across rows -- the ix[K][4] array this is meant to avoid).
-template <int K>
-__device__ __forceinline__ void launder(u32x4 (&x)[K]) {
-#pragma unroll
-  for (int c = 0; c < K; ++c)
-#pragma unroll
-    for (int d = 0; d < 4; ++d) asm volatile("" : "+v"(x[c][d]));
-}
-
-// One row r from the inputs' bytes, split on the fly (no chunk-index array).
-template <int K, int M>
-__device__ __forceinline__ u32x4 gf_row_x(const uint8_t* plan, const u32x4 (&x)[K], int r) {
-  u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
-  if constexpr (RS_PATTERN_ONLY) {
-#pragma unroll
-    for (int c = 0; c < K; ++c) y ^= x[c] + static_cast<uint32_t>(r);
-    return y;
-  }
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    const uint8_t* tcol = plan;
-    asm volatile("" : "+s"(tcol));  // one opaque base per input: tables never all in SGPRs
-    const PlanView pc(tcol, K, M);
-    const RS_CONST uint32_t* tb = pc.quad(r, c);
-    const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(r, c);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const uint32_t prod = lookup3(split3(x[c][d]), q0, q1, q2, q3, q4);
-      if (c & 1)
-        y[d] = xor3(y[d], pend[d], prod);
-      else if (c == K - 1)
-        y[d] ^= prod;
-      else
-        pend[d] = prod;
-    }
-    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
-  }
-  return y;
-}
-
-template <int K, int M, int E>
-__global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_index();
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  // list mode (E = m launches over a scan's batch): the tasks cover only the damaged
-  // stripes, listed by compact_damaged_kernel; logical stripe s is list[s]
-  const bool listed = a.stripe_list != nullptr;
-  const uint32_t N = listed ? wave_uniform(*as_const<uint32_t>(a.list_count)) : a.n_stripes;
-  const uint32_t cols = (a.shard_len + 15u) >> 4;
-  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
-  const uint32_t cstride = (cols + 7u) & ~7u;
-  if (static_cast<uint64_t>(wave) * 64u >= static_cast<uint64_t>(N) * cstride) return;
-  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
-  const uint32_t full = a.full_mask;
-  const uint64_t g0 = static_cast<uint64_t>(wave) * 64u;
-  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
-  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
-  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 64u;
-  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
-  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
-  uint32_t bad = 0u;
-
   // stripe s's present mask (a skipped one: all present) and plan
-  auto phys = [&](uint32_t s) -> uint32_t { return listed ? as_const<uint32_t>(a.stripe_list)[s] : s; };
   auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
     const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
     uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
@@ -1329,31 +1026,28 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
     const bool straddle = c0 + 63u >= cstride && s0 + 1u < N;  // wave-uniform
     const bool live = !inB || straddle;                         // past the batch end: dead
     const uint32_t col = live ? min(colr, cols - 1u) : 0u;      // clamped load column
-    const uint32_t pA = phys(s0), pB = straddle ? phys(s0 + 1u) : pA;  // wave-uniform
     uint32_t mA, nA, mB, nB;
-    const uint8_t* planA = plan_of(pA, mA, nA);
+    const uint8_t* planA = plan_of(s0, mA, nA);
     const uint8_t* planB = planA;
     mB = mA;
     nB = nA;
-    if (straddle) planB = plan_of(pB, mB, nB);
-    // wave-uniform: two passes, one per stripe -- when the stripes' patterns differ,
-    // and in list mode whenever the task straddles (listed stripes are not adjacent
-    // in memory, so each pass addresses its own stripe's base)
-    const bool two = listed ? straddle : planA != planB;
-    const bool lb = live && inB && !listed;  // B lanes addressed off stripe s0's base
+    if (straddle) planB = plan_of(s0 + 1u, mB, nB);
+    const bool two = planA != planB;  // wave-uniform: two passes, one per stripe
+    const bool lb = live && inB;      // B lanes are addressed off stripe s0's base
     const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
     const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
     const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
     const bool fullc = live && colr < a.full_cols;
     const bool part = nb != 0u && live && colr == a.full_cols;
+    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
+                                                       0x7FFFFFFF, 0x00020000);
+    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
+    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
+                                                        0x7FFFFFFF, 0x00020000);
     for (uint32_t seg = 0; seg < (two ? 2u : 1u); ++seg) {
       const bool sb = seg != 0u;
-      const uint64_t base_s = (listed && sb) ? pB : pA;  // stripe whose base this pass addresses
-      const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + base_s * a.data_sp, 0, 0x7FFFFFFF, 0x00020000);
-      const auto pin =
-          __builtin_amdgcn_make_buffer_rsrc(a.parity + base_s * a.parity_sp, 0, 0x7FFFFFFF, 0x00020000);
-      // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
-      const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + base_s * a.out_sp, 0, 0x7FFFFFFF, 0x00020000);
       const uint8_t* plan = sb ? planB : planA;
       uint32_t bits = sb ? mB : mA;
       const uint32_t nout = sb ? nB : nA;  // wave-uniform
@@ -1389,37 +1083,7 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
       } else {
         u32x4 y[E];
-        if constexpr (RS_FLAT_EM_ROWS == 2) {
-          u32x4 y01[2];
-          if (nout <= 1u) {
-            u32x4 y0[1];
-            gf_rows<K, M, 0, 1>(plan, x, y0);
-            y01[0] = y01[1] = y0[0];
-          } else {
-            gf_rows<K, M, 0, 2>(plan, x, y01);
-          }
-          y[0] = y01[0];
-          y[1] = y01[1];
-          u32x4 yh[E - 2];
-#pragma unroll
-          for (int r = 0; r < E - 2; ++r) yh[r] = y01[0];
-          if (nout > 2u) {
-            launder(x);
-            gf_rows<K, M, 2, E - 2>(plan, x, yh);
-          }
-#pragma unroll
-          for (int r = 2; r < E; ++r) y[r] = yh[r - 2];
-        } else if constexpr (RS_FLAT_EM_ROWS == 1) {
-          y[0] = gf_row_x<K, M>(plan, x, 0);
-#pragma unroll
-          for (int r = 1; r < E; ++r) {
-            y[r] = y[0];  // dropped unless computed
-            if (static_cast<uint32_t>(r) < nout) {
-              launder(x);
-              y[r] = gf_row_x<K, M>(plan, x, r);
-            }
-          }
-        } else {
+        {
           Idx3 ix[K][4];
 #pragma unroll
           for (int c = 0; c < K; ++c)
@@ -1775,28 +1439,6 @@ __global__ __launch_bounds__(256) void copy_kernel(const uint8_t* __restrict__ s
 }
 
 // ---------------------------------------------------------------------------
-// List of the damaged stripes of a per-stripe batch (round 5): list[1 + j] = the
-// j-th stripe whose mask misses a shard, list[0] = how many.  One thread per stripe,
-// one atomic per wave (a vector atomic, from lane 0); the order across waves is
-// whatever the atomics give (each stripe is computed on its own, so the bytes do not
-// depend on it).  The flat E = m kernel then runs over damaged stripes only: a scan's
-// batch of intact and damaged stripes reads the damaged ones back to back instead of
-// leaving a hole in the read stream for every intact stripe.
-__global__ __launch_bounds__(256) void compact_damaged_kernel(const uint32_t* __restrict__ masks, uint32_t n,
-                                                               uint32_t full, uint32_t* __restrict__ list) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const bool dmg = i < n && (masks[i] & full) != full;
-  const uint64_t b = __builtin_amdgcn_ballot_w64(dmg);
-  if (b == 0) return;  // wave-uniform
-  uint32_t base = 0;
-  if ((threadIdx.x & 63u) == 0u) base = atomicAdd(list, static_cast<uint32_t>(__builtin_popcountll(b)));
-  base = __builtin_amdgcn_readfirstlane(base);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
-  if (dmg) list[1u + base + rank] = i;
-}
-
-// ---------------------------------------------------------------------------
 // Host-side launch dispatch.
 template <int K, int M, int E>
 static const void* spec_fn(bool per_stripe) {
@@ -1871,14 +1513,10 @@ static const void* pick_bitsliced(int k, int m, const char** name, uint32_t* tas
 // or the bound a caller (host masks: their maximum; device masks: max_missing)
 // gives -- E <= 2 runs input-outer with x[K] as the only per-input state.
 static const void* pick_flat_ps(int k, int m, int e, const char** name) {
-#define RS_PSFLAT(KK, MM, EE)                                                   \
-  if (k == KK && m == MM && e == EE) {                                          \
-    if (RS_FLAT_SEG) {                                                          \
-      *name = "apply_flat_seg_kernel<" #KK "," #MM "," #EE ">";                 \
-      return reinterpret_cast<const void*>(&apply_flat_seg_kernel<KK, MM, EE>); \
-    }                                                                           \
-    *name = "apply_flat_ps_kernel<" #KK "," #MM "," #EE ">";                    \
-    return reinterpret_cast<const void*>(&apply_flat_ps_kernel<KK, MM, EE>);   \
+#define RS_PSFLAT(KK, MM, EE)                                                 \
+  if (k == KK && m == MM && e == EE) {                                        \
+    *name = "apply_flat_seg_kernel<" #KK "," #MM "," #EE ">";                 \
+    return reinterpret_cast<const void*>(&apply_flat_seg_kernel<KK, MM, EE>); \
   }
   RS_PSFLAT(4, 2, 1) RS_PSFLAT(4, 2, 2)
   RS_PSFLAT(8, 4, 1) RS_PSFLAT(8, 4, 2) RS_PSFLAT(8, 4, 4)
@@ -1929,7 +1567,7 @@ static dim3 full_grid(uint64_t waves) {
 #endif
 // The segmented flat reconstructs (apply_flat_seg_kernel) at 4 waves per SIMD, one
 // task per wave (round 5, same-process A/B over shared buffers, 4 rounds,
-// profiles/r05d_ab_same_seg.log, RS(10+4) 64 KiB, against apply_flat_ps_kernel):
+// profiles/r05d_ab_same_seg.log, RS(10+4) 64 KiB, against round 4's flat kernel):
 // bounded 1-erasure 72.2 -> 73.9 %, bounded 2-erasure 73.4 -> 74.7 % (3 or 5 waves:
 // 69.7 / 69.4 %), unbounded 2-erasure 68.3 -> 72.0 %, mixed 0..4 57.9 -> 61.8 %,
 // mixed 1..4 65.1 -> 66.9 %; unbounded 1- and 4-erasure 69.7 -> 69.0 % and 66.0 ->
@@ -2003,23 +1641,14 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
       const uint64_t waves = (static_cast<uint64_t>(a.n_stripes) * ((cols + 7u) & ~7ull) + 63u) / 64u;
       if (waves == 0) return name;
-      KernelArgs la = a;
-      if (RS_FLAT_LIST && RS_FLAT_SEG && e == a.m && a.list_scratch && a.present_masks) {
-        // E = m (no caller bound: a scan's batch): list the damaged stripes first
-        if (hipMemsetAsync(a.list_scratch, 0, 4, s) != hipSuccess) return nullptr;
-        hipLaunchKernelGGL(compact_damaged_kernel, dim3((a.n_stripes + 255u) / 256u), dim3(256), 0, s,
-                           a.present_masks, a.n_stripes, a.full_mask, a.list_scratch);
-        la.list_count = a.list_scratch;
-        la.stripe_list = a.list_scratch + 1;
-      }
-      void* largs[] = {&la};
-      // E <= 2: one task per wave (r04zi: RS(10+4) 64 KiB 1-/2-erasure +0.9 / +2.5
-      // points); E = M keeps its grid-stride loop (a full grid lost 10 points there)
+      // one task per wave (E <= 2: r04zi, +0.9 / +2.5 points for RS(10+4) 64 KiB 1- /
+      // 2-erasure; E = M since round 5's segmented kernel: unbounded 2-erasure and
+      // mixed batches +3.5 / +3.9 points, r05b_ab_same_flat.log, r05e_ab_same_em.log)
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
       const dim3 grid = (!blocks_per_cu && (e <= 2 || RS_FLAT_EM_FULL)) ? full_grid(waves)
                                                                          : grid_for(waves, bpc, cu_count);
       const uint32_t cap = e == 1 ? RS_OCC_CAP_FLAT_E1 : e == 2 ? RS_OCC_CAP_FLAT_E2 : RS_OCC_CAP_FLAT_EM;
-      if (hipLaunchKernel(ff, grid, dim3(256), largs, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
+      if (hipLaunchKernel(ff, grid, dim3(256), args, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
       return name;
     }
   }

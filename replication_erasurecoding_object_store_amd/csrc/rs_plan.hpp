@@ -102,10 +102,6 @@ struct KernelArgs {
   const uint64_t* shard_ptrs;      // pointer-table launches: stripe i's shard s at device address
                                    //   shard_ptrs[i*(k+m) + s] (inputs: present shards; outputs:
                                    //   the missing shards' buffers), each S bytes, 16-B aligned
-  uint32_t* list_scratch;          // PER_STRIPE, E = m launches: n_stripes + 1 words the flat
-                                   //   kernel may use to list the damaged stripes (word 0 = count)
-  const uint32_t* stripe_list;     // set by launch_window: the flat kernel runs over the stripes
-  const uint32_t* list_count;      //   listed here (count on the device), not over 0..n_stripes
 };
 
 // Parity rows the generated bitsliced encode program of (k, m) was derived from
