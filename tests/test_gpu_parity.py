@@ -1027,7 +1027,7 @@ def test_flat_reconstruct_tasks(engines, k, m, S, N):
     torch.cuda.synchronize()
     kname = eng.last_kernel()
     cols = -(-S // 16)
-    assert ("flat_ps" in kname) == (cols >= 64 and cols % 64 != 0), kname
+    assert ("flat_seg" in kname) == (cols >= 64 and cols % 64 != 0), kname
     got = out.cpu().numpy()
     for i in range(N):
         if i in invalid:
@@ -1109,7 +1109,7 @@ def test_flat_reconstruct_host_masks_e2(engines, k, m, S, N):
     eng.reconstruct_out(data, parity, out, S, N, present_masks=masks)
     torch.cuda.synchronize()
     cols = -(-S // 16)
-    assert ("flat_ps" in eng.last_kernel()) == (cols % 64 != 0), eng.last_kernel()
+    assert ("flat_seg" in eng.last_kernel()) == (cols % 64 != 0), eng.last_kernel()
     got = out.cpu().numpy()
     for i in range(N):
         missing = [j for j in range(t) if not (masks[i] >> j) & 1]
