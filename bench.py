@@ -621,12 +621,12 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
         timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"])
         timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
         if SS % 128:
-            # rs_set_out_pad_writes: output rows end on whole 128-B lines (the outputs
-            # are the bench's own, full-pitch rows); bytes counted stay N*S*(K+e)
-            e2.set_out_pad_writes(True)
-            timed("reconstruct2_out_pad", lambda i: w.rec(i, bound=2), alg["reconstruct"])
-            timed("reconstruct1_out_pad", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+            # output rows end on whole 128-B lines by default (round 5); the same legs
+            # with exact rows (rs_set_out_pad_writes(0): nothing past S written)
             e2.set_out_pad_writes(False)
+            timed("reconstruct2_exact_rows", lambda i: w.rec(i, bound=2), alg["reconstruct"])
+            timed("reconstruct1_exact_rows", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+            e2.set_out_pad_writes(True)
         if mm > 2:
             # no caller bound (kernel sized for m); the mixed legs: 0..m erasures per
             # stripe, intact stripes included, device and host masks

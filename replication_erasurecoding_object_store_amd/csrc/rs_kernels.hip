@@ -153,9 +153,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(uint8_t* base) {
 // (SC1 there costs 1.5-8 points).
 constexpr int kCpolNt = 2;
 constexpr int kCpolSc1 = 16;
+// (A/B overrides: RS_CPOL_E1_K8 for 1-erasure K >= 8, RS_CPOL_E2_K10 for 2-erasure
+// K >= 10, RS_CPOL_PATH2 for the E = M kernels' 2-row path.)
+#ifndef RS_CPOL_E1_K8
+#define RS_CPOL_E1_K8 kCpolSc1
+#endif
+#ifndef RS_CPOL_E2_K10
+#define RS_CPOL_E2_K10 (kCpolSc1 | kCpolNt)
+#endif
+#ifndef RS_CPOL_PATH2
+#define RS_CPOL_PATH2 kCpolNt
+#endif
+// The segmented flat E = m kernel's 1-row path stores NT (round 5, same-process A/B,
+// profiles/r05h_ab_same_fp1.log, RS(10+4) 64 KiB): unbounded 1-erasure 68.4 ->
+// 71.5 %, mixed 0..4 61.7 -> 63.1 %, mixed 1..4 66.8 -> 68.4 %, others level; the
+// bounded E = 1 kernels keep SC1 (NT there: -2.9 flat, -5.1 stripe-aligned RS(8+4),
+// profiles/r05g_ab_same_cpol.log).
+#ifndef RS_CPOL_FLAT_PATH1
+#define RS_CPOL_FLAT_PATH1 kCpolNt
+#endif
 template <int K, int E>
 constexpr int out_cpol() {
-  return (E == 1 && K >= 8) ? kCpolSc1 : (E == 2 && K >= 10) ? (kCpolSc1 | kCpolNt) : kCpolNt;
+  return (E == 1 && K >= 8) ? RS_CPOL_E1_K8 : (E == 2 && K >= 10) ? RS_CPOL_E2_K10 : kCpolNt;
 }
 
 // Per-stripe kernels sized for E > 2 outputs (device masks without a caller bound:
@@ -182,7 +201,7 @@ constexpr int out_cpol() {
 #endif
 template <int K, int E, int NR>
 constexpr int path_cpol() {
-  return RS_WAVE_ROWS_CPOL == 2 ? (NR == 1 ? out_cpol<K, 1>() : kCpolNt)
+  return RS_WAVE_ROWS_CPOL == 2 ? (NR == 1 ? out_cpol<K, 1>() : RS_CPOL_PATH2)
          : RS_WAVE_ROWS_CPOL    ? out_cpol<K, NR>()
                                 : out_cpol<K, E>();
 }
@@ -1097,7 +1116,7 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
           }
         }
         if (RS_WAVE_ROWS && nout <= 1u)  // wave-uniform: the bounded kernels' store policy
-          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, RS_CPOL_FLAT_PATH1>{}, y);
         else if (RS_WAVE_ROWS && nout == 2u)
           emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
         else
