@@ -16,6 +16,7 @@ a)
   tools/gpustep.sh ${T}_sweep 700 tools/profile_sweep.sh $T
   ;;
 b)
+  tools/gpustep.sh ${T}_large_tests 300 python -u -m pytest tests/test_gpu_large.py -x -v --timeout 250 --timeout-method thread && \
   tools/gpustep.sh ${T}_ceiling 700 tools/ceiling_probe.sh $T && \
   tools/gpustep.sh ${T}_drop_in 400 tools/run_drop_in.sh && \
   RSGPU_BENCH_BACKEND=gloo tools/gpustep.sh ${T}_bench_gpus2 300 python -u bench.py --gpus 2 --steps 50 \
