@@ -142,6 +142,9 @@ std::vector<uint8_t> make_plan(int k, int m, uint32_t present, uint32_t out_mask
   uint32_t* ii = reinterpret_cast<uint32_t*>(p.data() + 16);
   for (int c = 0; c < k; ++c) ii[c] = static_cast<uint32_t>(in_idx[c]);
   for (size_t r = 0; r < out_idx.size(); ++r) ii[k + r] = static_cast<uint32_t>(out_idx[r]);
+  uint8_t* coef = p.data() + rs::plan_coef_offset(k, m);
+  for (size_t r = 0; r < out_idx.size(); ++r)
+    for (int c = 0; c < k; ++c) coef[r * rs::plan_coef_row(k) + c] = rows[r * k + c];
   uint32_t* tab = reinterpret_cast<uint32_t*>(p.data() + rs::plan_tab_offset(k, m));
   for (size_t r = 0; r < out_idx.size(); ++r)
     for (int c = 0; c < k; ++c) perm_tables(rows[r * k + c], tab + (c * m + r) * 5);

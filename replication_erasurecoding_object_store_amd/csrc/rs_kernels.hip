@@ -187,6 +187,18 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS
 #define RS_WAVE_ROWS 1
 #endif
+// Row paths of the E = M kernels, RS_EM_EMIT_EACH_{FLAT,APPLY}: 1 = each path computes
+// only its own rows (no row 0 ahead of the branch) and 3+ rows are stored one by one
+// as they are computed; 0 = row 0 first, then the other rows, then one store group.
+// Same-process A/B (profiles/r05i_ab_emit_each.log, 64 KiB, 4 rounds): the flat
+// RS(10+4) kernel gains 0.3-0.9 points on every E = M leg (mixed 64.8 -> 65.7 %),
+// the stripe-aligned RS(8+4) kernel loses 2.3-4.2 (its SGPRs spill: 10 -> 69).
+#ifndef RS_EM_EMIT_EACH_FLAT
+#define RS_EM_EMIT_EACH_FLAT 1
+#endif
+#ifndef RS_EM_EMIT_EACH_APPLY
+#define RS_EM_EMIT_EACH_APPLY 0
+#endif
 // Store policy of those paths (RS_WAVE_ROWS_CPOL):
 //   2 (default): the 1-row path with out_cpol<K, 1> (SC1 for K >= 8), the 2-row path
 //     NT.  Interleaved A/B against 1 (profiles/r04t_ab_p2nt.log, RS(10+4) 64 KiB,
@@ -344,7 +356,63 @@ __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K]
   }
 }
 
+// The 3-chunk v_perm tables of every coefficient f, 5 dwords each (the layout of
+// perm_tables in rs_engine.cpp), built at compile time in constant memory: 5 KiB
+// that every XCD keeps cache-hot.  The E = M rows read a plan's coefficient bytes
+// (its first 128 B, with the header) and fetch each coefficient's tables here
+// instead of from the plan's own 800-B table block (RS_EM_COEF, below).
+struct GfPermTabs {
+  uint32_t v[256 * 5];
+};
+constexpr uint8_t gf_mul_ct(uint8_t a, uint8_t b) {
+  uint8_t r = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (b & 1u) r = static_cast<uint8_t>(r ^ a);
+    const bool hi = (a & 0x80u) != 0u;
+    a = static_cast<uint8_t>(a << 1);
+    if (hi) a = static_cast<uint8_t>(a ^ 0x1Du);  // x^8 = x^4 + x^3 + x^2 + 1 (0x11d)
+    b = static_cast<uint8_t>(b >> 1);
+  }
+  return r;
+}
+constexpr GfPermTabs make_gf_perm_tabs() {
+  GfPermTabs t{};
+  for (int f = 0; f < 256; ++f)
+    for (int j = 0; j < 4; ++j) {
+      const uint8_t ff = static_cast<uint8_t>(f);
+      t.v[f * 5 + 0] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j))) << (8 * j);
+      t.v[f * 5 + 1] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(4 + j))) << (8 * j);
+      t.v[f * 5 + 2] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j << 3))) << (8 * j);
+      t.v[f * 5 + 3] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>((4 + j) << 3))) << (8 * j);
+      t.v[f * 5 + 4] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j << 6))) << (8 * j);
+    }
+  return t;
+}
+__constant__ GfPermTabs kGfPermTabs = make_gf_perm_tabs();
+
+// RS_EM_COEF (A/B): 1 = gf_row_ix takes each coefficient's tables from kGfPermTabs
+// through the plan's coefficient bytes; 0 (default) = from the plan's table block.
+// A mixed RS(10+4) batch touches all 1 470 plans, and every XCD's L2 fetches each
+// plan's 896-B table block once per launch: ~10 MB, about 1 % of the launch's bytes
+// (the mixed legs' HBM/alg 1.031 against 1.017 for one pattern per stripe).  Fewer
+// bytes, but one more dependent scalar round trip per row: same-process A/B
+// (profiles/r05j_ab_coef.log) -0.8 to -1.7 points on every E = M leg but one.
+#ifndef RS_EM_COEF
+#define RS_EM_COEF 0
+#endif
+
 // One row r of a task from the inputs' precomputed chunk indices ix[c][d].
+// RS_ROWIX_GROUP (A/B): inputs whose table dwords share one opaque base, i.e. are
+// fetched by the scalar unit together and waited for once (scalar loads return out
+// of order, so every wait is lgkmcnt(0)).  RS_ROWIX_TABONLY (diagnostic only, wrong
+// bytes): the tables are fetched as usual but folded with one XOR instead of three
+// lookups, which separates the cost of the fetches from that of the arithmetic.
+#ifndef RS_ROWIX_GROUP
+#define RS_ROWIX_GROUP 1
+#endif
+#ifndef RS_ROWIX_TABONLY
+#define RS_ROWIX_TABONLY 0
+#endif
 template <int K, int M>
 __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)[K][4], int r) {
   u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
@@ -355,16 +423,31 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
       for (int d = 0; d < 4; ++d) y[d] ^= ix[c][d].a + static_cast<uint32_t>(r);
     return y;
   }
+  const uint8_t* tg = plan;
+  const uint32_t* gt = kGfPermTabs.v;
+  constexpr int kWords = (K + 3) / 4;
+  uint32_t cw[kWords];
+  if constexpr (RS_EM_COEF) {
+    const RS_CONST uint32_t* cwp = PlanView(plan, K, M).coef_words(r);
+#pragma unroll
+    for (int i = 0; i < kWords; ++i) cw[i] = cwp[i];
+  }
 #pragma unroll
   for (int c = 0; c < K; ++c) {
-    const uint8_t* tcol = plan;
-    asm volatile("" : "+s"(tcol));  // one opaque base per input: tables never all in SGPRs
-    const PlanView pc(tcol, K, M);
-    const RS_CONST uint32_t* tb = pc.quad(r, c);
-    const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = pc.c4(r, c);
+    if (c % RS_ROWIX_GROUP == 0) {
+      tg = plan;
+      gt = kGfPermTabs.v;
+      asm volatile("" : "+s"(tg));  // one opaque base per group: tables never all in SGPRs
+      asm volatile("" : "+s"(gt));
+    }
+    const PlanView pc(tg, K, M);
+    const RS_CONST uint32_t* tb =
+        RS_EM_COEF ? as_const<uint32_t>(gt + ((cw[c >> 2] >> (8 * (c & 3))) & 0xFFu) * 5u) : pc.quad(r, c);
+    const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const uint32_t prod = lookup3(ix[c][d], q0, q1, q2, q3, q4);
+      const uint32_t prod = RS_ROWIX_TABONLY ? xor3(ix[c][d].a, q0 ^ q1 ^ q2, q3 ^ q4)
+                                             : lookup3(ix[c][d], q0, q1, q2, q3, q4);
       if (c & 1)
         y[d] = xor3(y[d], pend[d], prod);
       else if (c == K - 1)
@@ -372,7 +455,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
       else
         pend[d] = prod;
     }
-    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < K && (c + 1) % RS_ROWIX_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
   }
   return y;
 }
@@ -549,6 +632,31 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
 #pragma unroll
         for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
       const uint32_t nrow = pv.n_out();
+      if constexpr (RS_EM_EMIT_EACH_APPLY && RS_WAVE_ROWS) {
+        // each path computes only its rows; 3+ rows are stored one by one as computed
+        if (nrow <= 1u) {
+          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
+        } else if (nrow == 2u) {
+          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+          y[1] = gf_row_ix<K, M>(plan, ix, 1);
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+        } else {
+          constexpr int CPOL = out_cpol<K, E>();
+          const bool last = nb != 0u && blk + 1u == bps;  // wave-uniform
+          const bool part = col == a.full_cols;
+#pragma unroll
+          for (int r = 0; r < E; ++r) {
+            if (static_cast<uint32_t>(r) < nrow) {
+              const u32x4 yr = gf_row_ix<K, M>(plan, ix, r);
+              uint8_t* ob = out_ptr(a, K, stripe, r, pv.out_idx(r));
+              store16_or_drop<CPOL>(ob, off, full, yr);
+              if (last) store_part_or_drop<CPOL>(ob, off, part, yr, nb);
+            }
+          }
+        }
+        continue;
+      }
       y[0] = gf_row_ix<K, M>(plan, ix, 0);
 #pragma unroll
       for (int r = 1; r < E; ++r) {
@@ -1100,6 +1208,35 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         u32x4 y[E];
         gf_rows<K, M, 0, E>(plan, x, y);
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+      } else if constexpr (RS_EM_EMIT_EACH_FLAT && RS_WAVE_ROWS) {
+        // each row path computes only its rows; stripes missing 3+ shards store each
+        // row as soon as it is computed (one row's accumulators live instead of E)
+        Idx3 ix[K][4];
+#pragma unroll
+        for (int c = 0; c < K; ++c)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+        if (nout <= 1u) {
+          u32x4 y[1];
+          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, RS_CPOL_FLAT_PATH1>{}, y);
+        } else if (nout == 2u) {
+          u32x4 y[2];
+          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+          y[1] = gf_row_ix<K, M>(plan, ix, 1);
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+        } else {
+          constexpr int CPOL = out_cpol<K, E>();
+          const bool anypart = __builtin_amdgcn_ballot_w64(part) != 0u;  // wave-uniform
+#pragma unroll
+          for (int r = 0; r < E; ++r) {
+            if (static_cast<uint32_t>(r) < nout) {
+              const u32x4 yr = gf_row_ix<K, M>(plan, ix, r);
+              __builtin_amdgcn_raw_buffer_store_b128(yr, oout, fullc && mine ? offO : kDropOffset, r * pitch, CPOL);
+              if (anypart) store_part_rsrc<CPOL>(oout, offO, r * pitch, part && mine, yr, nb);
+            }
+          }
+        }
       } else {
         u32x4 y[E];
         {

@@ -7,10 +7,12 @@
 //   reconstruct  : in = first K present shards in index order, out = every missing
 //                  shard (data then parity, index order), C = composed decode rows
 //                  ([upstream reedsolomon.go reconstruct] phases 1+2 folded).
-// Byte layout (plan_bytes = plan_stride(K, M), 16-B aligned):
+// Byte layout (plan_bytes = plan_stride(K, M), 128-B aligned):
 //   u32 n_out; u32 present; u32 out_mask; u32 reserved; u32 in_idx[K]; u32 out_idx[M];
 //   pad to 16;   (present: the shards the plan reads from; out_mask: the shards it
 //                 may fill -- all, or the data shards for ReconstructData)
+//   u8 coef[M][plan_coef_row(K)] -- the coefficients C[r][c] themselves, rows padded to
+//                        4 B; pad to 16 (RS(10+4): header + coef = the plan's first 128 B)
 //   u32 tab[K][M][5]  -- per coefficient f = C[r][c]: the 3-chunk v_perm tables
 //                        {A_lo, A_hi, B_lo, B_hi, C_lo} (see rs_kernels.hip), input-major
 //                        so one input's E rows are one contiguous scalar load
@@ -32,11 +34,15 @@ constexpr uint32_t kPlanInvalid = 0xFFFFu;
 // 1 GiB column windows (the codec is column-wise).
 constexpr uint32_t kColumnWindow = 1u << 30;
 
-__host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
+__host__ __device__ constexpr uint32_t plan_coef_row(int k) { return (static_cast<uint32_t>(k) + 3u) & ~3u; }
+__host__ __device__ constexpr uint32_t plan_coef_offset(int k, int m) {
   return (16u + 4u * static_cast<uint32_t>(k) + 4u * static_cast<uint32_t>(m) + 15u) & ~15u;
 }
+__host__ __device__ constexpr uint32_t plan_tab_offset(int k, int m) {
+  return (plan_coef_offset(k, m) + static_cast<uint32_t>(m) * plan_coef_row(k) + 15u) & ~15u;
+}
 __host__ __device__ constexpr uint32_t plan_stride(int k, int m) {
-  return (plan_tab_offset(k, m) + 20u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 15u) & ~15u;
+  return (plan_tab_offset(k, m) + 20u * static_cast<uint32_t>(k) * static_cast<uint32_t>(m) + 127u) & ~127u;
 }
 
 // Plans, masks and LUT are written by the host before a launch and never by a
@@ -66,6 +72,10 @@ struct PlanView {
     return as_const<uint32_t>(p + plan_tab_offset(k, m)) + (c * m + r) * 5;
   }
   __host__ __device__ uint32_t c4(int r, int c) const { return quad(r, c)[4]; }
+  // coefficient bytes C[r][0..K) as dwords (4 per dword, little-endian)
+  __host__ __device__ const RS_CONST uint32_t* coef_words(int r) const {
+    return as_const<uint32_t>(p + plan_coef_offset(k, m) + static_cast<uint32_t>(r) * plan_coef_row(k));
+  }
 };
 
 // Shard slot s of stripe i lives at

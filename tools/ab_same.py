@@ -9,7 +9,7 @@ timed over >= min_ms of back-to-back launches.  Reported per variant: the median
 fraction of 8 TB/s and the median of its per-round difference to the first
 variant (paired, so a drift of the chip's state cancels).
 
-Usage: python tools/ab_same.py --variants base,seg --workloads rs104_64K_rec1pb_out,... [--rounds 5]
+Usage: python tools/ab_same.py --variants base,seg,pat@3 --workloads rs104_64K_rec1pb_out,... [--rounds 5]
 Workload names and modes: tools/ab_bench.py (device-resident modes only).
 """
 import argparse
@@ -34,13 +34,15 @@ SIGS = {
     "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
     "rs_set_out_pad_writes": (_i, [_vp, _i]),
+    "rs_set_occupancy_cap": (_i, [_vp, _i]),
     "rs_sync": (_i, [_vp, _vp]),
 }
 
 
 class Variant:
-    def __init__(self, name, path):
+    def __init__(self, name, path, occ_cap=None):
         self.name = name
+        self.occ_cap = occ_cap
         self.lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
         for fn, (res, args) in SIGS.items():
             f = getattr(self.lib, fn)
@@ -52,6 +54,8 @@ class Variant:
             c = _vp()
             rc = self.lib.rs_create(k, m, 0, 0, ctypes.byref(c))
             assert rc == 0, f"{self.name}: rs_create {rc}"
+            if self.occ_cap is not None:
+                assert self.lib.rs_set_occupancy_cap(c, self.occ_cap) == 0
             self.ctx[(k, m)] = c
         return self.ctx[(k, m)]
 
@@ -72,7 +76,10 @@ def main():
 
     GiB = 1 << 30
     names = args.variants.split(",")
-    vs = [Variant(n, os.path.join(ROOT, "abx", n + ".so")) for n in names]
+    # "name@c": abx/name.so with rs_set_occupancy_cap(c) (e.g. a compute-free twin at the
+    # occupancy its real kernel's registers allow)
+    vs = [Variant(n, os.path.join(ROOT, "abx", n.split("@")[0] + ".so"),
+                  int(n.split("@")[1]) if "@" in n else None) for n in names]
     print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
     for wl in args.workloads.split(","):
         k, m, S, N, mode = WORKLOADS[wl]
@@ -99,7 +106,7 @@ def main():
             mk = np.array([full & ~sum(1 << int(j) for j in rng.choice(t, size=min(4, m), replace=False))
                            for _ in range(N)])
             bound = 0
-        elif mode in ("recmix_out", "recmix1_out"):
+        elif mode in ("recmix_out", "recmix1_out", "recmixh_out"):
             lo = 1 if mode == "recmix1_out" else 0
             mk = np.full(N, full)
             for i, ne in enumerate(rng.integers(lo, m + 1, N)):
@@ -113,10 +120,11 @@ def main():
         alg = alg_bytes(wl)
         if mk is not None:
             mk = mk.astype(np.uint32)
-            if mode in ("recmix_out", "recmix1_out"):
+            if mode in ("recmix_out", "recmix1_out", "recmixh_out"):
                 nmiss = np.array([bin(int(x) ^ full).count("1") for x in mk])
                 alg = int(S * (k * np.count_nonzero(nmiss) + nmiss.sum()))
             md = torch.from_numpy(mk.view(np.int32)).cuda()
+            mh = np.ascontiguousarray(mk)  # host masks (recmixh_out): the engine uploads them
         for v in vs:
             v.lib.rs_set_out_pad_writes(v.ctx_for(k, m), 1 if args.out_pad else 0)
 
@@ -129,6 +137,9 @@ def main():
                 rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
                                                             md.data_ptr(), bound, outs[i % nb].data_ptr(), m * P,
                                                             None)
+            elif mode == "recmixh_out":
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                    mh.ctypes.data, N, 0, outs[i % nb].data_ptr(), m * P, None)
             else:
                 rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
                                                     md.data_ptr(), N, 1, outs[i % nb].data_ptr(), m * P, None)
