@@ -1106,6 +1106,11 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
 #ifndef RS_FLAT_EM_FULL
 #define RS_FLAT_EM_FULL 1
 #endif
+// RS_FLAT_ALIGNED (A/B): out-of-place per-stripe launches whose shard length is a
+// whole number of 64-column tasks also take the flat kernel (no task then straddles).
+#ifndef RS_FLAT_ALIGNED
+#define RS_FLAT_ALIGNED 0
+#endif
 
 
 template <int K, int M, int E>
@@ -1744,6 +1749,18 @@ static dim3 full_grid(uint64_t waves) {
 #ifndef RS_OCC_CAP_BS
 #define RS_OCC_CAP_BS RS_OCC_CAP
 #endif
+// Per-stripe stripe-aligned reconstructs with a bound of 1 or 2 (apply_kernel<K, M,
+// E <= 2, true>): 4 waves per SIMD when a stripe spans several 64-column tasks, 5
+// for a 1-erasure bound on single-task stripes, uncapped for 2 on single-task
+// stripes.  Same-process A/B over object sizes (profiles/r05k_ab_caps_sizes.log,
+// RS(4+2), 4 rounds): 1-erasure 16 KiB / 64 KiB / 1 MiB objects +4.2 / +3.8 / +2.4
+// points at 4 waves, 4 KiB objects +1.3 at 5 (-1.0 at 4); 2-erasure +0.8 to +1.1 at
+// 4 for 16 KiB and more, 4 KiB objects (the headline) -1.7 at 4 and level at 5-6;
+// RS(8+4) 64 KiB 1-erasure +0.6, 2-erasure level.  Encodes and uniform reconstructs
+// stay uncapped (4 waves: -1.4 to -5.3).  RS_OCC_CAP_PS_AUTO=0: uncapped (A/B).
+#ifndef RS_OCC_CAP_PS_AUTO
+#define RS_OCC_CAP_PS_AUTO 1
+#endif
 constexpr size_t kLdsPerCu = 160u * 1024u;
 
 // Dynamic LDS bytes that cap `fn` at `cap` workgroups per CU (0: none): halfway
@@ -1791,7 +1808,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       return name;
     }
   }
-  if (per_stripe && !generic && a.out && cols >= 64u && cols % 64u != 0u && a.data_sp + span < (1ull << 31) &&
+  if (per_stripe && !generic && a.out && cols >= 64u && (cols % 64u != 0u || RS_FLAT_ALIGNED) &&
+      a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
     if (const void* ff = pick_flat_ps(a.k, a.m, e, &name)) {
@@ -1829,7 +1847,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     // 76.4 %.  Partial grids (32 or 64 per CU, still looping) were slower than both.
     grid = full_grid(waves);
   }
-  if (hipLaunchKernel(fn, grid, dim3(256), args, generic ? 0 : occ_lds(fn, cap_of(RS_OCC_CAP_APPLY)), s) != hipSuccess)
+  uint32_t dcap = RS_OCC_CAP_APPLY;
+  if (RS_OCC_CAP_PS_AUTO && dcap == 0u && per_stripe && !generic && e <= 2)
+    dcap = a.blocks_per_stripe >= 2u ? 4u : (e == 1 ? 5u : 0u);
+  if (hipLaunchKernel(fn, grid, dim3(256), args, generic ? 0 : occ_lds(fn, cap_of(dcap)), s) != hipSuccess)
     return nullptr;
   return name;
 }

@@ -19,6 +19,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 WORKLOADS = {
     # name: (k, m, S, N, mode)  mode: enc | rec2u (uniform {0,1}) | rec2p (per-stripe 2-erasure)
     "rs42_4K_enc": (4, 2, 1024, 65536, "enc"),
+    # occupancy-cap study across object sizes (round 5): 16 KiB and 1 MiB objects
+    "rs42_16K_enc": (4, 2, 4096, 65536, "enc"),
+    "rs42_16K_rec1pb_out": (4, 2, 4096, 65536, "rec1pb_out"),
+    "rs42_16K_rec2p_out": (4, 2, 4096, 65536, "rec2p_out"),
+    "rs42_1M_enc": (4, 2, 262144, 1024, "enc"),
+    "rs42_1M_rec1pb_out": (4, 2, 262144, 1024, "rec1pb_out"),
+    "rs42_1M_rec2p_out": (4, 2, 262144, 1024, "rec2p_out"),
+    "rs63_48K_rec1pb_out": (6, 3, 8192, 16384, "rec1pb_out"),
+    "rs63_48K_rec2pb_out": (6, 3, 8192, 16384, "rec2pb_out"),
+    "rs104_80K_rec1pb_out": (10, 4, 8192, 16384, "rec1pb_out"),
+    "rs104_80K_rec2pb_out": (10, 4, 8192, 16384, "rec2pb_out"),
+    "rs104_80K_rec2p_out": (10, 4, 8192, 16384, "rec2p_out"),
+    "rs104_80K_recmix_out": (10, 4, 8192, 16384, "recmix_out"),
     "rs42_4K_rec2p": (4, 2, 1024, 65536, "rec2p"),
     "rs42_4K_rec2u": (4, 2, 1024, 65536, "rec2u"),
     "rs42_4K_rec45p": (4, 2, 1024, 65536, "rec45p"),
