@@ -1106,8 +1106,13 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
 #ifndef RS_FLAT_EM_FULL
 #define RS_FLAT_EM_FULL 1
 #endif
-// RS_FLAT_ALIGNED (A/B): out-of-place per-stripe launches whose shard length is a
-// whole number of 64-column tasks also take the flat kernel (no task then straddles).
+// Out-of-place per-stripe launches whose shard length is a whole number of 64-column
+// tasks (no task then straddles) take the flat kernel too for RS(10+4) with a bound
+// of 2 or more: same-process A/B at 80 KiB objects (profiles/r05k_ab_flatal.log, S =
+// 8 192, 4 rounds) bounded 2-erasure 68.0 -> 76.4 %, unbounded 2-erasure +0.8, mixed
+// 70.0 -> 73.0 %; 1-erasure -0.3, and every other shape loses (RS(8+4) 2-erasure
+// -1.9 / -5.5, RS(4+2) -4.9 to -7.2, RS(6+3) -1.0) except RS(8+4) mixed (+1.7).
+// RS_FLAT_ALIGNED=1 routes every shape with a flat kernel there (A/B).
 #ifndef RS_FLAT_ALIGNED
 #define RS_FLAT_ALIGNED 0
 #endif
@@ -1808,7 +1813,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       return name;
     }
   }
-  if (per_stripe && !generic && a.out && cols >= 64u && (cols % 64u != 0u || RS_FLAT_ALIGNED) &&
+  if (per_stripe && !generic && a.out && cols >= 64u &&
+      (cols % 64u != 0u || RS_FLAT_ALIGNED || (a.k == 10 && e >= 2)) &&
       a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks

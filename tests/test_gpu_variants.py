@@ -18,7 +18,7 @@ from replication_erasurecoding_object_store_amd.ec import ECError
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(4, 2, 1024), (8, 4, 8192), (10, 4, 6554), (10, 4, 413), (6, 3, 1000), (4, 2, 1000)]
+SHAPES = [(4, 2, 1024), (8, 4, 8192), (10, 4, 6554), (10, 4, 413), (6, 3, 1000), (4, 2, 1000), (10, 4, 8192)]
 
 
 @pytest.fixture(scope="module")
@@ -179,7 +179,8 @@ def test_devmask_bound_flags_and_skips_excess(engines, k, m, S, bound):
 # Larger batches than the parity tests, two pattern draws each, every output row
 # and every unused output slot compared (vectorised).
 @pytest.mark.parametrize("k,m,S,bound", [(8, 4, 6554, 1), (10, 4, 6554, 2), (8, 4, 6554, 4), (8, 4, 8192, 1),
-                                         (10, 4, 6554, 1), (8, 4, 8192, 4), (10, 4, 6554, 4), (4, 2, 1024, 2)])
+                                         (10, 4, 6554, 1), (8, 4, 8192, 4), (10, 4, 6554, 4), (4, 2, 1024, 2),
+                                         (10, 4, 8192, 2), (10, 4, 8192, 4)])
 def test_out_of_place_stress(engines, k, m, S, bound):
     import torch
 
