@@ -111,6 +111,18 @@ WORKLOADS = {
 }
 
 
+# survey grid (round 5): every call kind on the shapes the reference's configs and
+# sweep use, plus 16 KiB, 1 MiB and task-aligned RS(10+4) objects
+_SURVEY_SHAPES = {"rs42_4K": (4, 2, 1024, 65536), "rs42_64K": (4, 2, 16384, 16384),
+                  "rs42_1M": (4, 2, 262144, 1024), "rs84_64K": (8, 4, 8192, 16384),
+                  "rs104_64K": (10, 4, 6554, 16384), "rs104_80K": (10, 4, 8192, 16384),
+                  "rs63_48K": (6, 3, 8192, 16384)}
+SURVEY_MODES = ("enc", "ver", "rec2u", "rec2u_out", "rec2p", "rec1pb_out", "rec2pb_out", "rec2p_out", "recmix_out")
+for _n, (_k, _m, _S, _N) in _SURVEY_SHAPES.items():
+    for _mode in SURVEY_MODES:
+        WORKLOADS.setdefault(f"{_n}_{_mode}", (_k, _m, _S, _N, _mode))
+
+
 def alg_bytes(name):
     """Algorithmic HBM bytes of one launch of workload `name`."""
     k, m, S, N, mode = WORKLOADS[name]

@@ -31,6 +31,9 @@ SIGS = {
     "rs_destroy": (None, [_vp]),
     "rs_encode_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _i, _vp]),
     "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
+    "rs_reconstruct_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp]),
+    "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
+    "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
     "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
     "rs_set_out_pad_writes": (_i, [_vp, _i]),
@@ -95,7 +98,12 @@ def main():
         if mode in ("rec1pb_out", "rec1p_out"):
             mk = full & ~(1 << rng.integers(0, t, N))
             bound = 1 if mode == "rec1pb_out" else 0
-        elif mode in ("rec2pb_out", "rec2p_out"):
+        elif mode in ("rec2u", "rec2u_out"):  # one host pattern for the batch: data 0 and 1 lost
+            mk = np.array([full & ~0b11])
+            bound = 0
+        elif mode == "ver":
+            mk, bound = None, 0
+        elif mode in ("rec2pb_out", "rec2p_out", "rec2p"):
             import itertools
 
             pairs = np.array(list(itertools.combinations(range(t), 2)))
@@ -117,6 +125,7 @@ def main():
             mk, bound = None, 0
         else:
             raise SystemExit(f"{wl}: mode {mode} not supported here")
+        bad = torch.zeros(N, dtype=torch.int32, device="cuda")
         alg = alg_bytes(wl)
         if mk is not None:
             mk = mk.astype(np.uint32)
@@ -133,6 +142,18 @@ def main():
             d, p = bufs[i % nb]
             if mode == "enc":
                 rc = v.lib.rs_encode_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, 0, None)
+            elif mode == "ver":
+                rc = v.lib.rs_verify_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, bad.data_ptr(), 0,
+                                           None)
+            elif mode == "rec2u":  # in place: rewrites the lost shards with their own bytes
+                rc = v.lib.rs_reconstruct_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, mh.ctypes.data,
+                                                1, 0, None)
+            elif mode == "rec2u_out":
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                    mh.ctypes.data, 1, 0, outs[i % nb].data_ptr(), m * P, None)
+            elif mode == "rec2p":  # in place, per-stripe device masks
+                rc = v.lib.rs_reconstruct_batch_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                        md.data_ptr(), None)
             elif bound:
                 rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
                                                             md.data_ptr(), bound, outs[i % nb].data_ptr(), m * P,
@@ -171,7 +192,8 @@ def main():
         for v in vs:
             run(v, 0)
             torch.cuda.synchronize()
-            o = (outs[0] if mode != "enc" else bufs[0][1]).cpu().numpy()
+            o = (bufs[0][1] if mode == "enc" else bad if mode == "ver" else
+                 bufs[0][0] if mode in ("rec2u", "rec2p") else outs[0]).cpu().numpy()
             digests[v.name] = hash(o.tobytes())
             kname = v.lib.rs_last_kernel(v.ctx_for(k, m)).decode()
             base = np.array(res[vs[0].name])
