@@ -627,15 +627,16 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             timed("reconstruct2_exact_rows", lambda i: w.rec(i, bound=2), alg["reconstruct"])
             timed("reconstruct1_exact_rows", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
             e2.set_out_pad_writes(True)
+        # no caller bound (kernel sized for m; for RS(4+2) the bounded 2-erasure legs
+        # above are that kernel already); the mixed legs: 0..m erasures per stripe,
+        # intact stripes included, device and host masks
+        mix = w.mix_alg_bytes()
+        ent["mixed_alg_bytes"] = mix
         if mm > 2:
-            # no caller bound (kernel sized for m); the mixed legs: 0..m erasures per
-            # stripe, intact stripes included, device and host masks
-            mix = w.mix_alg_bytes()
-            ent["mixed_alg_bytes"] = mix
             timed("reconstruct2_unbounded", w.rec, alg["reconstruct"])
             timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])
-            timed("reconstruct_mixed_unbounded", w.rec_mix, mix)
-            timed("reconstruct_mixed_host", lambda i: w.rec_mix(i, host=True), mix)
+        timed("reconstruct_mixed_unbounded", w.rec_mix, mix)
+        timed("reconstruct_mixed_host", lambda i: w.rec_mix(i, host=True), mix)
         ent["ok"] = rdist.all_true(w.check())
         ent["kernels"] = kern
         w.close()

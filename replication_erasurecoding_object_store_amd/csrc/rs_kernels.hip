@@ -187,6 +187,11 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS
 #define RS_WAVE_ROWS 1
 #endif
+// RS_PS_SKIP_INTACT: per-stripe E <= 2 tasks of stripes that miss nothing skip their
+// loads and stores (1) or load and drop them (0, A/B).
+#ifndef RS_PS_SKIP_INTACT
+#define RS_PS_SKIP_INTACT 1
+#endif
 // Row paths of the E = M kernels, RS_EM_EMIT_EACH_{FLAT,APPLY}: 1 = each path computes
 // only its own rows (no row 0 ahead of the branch) and 3+ rows are stored one by one
 // as they are computed; 0 = row 0 first, then the other rows, then one store group.
@@ -595,6 +600,13 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
         x[c] = bload16(r, loff, 0);
       }
     } else {
+      // E <= 2 per-stripe launches run one task per wave (a full grid), so a task of an
+      // intact (or skipped) stripe ends its wave here: no loads, no stores.  RS(4+2)
+      // device masks without a bound are this kernel (E = M = 2), and a scan's mixed
+      // batch had every intact stripe read for nothing.
+      if constexpr (PER_STRIPE && RS_PS_SKIP_INTACT) {
+        if (!work) continue;
+      }
 #pragma unroll
       for (int c = 0; c < K; ++c) x[c] = load16(slot_ptr(a, K, stripe, PER_STRIPE ? pv.in_idx(c) : uin[c]) + off);
     }
