@@ -1128,6 +1128,14 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
 #ifndef RS_FLAT_ALIGNED
 #define RS_FLAT_ALIGNED 0
 #endif
+// RS_FLAT_UNIFORM (A/B, off): out-of-place reconstructs with one erasure pattern for
+// the batch take the flat kernel with that one plan for every stripe wherever the
+// per-stripe form would.  The stripe-aligned uniform kernel, whose slots are resolved
+// once per launch, stays ahead (profiles/r05m_ab_uniform.log: RS(10+4) 2-erasure at
+// 64 / 80 KiB objects -3.5 / -3.8 points through the flat kernel).
+#ifndef RS_FLAT_UNIFORM
+#define RS_FLAT_UNIFORM 0
+#endif
 
 
 template <int K, int M, int E>
@@ -1150,8 +1158,17 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
   const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
   uint32_t bad = 0u;
 
-  // stripe s's present mask (a skipped one: all present) and plan
+  // stripe s's present mask (a skipped one: all present) and plan; a uniform launch
+  // (no masks: one erasure pattern for the batch) has the one plan for every stripe
+  const bool uni = a.present_masks == nullptr;
   auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
+    if (uni) {
+      const uint8_t* p = uniform_ptr(a.plans);
+      const PlanView pv(p, K, M);
+      m = pv.present() & full;
+      nout = pv.n_out();
+      return p;
+    }
     const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
     uint32_t pid = as_const<uint32_t>(a.lut)[(~present) & full];
     bad |= (pid == kPlanInvalid) ? 1u : 0u;
@@ -1825,7 +1842,7 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       return name;
     }
   }
-  if (per_stripe && !generic && a.out && cols >= 64u &&
+  if ((per_stripe || (RS_FLAT_UNIFORM && !a.data_inputs)) && !generic && a.out && cols >= 64u &&
       (cols % 64u != 0u || RS_FLAT_ALIGNED || (a.k == 10 && e >= 2)) &&
       a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
