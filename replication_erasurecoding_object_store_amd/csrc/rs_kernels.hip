@@ -441,9 +441,11 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
   for (int c = 0; c < K; ++c) {
     if (c % RS_ROWIX_GROUP == 0) {
       tg = plan;
-      gt = kGfPermTabs.v;
       asm volatile("" : "+s"(tg));  // one opaque base per group: tables never all in SGPRs
-      asm volatile("" : "+s"(gt));
+      if constexpr (RS_EM_COEF) {
+        gt = kGfPermTabs.v;
+        asm volatile("" : "+s"(gt));
+      }
     }
     const PlanView pc(tg, K, M);
     const RS_CONST uint32_t* tb =
