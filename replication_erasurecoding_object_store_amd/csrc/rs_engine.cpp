@@ -906,7 +906,7 @@ int ensure_pipe_stream(Engine* e, int i) {
 // must move every slot a stripe might use).  Memory the library does not own --
 // pageable, rs_host_register'ed or pinned by someone else -- never qualifies: a
 // kernel never reads or writes pages whose lifetime and placement the library does
-// not control (DESIGN.md §2).  Returns RS_ERR_NOT_SUPPORTED when the batch does
+// not control (DESIGN.md Appendix A.1).  Returns RS_ERR_NOT_SUPPORTED when the batch does
 // not qualify.
 int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
                    const uint32_t* masks_host, int e_out, uint32_t* bad_host) {
@@ -1859,7 +1859,7 @@ bool reg_erase(rs_ctx* c, void* ptr, bool owned) {
 // hipHostRegister'ed pageable memory as a user-pointer range whose pages the kernel
 // may still migrate, compact or collapse into huge pages under a running kernel;
 // the round-3 records show lost in-place writes and a late-reported illegal address
-// right after the only tests that ran GPU work on such ranges (DESIGN.md §2).  So no
+// right after the only tests that ran GPU work on such ranges (DESIGN.md Appendix A.1).  So no
 // kernel and no DMA of this library touches caller pages in place: calls on
 // registered buffers are staged through the library's own page-locked memory, and
 // in-place work needs rs_host_alloc.

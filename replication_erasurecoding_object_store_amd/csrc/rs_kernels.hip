@@ -485,7 +485,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // max_missing bound) is skipped and flagged (status bit 1).
 // Every trip issues the same loads; the wave-uniform branches differ only in VALU
 // work and in how many stores end the trip, so the compiler's vmcnt bookkeeping
-// stays exact (a branch around the loads does not: DESIGN.md §9).
+// stays exact (a branch around the loads does not: DESIGN.md Appendix A.5).
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
       // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
       // (profiles/r02c_ab_ix_rows.log).  Input-outer passes of <= 2 rows instead
       // (round 4) lost 9-10 points on 4-erasure and mixed batches
-      // (profiles/r04g_ab_twopass.log, DESIGN.md §9).
+      // (profiles/r04g_ab_twopass.log, DESIGN.md Appendix A.5).
       Idx3 ix[K][4];
 #pragma unroll
       for (int c = 0; c < K; ++c)
