@@ -187,6 +187,15 @@ constexpr int out_cpol() {
 #ifndef RS_WAVE_ROWS
 #define RS_WAVE_ROWS 1
 #endif
+// RS_APPLY_MIN_WAVES: launch bounds asking the compiler to fit the apply_kernel
+// instantiations with K <= 8 and E <= 2 into that many waves per SIMD (0: none).  The
+// uniform-plan RS(8+4) 2-erasure kernel then drops from 135 to 117 VGPRs (3 -> 4
+// waves, no scratch): same-process A/B (profiles/r05n_ab_lb4.log) one pattern for the
+// batch +6.0 points out of place, +3.9 in place; every other shape level.  K = 10
+// with E >= 2 would spill to scratch at 4 waves and is left alone.
+#ifndef RS_APPLY_MIN_WAVES
+#define RS_APPLY_MIN_WAVES 4
+#endif
 // RS_PS_SKIP_INTACT: per-stripe E <= 2 tasks of stripes that miss nothing skip their
 // loads and stores (1) or load and drop them (0, A/B).
 #ifndef RS_PS_SKIP_INTACT
@@ -487,7 +496,8 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // work and in how many stores end the trip, so the compiler's vmcnt bookkeeping
 // stays exact (a branch around the loads does not: DESIGN.md Appendix A.5).
 template <int K, int M, int E, bool PER_STRIPE>
-__global__ __launch_bounds__(256) void apply_kernel(const KernelArgs a) {
+__global__ __launch_bounds__(256, (RS_APPLY_MIN_WAVES && K <= 8 && E <= 2) ? RS_APPLY_MIN_WAVES : 1) void apply_kernel(
+    const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
