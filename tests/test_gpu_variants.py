@@ -315,3 +315,39 @@ def test_device_copy_exact(engines, nbytes):
     torch.cuda.synchronize()
     assert torch.equal(dst[:nbytes], src[:nbytes])
     assert (dst[nbytes:] == 0x5A).all(), "bytes past the copy written"
+
+
+@pytest.mark.parametrize("k,m,S", [(10, 4, 6554), (4, 2, 16384), (8, 4, 8192), (4, 2, 1024)])
+def test_occupancy_cap_never_changes_bytes(engines, k, m, S):
+    """rs_set_occupancy_cap (dynamic-LDS reservation per launch): every cap, the
+    tuned defaults (-1) and none (0) give the oracle's bytes on the encode, bounded,
+    unbounded and mixed per-stripe paths; caps outside -1..32 are refused."""
+    import torch
+
+    eng = BatchEngine(k, m, 0)  # its own context: the cap is context-wide
+    try:
+        t, N, P = k + m, 257, shard_pitch_for(S)
+        data, parity, uni = _codewords(eng, k, m, S, N, 4242 + S)
+        rng = np.random.default_rng(S + 1)
+        mixed = _masks(rng, N, t, 0, m)
+        for cap in (-1, 0, 2, 3, 4, 8, 32):
+            eng.set_occupancy_cap(cap)
+            p2 = torch.full_like(parity, 0xEE)
+            eng.encode(data, p2, S, N)
+            torch.cuda.synchronize()
+            assert np.array_equal(p2.cpu().numpy()[:, :, :S], uni[:, k:, :S]), ("encode", cap)
+            for bound, masks in ((1, _masks(rng, N, t, 1, 1)), (0, mixed)):
+                out = torch.full((N, m, P), 0xC3, dtype=torch.uint8, device="cuda")
+                eng.reconstruct_out(data, parity, out, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda(),
+                                    max_missing=bound)
+                eng.sync()
+                o = out.cpu().numpy()
+                for i in range(N):
+                    miss = [s for s in range(t) if not (masks[i] >> s) & 1]
+                    for r, s in enumerate(miss):
+                        assert np.array_equal(o[i, r, :S], uni[i, s, :S]), (cap, bound, i, s)
+        for bad in (-2, 33):
+            with pytest.raises(ECError):
+                eng.set_occupancy_cap(bad)
+    finally:
+        eng.close()
