@@ -95,27 +95,19 @@ def parse():
     return p.parse_args()
 
 
-def _free_port():
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def launch_ranks(n):
     """`--gpus N > 1` with no torchrun environment: one fresh process per GPU.
 
     The parent touches no GPU (no torch import at all): it starts N children of this
-    same command with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set,
+    same command with RANK / LOCAL_RANK / WORLD_SIZE set and a file-store rendezvous,
     as torch.distributed.run would, waits for all of them and returns a non-zero
     code if any fails -- terminating the others, which would otherwise wait forever
     at the next barrier.  Rank 0 prints the JSON line (its stdout is this process's).
     The reference likewise runs one codec per process (cmd/api/main.go:206)."""
+    import shutil
     import signal
     import subprocess
+    import tempfile
 
     procs = []
 
@@ -132,10 +124,14 @@ def launch_ranks(n):
 
     signal.signal(signal.SIGTERM, on_signal)
     signal.signal(signal.SIGINT, on_signal)
-    port = str(_free_port())
+    # rendezvous through a file store in a fresh directory (dist.init): no TCP port
+    # to race for between picking it here and rank 0 binding it
+    rdzv_dir = tempfile.mkdtemp(prefix="rsgpu_rdzv_")
+    rdzv = os.path.join(rdzv_dir, "store")
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+                   MASTER_ADDR="127.0.0.1", RSGPU_RDZV_FILE=rdzv)
+        env.pop("MASTER_PORT", None)
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       start_new_session=True))
@@ -154,6 +150,7 @@ def launch_ranks(n):
                 stop(live)
         if live:
             time.sleep(0.05)
+    shutil.rmtree(rdzv_dir, ignore_errors=True)
     return rc
 
 
@@ -172,11 +169,46 @@ def dry_run(args):
     dt = rdist.max_over_ranks(time.perf_counter() - t0 + 1e-3 * rank)
     ok = rdist.all_true(True)
     pids = rdist.distinct_count(os.getpid())  # a collective: every rank calls it
+    # the scaling fields' collectives and arithmetic on sleeps: alone each rank
+    # "processes" 1 MiB in 20 ms, together in 20 ms x (1 + rank / 10)
+    solo = solo_times(rdist, lambda: (time.sleep(0.02), 0.02)[1])
+    conc = rdist.gather_floats(0.02 * (1 + rank / 10))
+    sc = scaling_fields(conc, solo, [1 << 20] * world)
     if rank == 0:
         print(json.dumps({"metric": "dry run (no GPU): rank launcher + control collectives", "value": None,
                           "n_gpus": world, "physical_gpus": 0, "ranks_ok": ok, "max_rank_s": dt,
-                          "pids_distinct": pids}), flush=True)
+                          "pids_distinct": pids, "scaling_check": sc}), flush=True)
     rdist.shutdown()
+
+
+def solo_times(rdist, fn):
+    """Each rank runs fn() ALONE, in rank order, while every other rank waits at a
+    barrier; returns every rank's result (seconds) in rank order.  With the ranks on
+    distinct GPUs this is each GPU's rate with the node otherwise idle -- the
+    denominator of the per-GPU efficiency (the first 8-GPU line must
+    state its own efficiency)."""
+    rank, _, world = rdist.world()
+    mine = None
+    for r in range(world):
+        rdist.barrier()
+        if r == rank:
+            mine = fn()
+        rdist.barrier()
+    return rdist.gather_floats(mine)
+
+
+def scaling_fields(conc_s, solo_s, bytes_per_rank):
+    """Per-GPU efficiency of a run whose ranks each process bytes_per_rank[r] bytes:
+    the concurrent aggregate (all ranks' bytes / the slowest rank's concurrent time)
+    over world x the mean solo rate.  conc_s / solo_s: per-rank seconds, concurrent
+    and alone.  Rates in GiB/s."""
+    world = len(conc_s)
+    per_rank = [b / t / GiB for b, t in zip(bytes_per_rank, conc_s)]
+    solo = [b / t / GiB for b, t in zip(bytes_per_rank, solo_s)]
+    agg = sum(bytes_per_rank) / max(conc_s) / GiB
+    return {"per_rank_GiBps": [round(x, 2) for x in per_rank], "solo_GiBps": [round(x, 2) for x in solo],
+            "concurrent_aggregate_GiBps": round(agg, 2),
+            "per_gpu_efficiency": round(agg / (world * float(np.mean(solo))), 4)}
 
 
 def two_erasure_masks(rng, n, t):
@@ -295,10 +327,26 @@ class RSWorkload:
             self.enc(i)
             self.rec(i)
         torch.cuda.synchronize()
+        self.last_own_s = time.perf_counter() - t0  # this rank's own time (no closing barrier)
         barrier()
         dt = time.perf_counter() - t0
         self.eng.sync()
         return dt
+
+    def solo_steps(self, steps):
+        """`steps` steps on this rank with no barrier inside (solo_times runs it while
+        every other rank waits)."""
+        torch = self.torch
+        for i in range(2):
+            self.enc(i)
+            self.rec(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            self.enc(i)
+            self.rec(i)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
 
     def kernel_ms(self, min_ms=100.0):
         """Each kernel's average launch duration: one HIP event pair around >= min_ms
@@ -378,6 +426,33 @@ def cpu_info():
     return model, os.cpu_count() or 1, affinity
 
 
+def cpu_quota(cgroup="/sys/fs/cgroup"):
+    """(threads, quota, source): the CPUs this process may keep busy.  The cgroup's
+    CPU bandwidth quota when one is set (cgroup v2 cpu.max, else v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), capped by the affinity mask; the affinity
+    mask alone otherwise.  The reference's codec sizes itself by runtime.NumCPU()
+    (internal/ec/ec.go:26), which a container's quota also bounds in practice."""
+    _, nproc, affinity = cpu_info()
+    quota, source = None, "no cgroup CPU quota: every CPU in the affinity mask"
+    try:
+        with open(os.path.join(cgroup, "cpu.max")) as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota, source = int(q) / int(period), f"{cgroup}/cpu.max ({q} {period})"
+    except (OSError, ValueError):
+        try:
+            with open(os.path.join(cgroup, "cpu", "cpu.cfs_quota_us")) as f:
+                q = int(f.read())
+            with open(os.path.join(cgroup, "cpu", "cpu.cfs_period_us")) as f:
+                period = int(f.read())
+            if q > 0:
+                quota, source = q / period, f"{cgroup}/cpu/cpu.cfs_quota_us ({q} / {period})"
+        except (OSError, ValueError):
+            pass
+    threads = affinity if quota is None else max(1, min(affinity, int(quota)))
+    return threads, quota, source
+
+
 def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
     """CPU codec on a bounded sample of the workload.  With `eng`, the same sample's
     data shards are also encoded on the GPU and compared with the CPU's parity
@@ -388,7 +463,7 @@ def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
     P = S  # host layout: contiguous shards
     buf = np.random.default_rng(1).integers(0, 256, N_sample * t * P, dtype=np.uint8)
     model, nproc, affinity = cpu_info()
-    threads = max(1, min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity))))
+    threads, quota, quota_src = cpu_quota()
     mat = rs_oracle.build_matrix(k, m)
     surv, miss, rows = rs_oracle.decode_rows(k, m, [0, 0] + [1] * (t - 2))
     level = 0
@@ -431,10 +506,13 @@ def cpu_baseline(k, m, S, N_sample, seconds, torch=None, eng=None):
         "cpu_model": model,
         "nproc": nproc,
         "affinity_cpus": affinity,
+        "cpu_quota": quota,
+        "cores_source": quota_src,
         "sample": f"{done} passes x (encode + 2-erasure reconstruct) of {N_sample} x {k * S // 1024} KiB "
                   f"RS({k}+{m}) stripes in {dt:.1f} s, {simd}, one stripe per task, {threads} threads on "
-                  f"'{model}' (nproc {nproc}, {affinity} CPUs in this process's affinity mask; C restatement of "
-                  f"klauspost's CPU kernels, Go reference absent)",
+                  f"'{model}' (nproc {nproc}, {affinity} CPUs in this process's affinity mask, CPU quota "
+                  f"{quota if quota is not None else 'none'}: threads = the quota, capped by the mask; C restatement "
+                  f"of klauspost's CPU kernels, Go reference absent)",
     }
 
 
@@ -544,20 +622,35 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
         dn[lost_d] = 0
         pn[lost_p] = 0
 
-    e2e, ok = {}, True
+    def one_pass():
+        erase()
+        t0 = time.perf_counter()
+        eng.reconstruct_host(dn, pn, S, N, masks)
+        return time.perf_counter() - t0
+
+    e2e, ok, scaling = {}, True, {}
+    share_bytes = rdist.gather_floats(float(N * k * S))
     for zc in (True, False):
         eng.set_host_zero_copy(zc)
         erase()
         eng.reconstruct_host(dn, pn, S, N, masks)  # warm: pipeline slabs, LUT
-        times = []
+        times, own = [], []
         for _ in range(2):
             erase()
             rdist.barrier()
             t0 = time.perf_counter()
             eng.reconstruct_host(dn, pn, S, N, masks)
-            times.append(rdist.max_over_ranks(time.perf_counter() - t0))
+            own.append(time.perf_counter() - t0)
+            times.append(rdist.max_over_ranks(own[-1]))
         ok = ok and bool(np.array_equal(dn[sample], ref_d) and np.array_equal(pn[sample], ref_p))
-        e2e[eng.last_host_path()] = min(times)
+        path = eng.last_host_path()
+        e2e[path] = min(times)
+        if world > 1:
+            # each rank's share alone (host DRAM and PCIe to itself), then the
+            # concurrent passes above: how much the ranks slow each other down
+            alone = solo_times(rdist, lambda: min(one_pass(), one_pass()))
+            scaling[path] = scaling_fields(rdist.gather_floats(min(own)), alone, share_bytes)
+            ok = ok and bool(np.array_equal(dn[sample], ref_d) and np.array_equal(pn[sample], ref_p))
     eng.set_host_zero_copy(True)
     # device-resident, same masks, in place
     dd = data.cuda()
@@ -577,8 +670,112 @@ def healer_mix(torch, eng, rdist, k, m, S, N_total, seed=0x5EED0005):
             "e2e_GiBps": {p: round(user / t / GiB, 2) for p, t in e2e.items()},
             "e2e_objects_per_s": {p: round(N_total / t) for p, t in e2e.items()},
             "device_GiBps": round(user / t_dev / GiB, 1), "ok_sample": rdist.all_true(ok),
+            **({"e2e_scaling_check": scaling} if scaling else {}),
             "note": "zero-copy: kernel reads survivors / writes missing shards over PCIe in place; "
-                    "staged: every k+m slot DMA'd each way"}
+                    "staged: the data slots H2D, parity survivors gathered on the host, the missing rows D2H "
+                    "and scattered"}
+
+
+def multi_ctx_leg(torch, rdist, eng, k, m, N=1 << 18, S=1024, burst=2048, burst_S=16384):
+    """One library context over every GPU this process sees (rs_create_multi(k, m,
+    0): what the Go shim's NewService builds, cmd/api/main.go:206) on rank 0 while
+    the other ranks wait at a barrier.  Runs
+      * a host batch through fan_out (contiguous stripe ranges, one per GPU, on the
+        engines' worker threads): encode, then a per-stripe 1-erasure repair, N
+        objects of k*S bytes in the context's page-locked memory (zero-copy) and
+        again staged;
+      * a coalesced burst (rs_co_encode_many: batches opened on the least-loaded
+        GPU) of `burst` objects of k*burst_S bytes;
+    and reports each GPU's kernel launches (rs_device_launches) for each part.
+    Checks, outside the timed region and without the CPU oracle: the multi-GPU
+    parity equals the single-GPU engine's device encode of the same data, and every
+    erased shard comes back equal to the original."""
+    from replication_erasurecoding_object_store_amd.batch import BatchEngine
+    from replication_erasurecoding_object_store_amd.coalescer import CoalescingService
+
+    rank, _, _ = rdist.world()
+    res = None
+    rdist.barrier()
+    if rank == 0:
+        t = k + m
+        mc = BatchEngine(k, m, "all")
+        res = {"devices": mc.devices(), "objects": N, "object_bytes": k * S}
+        rng = np.random.default_rng(0x5EED0008)
+        data = mc.host_alloc(N * k * S).reshape(N, k, S)
+        parity = mc.host_alloc(N * m * S).reshape(N, m, S)
+        data[:] = rng.integers(0, 256, (N, k, S), dtype=np.uint8)
+        # the single-GPU engine's parity of a sample, computed on the device
+        sample = rng.choice(N, size=4096, replace=False)
+        dsamp = torch.from_numpy(np.ascontiguousarray(data[sample])).cuda()
+        psamp = torch.empty((len(sample), m, S), dtype=torch.uint8, device="cuda")
+        eng.encode(dsamp, psamp, S, len(sample))
+        want_p = psamp.cpu().numpy()
+        lost = rng.integers(0, t, N)
+        masks = (((1 << t) - 1) & ~(1 << lost)).astype(np.uint32)
+        ok = True
+        try:
+            for zc in (True, False):
+                mc.set_host_zero_copy(zc)
+                parity[:] = 0
+                before = mc.device_launches()
+                t0 = time.perf_counter()
+                mc.encode_host(data, parity, S, N)
+                t_enc = time.perf_counter() - t0
+                path = mc.last_host_path()
+                ok_enc = bool(np.array_equal(parity[sample], want_p))
+                ref_d, ref_p = data[sample].copy(), parity[sample].copy()
+                # erase one shard per stripe, repair (every stripe's own pattern)
+                ld = (lost < k)
+                data[np.nonzero(ld)[0], lost[ld]] = 0
+                parity[np.nonzero(~ld)[0], lost[~ld] - k] = 0
+                t0 = time.perf_counter()
+                mc.reconstruct_host(data, parity, S, N, masks)
+                t_rec = time.perf_counter() - t0
+                ok_rec = bool(np.array_equal(data[sample], ref_d) and np.array_equal(parity[sample], ref_p))
+                after = mc.device_launches()
+                ok = ok and ok_enc and ok_rec
+                res[path] = {"encode_GiBps": round(N * k * S / t_enc / GiB, 2),
+                             "reconstruct1_GiBps": round(N * k * S / t_rec / GiB, 2),
+                             "launches_per_device": [a - b for a, b in zip(after, before)],
+                             "parity_equals_single_gpu": ok_enc, "repair_ok": ok_rec}
+        finally:
+            mc.set_host_zero_copy(True)
+            mc.host_free(data)
+            mc.host_free(parity)
+            mc.close()
+        # coalesced per-object burst over every GPU
+        cs = CoalescingService(k, m, "all")
+        try:
+            objs = []
+            bd = rng.integers(0, 256, (burst, k, burst_S), dtype=np.uint8)
+            for i in range(burst):
+                objs.append([bytearray(bd[i, c].tobytes()) for c in range(k)] + [bytearray(burst_S) for _ in range(m)])
+            before = cs.device_launches()
+            t0 = time.perf_counter()
+            errs = cs.EncodeMany(objs)
+            t_b = time.perf_counter() - t0
+            after = cs.device_launches()
+            dd = torch.from_numpy(bd).cuda()
+            pp = torch.empty((burst, m, burst_S), dtype=torch.uint8, device="cuda")
+            eng.encode(dd, pp, burst_S, burst)
+            want = pp.cpu().numpy()
+            ok_b = all(e is None for e in errs) and all(
+                bytes(objs[i][k + p]) == want[i, p].tobytes() for i in range(burst) for p in range(m))
+            ok = ok and ok_b
+            res["coalesced_burst"] = {"objects": burst, "object_bytes": k * burst_S,
+                                      "GiBps": round(burst * k * burst_S / t_b / GiB, 2),
+                                      "launches_per_device": [a - b for a, b in zip(after, before)],
+                                      "parity_equals_single_gpu": ok_b, **cs.stats()}
+        finally:
+            cs.close()
+        res["devices_used"] = sum(1 for i in range(len(res["devices"]))
+                                  if any(res[p]["launches_per_device"][i] for p in ("zero-copy", "staged",
+                                                                                      "coalesced_burst")
+                                         if p in res))
+        res["ok"] = ok
+        torch.cuda.empty_cache()
+    rdist.barrier()
+    return res
 
 
 def kmsweep(torch, rdist, rotate, min_ms=100.0):
@@ -602,23 +799,32 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
         ent = {"shard_len": SS, "stripes_per_gpu": NN, "min_timed_ms": min_ms}
         kern = {}
 
-        def timed(key, fn, bytes_):
+        def timed(key, fn, bytes_, solo=False):
             rdist.barrier()
-            ms, reps = sustained_kernel_ms(torch, fn, min_ms)
-            ms = rdist.max_over_ranks(ms)
+            ms_own, reps = sustained_kernel_ms(torch, fn, min_ms)
+            ms = rdist.max_over_ranks(ms_own)
             kern[key] = e2.last_kernel()
             ent[f"{key}_GiBps"] = round(world * NN * kk * SS / (ms * 1e-3) / GiB, 1)
             ent[f"{key}_hbm_frac"] = round(bytes_ / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             ent[f"{key}_launches"] = reps
+            if solo and world > 1:
+                # the same launches on each rank alone, then the efficiency of the
+                # concurrent window above (per-GPU rates in user GiB/s)
+                conc = rdist.gather_floats(ms_own * 1e-3)
+                alone = solo_times(rdist, lambda: sustained_kernel_ms(torch, fn, min_ms)[0] * 1e-3)
+                sc = scaling_fields(conc, alone, [NN * kk * SS] * world)
+                ent[f"{key}_per_rank_GiBps"] = sc["per_rank_GiBps"]
+                ent[f"{key}_solo_GiBps"] = sc["solo_GiBps"]
+                ent[f"{key}_per_gpu_efficiency"] = sc["per_gpu_efficiency"]
 
-        timed("encode", w.enc, alg["encode"])
+        timed("encode", w.enc, alg["encode"], solo=True)
         if SS % 128:
             # rs_set_parity_pad_writes: parity shards end on whole 128-B lines (the
             # bench's own layout, pitch 256-B aligned); bytes counted stay N*S*(K+M)
             e2.set_parity_pad_writes(True)
             timed("encode_parity_pad", w.enc, alg["encode"])
             e2.set_parity_pad_writes(False)
-        timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"])
+        timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"], solo=True)
         timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
         if SS % 128:
             # output rows end on whole 128-B lines by default (round 5); the same legs
@@ -748,8 +954,7 @@ def sha256_rate(torch, eng, N=65536, length=4096, reps=5, cpu_seconds=3.0):
     ok = all(out[i].cpu().numpy().tobytes() == hashlib.sha256(host[i].tobytes()).digest() for i in range(0, 256, 17))
     from oracle import rs_oracle
 
-    _, _, affinity = cpu_info()
-    threads = min(affinity, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    threads, _, _ = cpu_quota()
     sample = bufs[0][:8192].cpu().numpy()
     ns, t_cpu, ni = 0, 0.0, False
     while t_cpu < cpu_seconds:
@@ -869,6 +1074,15 @@ def main():
         dt2 = rdist.max_over_ranks(w.run_steps(steps2, 2, rdist.barrier))
         sustained = {"steps": steps2, "timed_s": round(dt2, 4), "ms_per_step": round(dt2 / steps2 * 1e3, 4),
                      "value_GiBps": round(world * steps2 * user_bytes_per_step / dt2 / GiB, 3)}
+    scaling = None
+    if world > 1:
+        # the same step on every rank, first each rank alone (the others wait at a
+        # barrier), then all together; >= sustained_ms per window
+        steps3 = max(args.steps, int(np.ceil(args.sustained_ms / ms_step)) if args.sustained_ms > 0 else 0)
+        solo = solo_times(rdist, lambda: w.solo_steps(steps3))
+        w.run_steps(steps3, 2, rdist.barrier)
+        conc = rdist.gather_floats(w.last_own_s)
+        scaling = {"steps": steps3, **scaling_fields(conc, solo, [steps3 * user_bytes_per_step] * world)}
     ok = rdist.all_true(w.check())
     alg = w.alg_bytes()
     w.close()
@@ -945,6 +1159,8 @@ def main():
     }
     if sustained:
         out["sustained"] = sustained
+    if scaling:
+        out["scaling_check"] = scaling
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(k, m, S, 16384, args.cpu_seconds, torch, eng)
     if not args.no_extras:
@@ -955,6 +1171,9 @@ def main():
         extras["copy_kernel_bytes_per_launch"] = alg[dom] // 2 * 2
         extras["kmsweep_64KiB_device"] = kmsweep(torch, rdist, rotate)
         extras["healer_mix_config5"] = healer_mix(torch, eng, rdist, k, m, S, 1 << 20)
+        mc = multi_ctx_leg(torch, rdist, eng, k, m)
+        if rank == 0:
+            extras["multi_ctx"] = mc
         if world == 1:
             extras["config3_patterns_and_soa_rs42_4KiB"] = layout_and_patterns(torch, eng, k, m, S, N, rotate)
             extras["scrub_verify_device"] = {"rs42_4KiB": scrub_rate(torch, eng, k, m, S, N, rotate)}

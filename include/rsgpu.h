@@ -82,6 +82,10 @@ int rs_parity_shards(const rs_ctx *ctx);
 int rs_device(const rs_ctx *ctx);               /* the first engine's ordinal */
 int rs_device_count(const rs_ctx *ctx);         /* engines in the context */
 int rs_device_at(const rs_ctx *ctx, int i);     /* ordinal of engine i (-1 if none) */
+/* Codec kernels (encode / reconstruct / verify) this context has launched on engine
+ * i since creation: which GPUs of a multi-GPU context a host batch or a coalesced
+ * burst actually used (bench.py's multi_ctx leg). */
+int rs_device_launches(const rs_ctx *ctx, int i, uint64_t *launches);
 /* Description of the backend for NewService's log line (ec.go:32-41). */
 const char *rs_backend(const rs_ctx *ctx);
 const char *rs_strerror(int code);
@@ -369,17 +373,19 @@ int rs_set_occupancy_cap(rs_ctx *ctx, int waves_per_simd);
  * 0 (the default): no byte past S of any slot is ever written. */
 int rs_set_parity_pad_writes(rs_ctx *ctx, int enable);
 /* The same for the out-of-place reconstructs (rs_reconstruct_batch_out and its
- * _devmask form), ON by default since round 5: each output row written gets its
- * padding up to the next 128-B line, bytes [S, min(pitch, round_up(S, 128))) of the
- * row at out + i*out_sp + r*pitch -- never past the row's own slot: only when that
- * line end also fits the out stripe pitch (plane-major outputs with out_sp below it
- * are written exactly) -- and the inputs' padding is read over the same range.
- * Output rows are fresh shards (the reference's Reconstruct hands back new slices);
- * a partial last line costs HBM a read-modify-write (RS(10+4) 64 KiB 2-erasure
- * 0.728 -> 0.756 of 8 TB/s, profiles/r04zj_sweep_trace.md).  Bytes [0, S) are
- * unchanged, rows a stripe does not miss are untouched.  0: no byte past S of an
- * output row is written.  (Parity padding, above, stays opt-in: parity slots are
- * the caller's stored shards.) */
+ * _devmask form), opt-in: each output row written gets its padding up to the next
+ * 128-B line, bytes [S, min(pitch, round_up(S, 128))) of the row at
+ * out + i*out_sp + r*pitch -- never past the row's own slot: only when that line end
+ * also fits the out stripe pitch (plane-major outputs with out_sp below it are
+ * written exactly) -- and the inputs' padding is read over the same range.  Enable
+ * it only when every output row owns its whole pitch (the last row of the buffer
+ * included): a partial last line costs HBM a read-modify-write (RS(10+4) 64 KiB
+ * 2-erasure 0.728 -> 0.756 of 8 TB/s, profiles/r04zj_sweep_trace.md).  Bytes [0, S)
+ * are unchanged, rows a stripe does not miss are untouched.  0 (the default): no
+ * byte past S of an output row is written, so an output buffer may end exactly at
+ * the last row's byte S.  (Round 5 shipped this ON by default; round 6 restored the
+ * exact-row default for C and Go callers.  The Python BatchEngine, whose outputs are
+ * whole-pitch tensors, and the engine's own staging slabs turn it on.) */
 int rs_set_out_pad_writes(rs_ctx *ctx, int enable);
 /* RS_MEM_HOST batches whose shards all lie in rs_host_alloc'ed memory, 16-B
  * aligned, run zero-copy by default: the kernel reads the survivors and writes the

@@ -11,7 +11,10 @@ import os
 import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "librsgpu.so")
+SHIPPED_LIB_PATH = os.path.join(PKG_DIR, "librsgpu.so")
+# RSGPU_LIB: load a measurement build by path instead (tools/ceiling_probe.sh runs the
+# compute-free RS_PATTERN_ONLY twin this way; the shipped library is never replaced)
+LIB_PATH = os.environ.get("RSGPU_LIB") or SHIPPED_LIB_PATH
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "rsgpu.h")
 
 RS_OK = 0
@@ -46,6 +49,7 @@ SIGNATURES = {
     "rs_create_devices": (_i, [_i, _i, ctypes.POINTER(_i), _i, _i, ctypes.POINTER(_vp)]),
     "rs_device_count": (_i, [_vp]),
     "rs_device_at": (_i, [_vp, _i]),
+    "rs_device_launches": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_uint64)]),
     "rs_destroy": (None, [_vp]),
     "rs_data_shards": (_i, [_vp]),
     "rs_parity_shards": (_i, [_vp]),

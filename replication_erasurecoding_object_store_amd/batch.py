@@ -49,7 +49,16 @@ def _u32p(a: np.ndarray):
 
 
 class BatchEngine(Service):
-    """Service plus the batched entry points (rs_*_batch)."""
+    """Service plus the batched entry points (rs_*_batch).
+
+    Out-of-place outputs are whole-pitch tensors ([N, rows, P] with P the shard
+    pitch; reconstruct_out derives the stripe pitch from the tensor), so every
+    output row owns its padding up to the next 128-B line: the engine turns
+    rs_set_out_pad_writes on (the C-ABI default is exact rows)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.set_out_pad_writes(True)
 
     # ---- device-resident, split layout --------------------------------------------
     def encode(self, data, parity, shard_len: int, n_stripes: int, shard_pitch: Optional[int] = None,

@@ -194,6 +194,10 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
 
 uint64_t full_mask64(int t) { return (t >= 64) ? ~0ull : ((1ull << t) - 1); }
 
+#ifndef RS_MASK_UPLOAD
+#define RS_MASK_UPLOAD 0
+#endif
+
 // ---- buffers -------------------------------------------------------------------
 // A lane serves one synchronous host call at a time.
 struct Lane {
@@ -208,6 +212,7 @@ struct Lane {
 // keeps a second caller off the slot between its upload and its launch.
 struct UploadSlot {
   PinnedBuf host;
+  void* host_dev = nullptr;  // GPU address of host (mask_mode 2)
   DevBuf dev;
   hipEvent_t done = nullptr;
   hipEvent_t copied = nullptr;  // the masks' H2D on the engine's upload stream
@@ -302,7 +307,7 @@ struct Engine {
   bool bitsliced = false;                 // generated encode XOR program matches enc
   bool host_zero_copy = true;             // pinned host batches: kernel reads/writes in place
   bool parity_pad = false;                // encode may write parity padding to the next 128-B line
-  bool out_pad = true;                    // out-of-place rows end on whole lines (rs_set_out_pad_writes)
+  bool out_pad = false;                   // out-of-place rows end on whole lines (rs_set_out_pad_writes)
   std::string name;
 
   DevBuf d_enc_plan;                      // encode plan (uniform)
@@ -333,6 +338,10 @@ struct Engine {
   // Host-mask H2D copies run here, off the caller's stream, which only waits on the
   // copy's event: the copy overlaps the kernels already queued there (round 4).
   hipStream_t upload_st = nullptr;
+  // How host masks reach a per-stripe kernel (A/B build switch RS_MASK_UPLOAD):
+  // 0 = H2D on upload_st + cross-stream event, 1 = H2D on the launch stream itself,
+  // 2 = the kernel reads the pinned slot in place (no copy).
+  int mask_mode = RS_MASK_UPLOAD;
 
   std::mutex host_mu;                     // host-resident batches: one at a time per engine
   hipStream_t pipe_st[kHostStreams] = {};
@@ -348,6 +357,7 @@ struct Engine {
   DevBuf d_bad;                           // zero-copy verify: per-stripe result before D2H
 
   std::atomic<int> inflight{0};           // calls running on this engine (dispatch)
+  std::atomic<uint64_t> launches{0};      // codec kernels launched here (rs_device_launches)
 
   // One persistent host thread per engine runs its share of a multi-GPU host batch
   // (fan_out), started on first use.
@@ -639,6 +649,7 @@ int launch(Engine* e, const rs::KernelArgs& args, int e_out, bool per_stripe, hi
   const uint32_t bpc = e->blocks_per_cu > 0 ? static_cast<uint32_t>(e->blocks_per_cu) : 0u;
   const char* name = rs::launch_apply(a, e_out, per_stripe, bpc, static_cast<uint32_t>(e->cu_count), s, e->occ_cap);
   if (!name) return RS_ERR_DEVICE;
+  e->launches.fetch_add(1, std::memory_order_relaxed);
   e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
@@ -650,6 +661,7 @@ int launch_verify_args(Engine* e, rs::KernelArgs& a, hipStream_t s) {
   const char* name =
       rs::launch_verify(a, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_DEVICE;
+  e->launches.fetch_add(1, std::memory_order_relaxed);
   e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
@@ -881,9 +893,23 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   if (!u->copied) RS_HIP(hipEventCreateWithFlags(&u->copied, hipEventDisableTiming));
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
   u->host.numa = e->numa;
+  if (e->mask_mode == 2) {
+    const void* before = u->host.p;
+    if (u->host.ensure(n * 4)) return RS_ERR_DEVICE;
+    if (u->host.p != before || !u->host_dev) {
+      void* dp = nullptr;
+      RS_HIP(hipHostGetDevicePointer(&dp, u->host.p, 0));
+      u->host_dev = dp;
+    }
+    std::memcpy(u->host.p, masks, n * 4);
+    *dev = static_cast<const uint32_t*>(u->host_dev);
+    return RS_OK;
+  }
   if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
   std::memcpy(u->host.p, masks, n * 4);
-  if (e->upload_st) {
+  if (e->mask_mode == 1) {
+    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
+  } else if (e->upload_st) {
     RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, e->upload_st));
     RS_HIP(hipEventRecord(u->copied, e->upload_st));
     RS_HIP(hipStreamWaitEvent(s, u->copied, 0));
@@ -1424,6 +1450,7 @@ int engine_apply_batch_ptrs(Engine* e, const uint64_t* shard_ptrs_dev, const uin
   const int bpc = e->blocks_per_cu > 0 ? e->blocks_per_cu : static_cast<int>(rs::default_blocks_per_cu(e->k, bound));
   const char* name = rs::launch_apply_ptrs(a, bound, static_cast<uint32_t>(bpc), static_cast<uint32_t>(e->cu_count), s);
   if (!name) return RS_ERR_NOT_SUPPORTED;
+  e->launches.fetch_add(1, std::memory_order_relaxed);
   e->shared->note(s, name);
   RS_HIP(hipGetLastError());
   return RS_OK;
@@ -1553,6 +1580,11 @@ int rs_device(const rs_ctx* c) { return c ? c->engines[0]->device : -1; }
 int rs_device_count(const rs_ctx* c) { return c ? static_cast<int>(c->engines.size()) : 0; }
 int rs_device_at(const rs_ctx* c, int i) {
   return (c && i >= 0 && i < static_cast<int>(c->engines.size())) ? c->engines[static_cast<size_t>(i)]->device : -1;
+}
+int rs_device_launches(const rs_ctx* c, int i, uint64_t* launches) {
+  if (!c || !launches || i < 0 || i >= static_cast<int>(c->engines.size())) return RS_ERR_INVALID_ARG;
+  *launches = c->engines[static_cast<size_t>(i)]->launches.load(std::memory_order_relaxed);
+  return RS_OK;
 }
 const char* rs_backend(const rs_ctx* c) { return c ? c->backend.c_str() : "none"; }
 const char* rs_last_kernel(const rs_ctx* c) { return c ? c->shared.last_kernel.load() : "none"; }

@@ -40,7 +40,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "rs_plan.hpp"
 
@@ -153,29 +156,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(uint8_t* base) {
 // (SC1 there costs 1.5-8 points).
 constexpr int kCpolNt = 2;
 constexpr int kCpolSc1 = 16;
-// (A/B overrides: RS_CPOL_E1_K8 for 1-erasure K >= 8, RS_CPOL_E2_K10 for 2-erasure
-// K >= 10, RS_CPOL_PATH2 for the E = M kernels' 2-row path.)
-#ifndef RS_CPOL_E1_K8
-#define RS_CPOL_E1_K8 kCpolSc1
-#endif
-#ifndef RS_CPOL_E2_K10
-#define RS_CPOL_E2_K10 (kCpolSc1 | kCpolNt)
-#endif
-#ifndef RS_CPOL_PATH2
-#define RS_CPOL_PATH2 kCpolNt
-#endif
+template <int K, int E>
+constexpr int out_cpol() {
+  return (E == 1 && K >= 8) ? kCpolSc1 : (E == 2 && K >= 10) ? (kCpolSc1 | kCpolNt) : kCpolNt;
+}
 // The segmented flat E = m kernel's 1-row path stores NT (round 5, same-process A/B,
 // profiles/r05h_ab_same_fp1.log, RS(10+4) 64 KiB): unbounded 1-erasure 68.4 ->
 // 71.5 %, mixed 0..4 61.7 -> 63.1 %, mixed 1..4 66.8 -> 68.4 %, others level; the
 // bounded E = 1 kernels keep SC1 (NT there: -2.9 flat, -5.1 stripe-aligned RS(8+4),
 // profiles/r05g_ab_same_cpol.log).
-#ifndef RS_CPOL_FLAT_PATH1
-#define RS_CPOL_FLAT_PATH1 kCpolNt
-#endif
-template <int K, int E>
-constexpr int out_cpol() {
-  return (E == 1 && K >= 8) ? RS_CPOL_E1_K8 : (E == 2 && K >= 10) ? RS_CPOL_E2_K10 : kCpolNt;
-}
+constexpr int kCpolFlatPath1 = kCpolNt;
 
 // Per-stripe kernels sized for E > 2 outputs (device masks without a caller bound:
 // E = M) compute only the rows a task's stripe(s) miss and then pick, in a
@@ -183,54 +173,32 @@ constexpr int out_cpol() {
 // their own policy (path_cpol below) and issue no dropped stores for the other rows,
 // more rows store E rows with out_cpol<K, E> (round 4).
 // Every store instruction has one policy for all its lanes and every 128-B output
-// line one writer instruction.  RS_WAVE_ROWS=0 builds the single-path kernels (A/B).
-#ifndef RS_WAVE_ROWS
-#define RS_WAVE_ROWS 1
-#endif
-// RS_APPLY_MIN_WAVES: launch bounds asking the compiler to fit the apply_kernel
-// instantiations with K <= 8 and E <= 2 into that many waves per SIMD (0: none).  The
-// uniform-plan RS(8+4) 2-erasure kernel then drops from 135 to 117 VGPRs (3 -> 4
-// waves, no scratch): same-process A/B (profiles/r05n_ab_lb4.log) one pattern for the
-// batch +6.0 points out of place, +3.9 in place; every other shape level.  K = 10
-// with E >= 2 would spill to scratch at 4 waves and is left alone.
-#ifndef RS_APPLY_MIN_WAVES
-#define RS_APPLY_MIN_WAVES 4
-#endif
-// RS_PS_SKIP_INTACT: per-stripe E <= 2 tasks of stripes that miss nothing skip their
-// loads and stores (1) or load and drop them (0, A/B).
-#ifndef RS_PS_SKIP_INTACT
-#define RS_PS_SKIP_INTACT 1
-#endif
-// Row paths of the E = M kernels, RS_EM_EMIT_EACH_{FLAT,APPLY}: 1 = each path computes
-// only its own rows (no row 0 ahead of the branch) and 3+ rows are stored one by one
-// as they are computed; 0 = row 0 first, then the other rows, then one store group.
-// Same-process A/B (profiles/r05i_ab_emit_each.log, 64 KiB, 4 rounds): the flat
-// RS(10+4) kernel gains 0.3-0.9 points on every E = M leg (mixed 64.8 -> 65.7 %),
-// the stripe-aligned RS(8+4) kernel loses 2.3-4.2 (its SGPRs spill: 10 -> 69).
-#ifndef RS_EM_EMIT_EACH_FLAT
-#define RS_EM_EMIT_EACH_FLAT 1
-#endif
-#ifndef RS_EM_EMIT_EACH_APPLY
-#define RS_EM_EMIT_EACH_APPLY 0
-#endif
-// Store policy of those paths (RS_WAVE_ROWS_CPOL):
-//   2 (default): the 1-row path with out_cpol<K, 1> (SC1 for K >= 8), the 2-row path
-//     NT.  Interleaved A/B against 1 (profiles/r04t_ab_p2nt.log, RS(10+4) 64 KiB,
-//     >= 100 ms per point, 3 rounds): unbounded 2-erasure 69.5 -> 70.5 % (median),
-//     mixed 0..4 erasures 59.5-59.8 -> 60.6 % (host masks 56.9-57.0 -> 57.6-57.7 %),
-//     mixed 1..4 65.3-65.8 -> 66.7-66.9 %; the bounded E = 2 kernel keeps NT|SC1.
-//   1: out_cpol<K, 1 or 2>, the bounded kernels' policies.
-//   0: out_cpol<K, E> for every path (all NT: 1-erasure 4-7 points slower,
-//     profiles/r04s_ab_em_cpol_mix.log).
-#ifndef RS_WAVE_ROWS_CPOL
-#define RS_WAVE_ROWS_CPOL 2
-#endif
+// line one writer instruction.
+// Store policy of those paths: the 1-row path with out_cpol<K, 1> (SC1 for K >= 8),
+// the 2-row path NT.  Interleaved A/B against the bounded kernels' policies
+// (profiles/r04t_ab_p2nt.log, RS(10+4) 64 KiB, >= 100 ms per point, 3 rounds):
+// unbounded 2-erasure 69.5 -> 70.5 % (median), mixed 0..4 erasures 59.5-59.8 ->
+// 60.6 % (host masks 56.9-57.0 -> 57.6-57.7 %), mixed 1..4 65.3-65.8 -> 66.7-66.9 %;
+// the bounded E = 2 kernel keeps NT|SC1.  out_cpol<K, E> on every path (all NT) was
+// 4-7 points slower on 1-erasure (profiles/r04s_ab_em_cpol_mix.log).
 template <int K, int E, int NR>
 constexpr int path_cpol() {
-  return RS_WAVE_ROWS_CPOL == 2 ? (NR == 1 ? out_cpol<K, 1>() : RS_CPOL_PATH2)
-         : RS_WAVE_ROWS_CPOL    ? out_cpol<K, NR>()
-                                : out_cpol<K, E>();
+  return NR == 1 ? out_cpol<K, 1>() : kCpolNt;
 }
+// Launch bounds asking the compiler to fit the apply_kernel instantiations with K <= 8
+// and E <= 2 into 4 waves per SIMD.  The uniform-plan RS(8+4) 2-erasure kernel then
+// drops from 135 to 117 VGPRs (3 -> 4 waves, no scratch): same-process A/B
+// (profiles/r05n_ab_lb4.log) one pattern for the batch +6.0 points out of place, +3.9
+// in place; every other shape level.  K = 10 with E >= 2 would spill to scratch at 4
+// waves and is left alone.
+constexpr int kApplyMinWaves = 4;
+#ifndef RS_EM_INOUT
+#define RS_EM_INOUT 0
+#endif
+#ifndef RS_EM_ROWB
+#define RS_EM_ROWB 0
+#endif
+constexpr bool kEmRowBarrier = RS_EM_ROWB != 0;
 
 // 16-B store at base + off, or nothing at all when !live: a raw buffer
 // store whose offset then fails the range check, so the hardware drops it -- no
@@ -323,7 +291,7 @@ __device__ __forceinline__ uint32_t pop_low(uint32_t& bits) {
 // the accumulator with one 3-input XOR.  The scheduling barrier per input stops the
 // compiler from hoisting every input's tables into SGPRs at once (K*NR*5 dwords,
 // e.g. 100 for RS(10+4) x 2 rows -> SGPR spills through VGPR lanes).
-template <int K, int M, int R0, int NR>
+template <int K, int M, int R0, int NR, bool ROW_BARRIER = false>
 __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K], u32x4 (&y)[NR]) {
   if constexpr (RS_PATTERN_ONLY) {
 #pragma unroll
@@ -362,71 +330,25 @@ __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K]
           pend[r][d] = prod;
       }
     };
+    // ROW_BARRIER: one row's lookups at a time (the scheduler would otherwise interleave
+    // every row's temporaries of this input for ILP, at the price of registers)
     row(std::integral_constant<int, 0>{});
+    if constexpr (ROW_BARRIER && NR > 1) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 1) row(std::integral_constant<int, 1>{});
+    if constexpr (ROW_BARRIER && NR > 2) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 2) row(std::integral_constant<int, 2>{});
+    if constexpr (ROW_BARRIER && NR > 3) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 3) row(std::integral_constant<int, 3>{});
     if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// The 3-chunk v_perm tables of every coefficient f, 5 dwords each (the layout of
-// perm_tables in rs_engine.cpp), built at compile time in constant memory: 5 KiB
-// that every XCD keeps cache-hot.  The E = M rows read a plan's coefficient bytes
-// (its first 128 B, with the header) and fetch each coefficient's tables here
-// instead of from the plan's own 800-B table block (RS_EM_COEF, below).
-struct GfPermTabs {
-  uint32_t v[256 * 5];
-};
-constexpr uint8_t gf_mul_ct(uint8_t a, uint8_t b) {
-  uint8_t r = 0;
-  for (int i = 0; i < 8; ++i) {
-    if (b & 1u) r = static_cast<uint8_t>(r ^ a);
-    const bool hi = (a & 0x80u) != 0u;
-    a = static_cast<uint8_t>(a << 1);
-    if (hi) a = static_cast<uint8_t>(a ^ 0x1Du);  // x^8 = x^4 + x^3 + x^2 + 1 (0x11d)
-    b = static_cast<uint8_t>(b >> 1);
-  }
-  return r;
-}
-constexpr GfPermTabs make_gf_perm_tabs() {
-  GfPermTabs t{};
-  for (int f = 0; f < 256; ++f)
-    for (int j = 0; j < 4; ++j) {
-      const uint8_t ff = static_cast<uint8_t>(f);
-      t.v[f * 5 + 0] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j))) << (8 * j);
-      t.v[f * 5 + 1] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(4 + j))) << (8 * j);
-      t.v[f * 5 + 2] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j << 3))) << (8 * j);
-      t.v[f * 5 + 3] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>((4 + j) << 3))) << (8 * j);
-      t.v[f * 5 + 4] |= static_cast<uint32_t>(gf_mul_ct(ff, static_cast<uint8_t>(j << 6))) << (8 * j);
-    }
-  return t;
-}
-__constant__ GfPermTabs kGfPermTabs = make_gf_perm_tabs();
-
-// RS_EM_COEF (A/B): 1 = gf_row_ix takes each coefficient's tables from kGfPermTabs
-// through the plan's coefficient bytes; 0 (default) = from the plan's table block.
-// A mixed RS(10+4) batch touches all 1 470 plans, and every XCD's L2 fetches each
-// plan's 896-B table block once per launch: ~10 MB, about 1 % of the launch's bytes
-// (the mixed legs' HBM/alg 1.031 against 1.017 for one pattern per stripe).  Fewer
-// bytes, but one more dependent scalar round trip per row: same-process A/B
-// (profiles/r05j_ab_coef.log) -0.8 to -1.7 points on every E = M leg but one.
-#ifndef RS_EM_COEF
-#define RS_EM_COEF 0
-#endif
-
-// One row r of a task from the inputs' precomputed chunk indices ix[c][d].
-// RS_ROWIX_GROUP (A/B): inputs whose table dwords share one opaque base, i.e. are
-// fetched by the scalar unit together and waited for once (scalar loads return out
-// of order, so every wait is lgkmcnt(0)).  RS_ROWIX_TABONLY (diagnostic only, wrong
-// bytes): the tables are fetched as usual but folded with one XOR instead of three
-// lookups, which separates the cost of the fetches from that of the arithmetic.
-#ifndef RS_ROWIX_GROUP
-#define RS_ROWIX_GROUP 1
-#endif
-#ifndef RS_ROWIX_TABONLY
-#define RS_ROWIX_TABONLY 0
-#endif
+// One row r of a task from the inputs' precomputed chunk indices ix[c][d].  Each
+// input's table dwords hang off their own opaque base, so the scalar unit fetches
+// them per input and they are never all held in SGPRs at once.  (Rejected, measured:
+// coefficient-indexed tables from a 5-KiB compile-time table instead of the plan's
+// table block, -0.8 to -1.7 points, profiles/r05j_ab_coef.log; several inputs per
+// fetch group.)
 template <int K, int M>
 __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)[K][4], int r) {
   u32x4 y{0u, 0u, 0u, 0u}, pend{0u, 0u, 0u, 0u};
@@ -437,33 +359,16 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
       for (int d = 0; d < 4; ++d) y[d] ^= ix[c][d].a + static_cast<uint32_t>(r);
     return y;
   }
-  const uint8_t* tg = plan;
-  const uint32_t* gt = kGfPermTabs.v;
-  constexpr int kWords = (K + 3) / 4;
-  uint32_t cw[kWords];
-  if constexpr (RS_EM_COEF) {
-    const RS_CONST uint32_t* cwp = PlanView(plan, K, M).coef_words(r);
-#pragma unroll
-    for (int i = 0; i < kWords; ++i) cw[i] = cwp[i];
-  }
 #pragma unroll
   for (int c = 0; c < K; ++c) {
-    if (c % RS_ROWIX_GROUP == 0) {
-      tg = plan;
-      asm volatile("" : "+s"(tg));  // one opaque base per group: tables never all in SGPRs
-      if constexpr (RS_EM_COEF) {
-        gt = kGfPermTabs.v;
-        asm volatile("" : "+s"(gt));
-      }
-    }
+    const uint8_t* tg = plan;
+    asm volatile("" : "+s"(tg));  // one opaque base per input: tables never all in SGPRs
     const PlanView pc(tg, K, M);
-    const RS_CONST uint32_t* tb =
-        RS_EM_COEF ? as_const<uint32_t>(gt + ((cw[c >> 2] >> (8 * (c & 3))) & 0xFFu) * 5u) : pc.quad(r, c);
+    const RS_CONST uint32_t* tb = pc.quad(r, c);
     const uint32_t q0 = tb[0], q1 = tb[1], q2 = tb[2], q3 = tb[3], q4 = tb[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const uint32_t prod = RS_ROWIX_TABONLY ? xor3(ix[c][d].a, q0 ^ q1 ^ q2, q3 ^ q4)
-                                             : lookup3(ix[c][d], q0, q1, q2, q3, q4);
+      const uint32_t prod = lookup3(ix[c][d], q0, q1, q2, q3, q4);
       if (c & 1)
         y[d] = xor3(y[d], pend[d], prod);
       else if (c == K - 1)
@@ -471,7 +376,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
       else
         pend[d] = prod;
     }
-    if (c + 1 < K && (c + 1) % RS_ROWIX_GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
   }
   return y;
 }
@@ -496,7 +401,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // work and in how many stores end the trip, so the compiler's vmcnt bookkeeping
 // stays exact (a branch around the loads does not: DESIGN.md Appendix A.5).
 template <int K, int M, int E, bool PER_STRIPE>
-__global__ __launch_bounds__(256, (RS_APPLY_MIN_WAVES && K <= 8 && E <= 2) ? RS_APPLY_MIN_WAVES : 1) void apply_kernel(
+__global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void apply_kernel(
     const KernelArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = wave_index();
@@ -616,7 +521,7 @@ __global__ __launch_bounds__(256, (RS_APPLY_MIN_WAVES && K <= 8 && E <= 2) ? RS_
       // intact (or skipped) stripe ends its wave here: no loads, no stores.  RS(4+2)
       // device masks without a bound are this kernel (E = M = 2), and a scan's mixed
       // batch had every intact stripe read for nothing.
-      if constexpr (PER_STRIPE && RS_PS_SKIP_INTACT) {
+      if constexpr (PER_STRIPE) {
         if (!work) continue;
       }
 #pragma unroll
@@ -642,7 +547,28 @@ __global__ __launch_bounds__(256, (RS_APPLY_MIN_WAVES && K <= 8 && E <= 2) ? RS_
       }
     };
     u32x4 y[E];
-    if constexpr (PER_STRIPE && E > 2) {
+    if constexpr (PER_STRIPE && E > 2 && RS_EM_INOUT >= 2) {
+      // input-outer by the stripe's row count (A/B), as in apply_flat_seg_kernel
+      const uint32_t nrow = pv.n_out();
+      if (nrow <= 1u) {
+        u32x4 yy[1];
+        gf_rows<K, M, 0, 1>(plan, x, yy);
+        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, yy);
+      } else if (nrow == 2u) {
+        u32x4 yy[2];
+        gf_rows<K, M, 0, 2>(plan, x, yy);
+        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, yy);
+      } else if (E == 3 || nrow == 3u) {
+        u32x4 yy[3];
+        gf_rows<K, M, 0, 3>(plan, x, yy);
+        emit(std::integral_constant<int, 3>{}, std::integral_constant<int, out_cpol<K, E>()>{}, yy);
+      } else {
+        u32x4 yy[E > 3 ? 4 : 3];
+        gf_rows<K, M, 0, (E > 3 ? 4 : 3)>(plan, x, yy);
+        emit(std::integral_constant<int, (E > 3 ? 4 : 3)>{}, std::integral_constant<int, out_cpol<K, E>()>{}, yy);
+      }
+      continue;
+    } else if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
       // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
       // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
@@ -655,39 +581,16 @@ __global__ __launch_bounds__(256, (RS_APPLY_MIN_WAVES && K <= 8 && E <= 2) ? RS_
       for (int c = 0; c < K; ++c)
 #pragma unroll
         for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+      // (Storing each of 3+ rows as soon as it is computed, as the flat kernel does,
+      // lost 2.3-4.2 points here: SGPRs spill, profiles/r05i_ab_emit_each.log.)
       const uint32_t nrow = pv.n_out();
-      if constexpr (RS_EM_EMIT_EACH_APPLY && RS_WAVE_ROWS) {
-        // each path computes only its rows; 3+ rows are stored one by one as computed
-        if (nrow <= 1u) {
-          y[0] = gf_row_ix<K, M>(plan, ix, 0);
-          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
-        } else if (nrow == 2u) {
-          y[0] = gf_row_ix<K, M>(plan, ix, 0);
-          y[1] = gf_row_ix<K, M>(plan, ix, 1);
-          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-        } else {
-          constexpr int CPOL = out_cpol<K, E>();
-          const bool last = nb != 0u && blk + 1u == bps;  // wave-uniform
-          const bool part = col == a.full_cols;
-#pragma unroll
-          for (int r = 0; r < E; ++r) {
-            if (static_cast<uint32_t>(r) < nrow) {
-              const u32x4 yr = gf_row_ix<K, M>(plan, ix, r);
-              uint8_t* ob = out_ptr(a, K, stripe, r, pv.out_idx(r));
-              store16_or_drop<CPOL>(ob, off, full, yr);
-              if (last) store_part_or_drop<CPOL>(ob, off, part, yr, nb);
-            }
-          }
-        }
-        continue;
-      }
       y[0] = gf_row_ix<K, M>(plan, ix, 0);
 #pragma unroll
       for (int r = 1; r < E; ++r) {
         y[r] = y[0];  // dropped unless computed
         if (static_cast<uint32_t>(r) < nrow) y[r] = gf_row_ix<K, M>(plan, ix, r);
       }
-      if (RS_WAVE_ROWS && n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
+      if (n_out <= 2u) {  // wave-uniform: the bounded kernels' store policy
         if (n_out <= 1u)
           emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, y);
         else
@@ -845,44 +748,8 @@ __device__ __forceinline__ void transpose8(uint32_t (&d)[8]) {
   swap(6, 7, 1, 0x55555555u);
 }
 
-// Inputs stream through a window of kBsWindow loads in flight: input c+W is
-// loaded once input c has been transposed, so only W inputs' raw bytes are live
-// (registers for more waves) while W 2 KiB loads per wave stay in flight.
-#ifndef RS_BS_WINDOW
-#define RS_BS_WINDOW 5
-#endif
-#ifndef RS_BS_OCC
-#define RS_BS_OCC 3
-#endif
-constexpr int kBsWindow = RS_BS_WINDOW;  // profiles/r01_ab_bs_window_occupancy.log
-
-// Programs shared over groups of 4 inputs (RS(10+4) 682 -> 573 XORs, RS(8+4) 564 ->
-// 473) were measured level on RS(8+4) and 2.5-3 points slower on RS(10+4)
-// (round 4, profiles/r04r_ab_bitsliced_groups.log): the per-input programs stay.
-template <int K, int M, int C>
-__device__ __forceinline__ void bs_fold(__amdgpu_buffer_rsrc_t din, uint32_t pitch, uint32_t off_a, uint32_t off_b,
-                                        u32x4 (&xa)[kBsWindow], u32x4 (&xb)[kBsWindow], uint32_t (&y)[8 * M]) {
-  if constexpr (C < K) {
-    constexpr int slot = C % kBsWindow;
-    uint32_t d[8] = {xa[slot][0], xa[slot][1], xa[slot][2], xa[slot][3],
-                     xb[slot][0], xb[slot][1], xb[slot][2], xb[slot][3]};
-    if constexpr (C + kBsWindow < K) {
-      xa[slot] = bload16(din, off_a, (C + kBsWindow) * pitch);
-      xb[slot] = bload16(din, off_b, (C + kBsWindow) * pitch);
-    }
-    if constexpr (RS_PATTERN_ONLY) {
-#pragma unroll
-      for (int i = 0; i < 8 * M; ++i) y[i] = (C == 0 ? 0u : y[i]) ^ d[i & 7];
-    } else {
-      transpose8(d);
-      bs_step<K, M, C>(d, y);
-    }
-    bs_fold<K, M, C + 1>(din, pitch, off_a, off_b, xa, xb, y);
-  }
-}
-
 // One lane-column of a flat task: global column g = (stripe s0, column c0 + i) of the
-// batch's N x cols columns, i < 128 <= cols, so the column lies in stripe s0 or s0+1.
+// batch's N x cols columns, i < 64 <= cols, so the column lies in stripe s0 or s0+1.
 struct FlatCol {
   uint32_t col;   // column within its stripe
   uint32_t doff;  // byte offset from the task's data stripe base (next stripe: + data_sp)
@@ -905,91 +772,13 @@ __device__ __forceinline__ FlatCol flat_col(const KernelArgs& a, uint32_t s0, ui
   return f;
 }
 
-// Task = 128 consecutive columns of the batch's flat column space (stripe-major,
-// ceil(S/16) columns per stripe rounded up to whole 128-B lines): lane l owns
-// columns l and l+64 of the task, 16 B of every shard each.  A task may straddle two stripes (one encode plan for all),
-// so no lane idles at a stripe's ragged end: RS(10+4) at 64 KiB objects (410
-// columns) runs 3.2 tasks per stripe instead of 4 (20 % of the VALU work and of
-// the memory instructions); the line rounding keeps a straddling access split at a
-// line boundary (measured: S = 6656 flat 72.5-73.5 % vs stripe-aligned 67-70.5 %,
-// while unaligned splits at S = 6554 cost 1-2 points, profiles/r02c_flat_encode.log).
-// Addresses: one buffer descriptor per region off the
-// task's first stripe, a per-lane 32-bit offset (next stripe: + its pitch) and the
-// slot as the scalar offset (c * pitch).  Host preconditions (launch_window):
-// cols >= 128, data_sp / parity_sp + 16 * cols < 2^31, (k+m) * pitch < 2^32.
-// Full columns store 16 B; the lane holding a stripe's partial last column stores
-// it byte-exact in a wave-uniform branch taken by tasks that contain one.
-template <int K, int M>
-__global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const KernelArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = wave_index();
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  const uint32_t cols = (a.shard_len + 15u) >> 4;
-  const uint32_t nb = a.shard_len & 15u;  // bytes of a partial last column (0: none)
-  // flat column space: each stripe rounded up to whole 128-B lines, so a task's
-  // stripe boundary -- where its 1 KiB wave accesses split in two -- is line-aligned
-  const uint32_t cstride = (cols + 7u) & ~7u;
-  const uint64_t total = static_cast<uint64_t>(a.n_stripes) * cstride;
-  if (static_cast<uint64_t>(wave) * 128u >= total) return;
-  const uint32_t pitch = static_cast<uint32_t>(a.shard_pitch);
-  // cursor (s0, c0) = divmod(t * 128, cols), advanced by divmod(nwaves * 128, cols)
-  const uint64_t g0 = static_cast<uint64_t>(wave) * 128u;
-  uint32_t s0 = wave_uniform(static_cast<uint32_t>(g0 / cstride));
-  uint32_t c0 = static_cast<uint32_t>(g0 - static_cast<uint64_t>(s0) * cstride);
-  const uint64_t gstep = static_cast<uint64_t>(nwaves) * 128u;
-  const uint32_t step_s = wave_uniform(static_cast<uint32_t>(gstep / cstride));
-  const uint32_t step_c = static_cast<uint32_t>(gstep - static_cast<uint64_t>(step_s) * cstride);
-  while (s0 < a.n_stripes) {
-    const FlatCol fa = flat_col(a, s0, c0 + lane, cstride, cols);
-    const FlatCol fb = flat_col(a, s0, c0 + 64u + lane, cstride, cols);
-    const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
-                                                       0x7FFFFFFF, 0x00020000);
-    const auto pout = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
-                                                        0x7FFFFFFF, 0x00020000);
-    u32x4 xa[kBsWindow], xb[kBsWindow];
-#pragma unroll
-    for (int c = 0; c < kBsWindow && c < K; ++c) {
-      xa[c] = bload16(din, fa.doff, c * pitch);
-      xb[c] = bload16(din, fb.doff, c * pitch);
-    }
-    uint32_t y[8 * M];
-    bs_fold<K, M, 0>(din, pitch, fa.doff, fb.doff, xa, xb, y);
-    const bool sa = fa.live && fa.col < a.full_cols, sb = fb.live && fb.col < a.full_cols;
-    const bool pa = nb != 0u && fa.live && fa.col == a.full_cols;  // this lane holds a partial column
-    const bool pb = nb != 0u && fb.live && fb.col == a.full_cols;
-    u32x4 part[M];
-#pragma unroll
-    for (int r = 0; r < M; ++r) {
-      uint32_t d[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d[i] = y[r * 8 + i];
-      if constexpr (!RS_PATTERN_ONLY) transpose8(d);
-      const u32x4 lo{d[0], d[1], d[2], d[3]}, hi{d[4], d[5], d[6], d[7]};
-      __builtin_amdgcn_raw_buffer_store_b128(lo, pout, sa ? fa.poff : kDropOffset, r * pitch, 2 /* nt */);
-      __builtin_amdgcn_raw_buffer_store_b128(hi, pout, sb ? fb.poff : kDropOffset, r * pitch, 2 /* nt */);
-      part[r] = pb ? hi : lo;
-    }
-    if (nb != 0u && __builtin_amdgcn_ballot_w64(pa || pb) != 0u) {  // wave-uniform
-      const uint32_t off = pb ? fb.poff : fa.poff;
-#pragma unroll
-      for (int r = 0; r < M; ++r) store_part_rsrc(pout, off, r * pitch, pa || pb, part[r], nb);
-    }
-    c0 += step_c;
-    s0 += step_s;
-    if (c0 >= cstride) {
-      c0 -= cstride;
-      ++s0;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Bitsliced encode over 1 KiB-wide tasks (64 columns, 16 B of every shard per lane).
 //
-// Bitslicing needs 32 B per lane to fill 8 plane dwords; the 2 KiB rows of
-// encode_bitsliced_kernel give each lane two columns, and that task shape streams
-// about 3 points below 1 KiB rows at RS(8+4) (compute-free probe).  Here a
-// lane fills its planes from two INPUTS instead: 16 B of input c (even) in dwords
+// Bitslicing needs 32 B per lane to fill 8 plane dwords; round 1-3's 2 KiB-row kernel
+// gave each lane two columns, and that task shape streams about 3 points below 1 KiB
+// rows at RS(8+4) (compute-free probe).  Here a lane fills its planes from two INPUTS
+// instead: 16 B of input c (even) in dwords
 // 0-3 and of input c ^ 1 in dwords 4-7, so after transpose8 plane j holds bit j of
 // input c in the low nibble of each byte and of input c ^ 1 in the high nibble.
 // The RS(8+4) and RS(10+4) encode matrices satisfy C[r ^ 1][c] = C[r][c ^ 1], so for
@@ -1000,13 +789,18 @@ __global__ __launch_bounds__(256, RS_BS_OCC) void encode_bitsliced_kernel(const 
 // rows r and r ^ 1 (dwords 0-3 and 4-7).  XORs per 32 B of every shard: RS(8+4) 532
 // (pair programs share the A / B terms) vs 564; the transposes: K / 2 + M / 2 per 16 B,
 // the same count per byte as the 2 KiB kernel, plus 4 VALU ops per packed plane.
-// Same flat column space, straddling and tail handling as encode_bitsliced_kernel.
+// Flat column space: the batch's columns, each stripe rounded up to whole 128-B lines
+// (a straddling wave access then splits at a line boundary), cut into 64-column tasks
+// that may straddle two stripes, so no lane idles at a stripe's ragged end (RS(10+4)
+// at 64 KiB objects: 6.5 tasks per stripe instead of 7).  Addresses: one buffer
+// descriptor per region off the task's first stripe, a per-lane 32-bit offset (next
+// stripe: + its pitch) and the slot as the scalar offset.  Host preconditions
+// (launch_window): cols >= 128, data_sp / parity_sp + 16 * cols < 2^31.
+// Full columns store 16 B; the lane holding a stripe's partial last column stores it
+// byte-exact in a wave-uniform branch taken by tasks that contain one.
 // Interleaved A/B against the 2 KiB kernel (round 4, profiles/r04zb_ab_bs16.log, 64 KiB
 // objects, >= 100 ms per point, 3 rounds): RS(8+4) 69.4-70.4 -> 72.0-73.1 % of 8 TB/s,
 // RS(10+4) 66.6-67.6 -> 67.5-68.2 %; a window of 3 pairs and 8 workgroups per CU level.
-#ifndef RS_BS16
-#define RS_BS16 2
-#endif
 #ifndef RS_BS16_WINDOW
 #define RS_BS16_WINDOW 5
 #endif
@@ -1125,30 +919,18 @@ __global__ __launch_bounds__(256, RS_BS16_OCC) void encode_bs16_kernel(const Ker
 // caller's max_missing for device masks.  E <= 2 runs input-outer with x[K] as the
 // only per-input state; E > 2 splits every input into chunk indices once and then
 // computes only the rows the stripe misses, one at a time.
-// RS_FLAT_EM_FULL: the E > 2 flat launches take one task per wave (a full grid) like
-// the E <= 2 ones, instead of a grid-stride loop over default_blocks_per_cu.
-#ifndef RS_FLAT_EM_FULL
-#define RS_FLAT_EM_FULL 1
-#endif
+// The E > 2 flat launches take one task per wave (a full grid) like the E <= 2 ones,
+// instead of a grid-stride loop over default_blocks_per_cu.
 // Out-of-place per-stripe launches whose shard length is a whole number of 64-column
 // tasks (no task then straddles) take the flat kernel too for RS(10+4) with a bound
 // of 2 or more: same-process A/B at 80 KiB objects (profiles/r05k_ab_flatal.log, S =
 // 8 192, 4 rounds) bounded 2-erasure 68.0 -> 76.4 %, unbounded 2-erasure +0.8, mixed
 // 70.0 -> 73.0 %; 1-erasure -0.3, and every other shape loses (RS(8+4) 2-erasure
 // -1.9 / -5.5, RS(4+2) -4.9 to -7.2, RS(6+3) -1.0) except RS(8+4) mixed (+1.7).
-// RS_FLAT_ALIGNED=1 routes every shape with a flat kernel there (A/B).
-#ifndef RS_FLAT_ALIGNED
-#define RS_FLAT_ALIGNED 0
-#endif
-// RS_FLAT_UNIFORM (A/B, off): out-of-place reconstructs with one erasure pattern for
-// the batch take the flat kernel with that one plan for every stripe wherever the
-// per-stripe form would.  The stripe-aligned uniform kernel, whose slots are resolved
-// once per launch, stays ahead (profiles/r05m_ab_uniform.log: RS(10+4) 2-erasure at
-// 64 / 80 KiB objects -3.5 / -3.8 points through the flat kernel).
-#ifndef RS_FLAT_UNIFORM
-#define RS_FLAT_UNIFORM 0
-#endif
-
+// (Rejected: one-pattern out-of-place reconstructs through this kernel with one plan
+// for every stripe; the stripe-aligned uniform kernel, whose slots are resolved once
+// per launch, stays ahead, profiles/r05m_ab_uniform.log: RS(10+4) 2-erasure at 64 /
+// 80 KiB objects -3.5 / -3.8 points through the flat kernel.)
 
 template <int K, int M, int E>
 __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a) {
@@ -1259,7 +1041,27 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         u32x4 y[E];
         gf_rows<K, M, 0, E>(plan, x, y);
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-      } else if constexpr (RS_EM_EMIT_EACH_FLAT && RS_WAVE_ROWS) {
+      } else if constexpr (RS_EM_INOUT >= 1) {
+        // input-outer by the stripe's row count (A/B): x[K] and NR accumulators live,
+        // every input split once and folded into each of its NR rows as it arrives
+        if (nout <= 1u) {
+          u32x4 y[1];
+          gf_rows<K, M, 0, 1, kEmRowBarrier>(plan, x, y);
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, kCpolFlatPath1>{}, y);
+        } else if (nout == 2u) {
+          u32x4 y[2];
+          gf_rows<K, M, 0, 2, kEmRowBarrier>(plan, x, y);
+          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
+        } else if (E == 3 || nout == 3u) {
+          u32x4 y[3];
+          gf_rows<K, M, 0, 3, kEmRowBarrier>(plan, x, y);
+          emit(std::integral_constant<int, 3>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+        } else {
+          u32x4 y[E > 3 ? 4 : 3];
+          gf_rows<K, M, 0, (E > 3 ? 4 : 3), kEmRowBarrier>(plan, x, y);
+          emit(std::integral_constant<int, (E > 3 ? 4 : 3)>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+        }
+      } else {
         // each row path computes only its rows; stripes missing 3+ shards store each
         // row as soon as it is computed (one row's accumulators live instead of E)
         Idx3 ix[K][4];
@@ -1270,7 +1072,7 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         if (nout <= 1u) {
           u32x4 y[1];
           y[0] = gf_row_ix<K, M>(plan, ix, 0);
-          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, RS_CPOL_FLAT_PATH1>{}, y);
+          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, kCpolFlatPath1>{}, y);
         } else if (nout == 2u) {
           u32x4 y[2];
           y[0] = gf_row_ix<K, M>(plan, ix, 0);
@@ -1288,27 +1090,6 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
             }
           }
         }
-      } else {
-        u32x4 y[E];
-        {
-          Idx3 ix[K][4];
-#pragma unroll
-          for (int c = 0; c < K; ++c)
-#pragma unroll
-            for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
-          y[0] = gf_row_ix<K, M>(plan, ix, 0);
-#pragma unroll
-          for (int r = 1; r < E; ++r) {
-            y[r] = y[0];  // dropped unless computed
-            if (static_cast<uint32_t>(r) < nout) y[r] = gf_row_ix<K, M>(plan, ix, r);
-          }
-        }
-        if (RS_WAVE_ROWS && nout <= 1u)  // wave-uniform: the bounded kernels' store policy
-          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, RS_CPOL_FLAT_PATH1>{}, y);
-        else if (RS_WAVE_ROWS && nout == 2u)
-          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-        else
-          emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
       }
     }
     c0 += step_c;  // grid stride in the flat column space
@@ -1493,7 +1274,7 @@ __global__ __launch_bounds__(256) void verify_kernel(const KernelArgs a) {
 }
 
 // The same check over flat 64-column tasks (each stripe rounded up to whole 128-B
-// lines, a task may straddle two stripes; see encode_bitsliced_kernel): RS(10+4)
+// lines, a task may straddle two stripes; see encode_bs16_kernel): RS(10+4)
 // at 64 KiB objects runs 6.5 tasks per stripe instead of 7 stripe-aligned ones.
 // Host preconditions as for the flat encode (cols >= 64 here).
 template <int K, int M>
@@ -1668,12 +1449,6 @@ static const void* pick_spec(int k, int m, int e, bool per_stripe, const char** 
   return nullptr;
 }
 
-template <int K, int M>
-static const void* bitsliced_fn() {
-  if constexpr (BsNet<K, M>::kAvailable) return reinterpret_cast<const void*>(&encode_bitsliced_kernel<K, M>);
-  return nullptr;
-}
-
 const uint8_t* bitsliced_encode_rows(int k, int m) {
 #define RS_BS(KK, MM) \
   if (k == KK && m == MM) return BsNet<KK, MM>::kRows;
@@ -1688,31 +1463,21 @@ static const void* bs16_fn() {
   return nullptr;
 }
 
-// Bitsliced encode kernel of (k, m) and its task width in columns (128: 2 KiB rows,
-// 64: the 1 KiB-task pair kernel).  RS_BS16: 0 = 2 KiB kernel only, 1 = pair kernel
-// for RS(8+4), 2 (default) = pair kernel for RS(8+4) and RS(10+4).
+// Bitsliced encode kernel of (k, m) (the 1 KiB-task pair kernel, 64-column tasks).
+// (4,2) and (6,3) are memory-bound on the lookup kernel already, and the bitsliced
+// one was slower / level there (profiles/r01_ab_bitsliced*.log).
 static const void* pick_bitsliced(int k, int m, const char** name, uint32_t* task_cols) {
-  *task_cols = 128u;
+  *task_cols = 64u;
 #define RS_BS16K(KK, MM)                                          \
   if (k == KK && m == MM) {                                       \
     if (const void* f = bs16_fn<KK, MM>()) {                      \
       *name = "encode_bs16_kernel<" #KK "," #MM ">";              \
-      *task_cols = 64u;                                           \
       return f;                                                   \
     }                                                             \
   }
-  if (RS_BS16 >= 1) RS_BS16K(8, 4)
-  if (RS_BS16 >= 2) RS_BS16K(10, 4)
+  RS_BS16K(8, 4)
+  RS_BS16K(10, 4)
 #undef RS_BS16K
-#define RS_BS(KK, MM)                                   \
-  if (k == KK && m == MM) {                             \
-    *name = "encode_bitsliced_kernel<" #KK "," #MM ">"; \
-    return bitsliced_fn<KK, MM>();                      \
-  }
-  // (4,2) and (6,3) are memory-bound on the lookup kernel already, and the
-  // bitsliced one was slower / level there (profiles/r01_ab_bitsliced*.log)
-  RS_BS(8, 4) RS_BS(10, 4)
-#undef RS_BS
   return nullptr;
 }
 
@@ -1803,26 +1568,48 @@ static dim3 full_grid(uint64_t waves) {
 // points at 4 waves, 4 KiB objects +1.3 at 5 (-1.0 at 4); 2-erasure +0.8 to +1.1 at
 // 4 for 16 KiB and more, 4 KiB objects (the headline) -1.7 at 4 and level at 5-6;
 // RS(8+4) 64 KiB 1-erasure +0.6, 2-erasure level.  Encodes and uniform reconstructs
-// stay uncapped (4 waves: -1.4 to -5.3).  RS_OCC_CAP_PS_AUTO=0: uncapped (A/B).
-#ifndef RS_OCC_CAP_PS_AUTO
-#define RS_OCC_CAP_PS_AUTO 1
-#endif
+// stay uncapped (4 waves: -1.4 to -5.3).
 constexpr size_t kLdsPerCu = 160u * 1024u;
+
+// Raises fn's dynamic-LDS limit on the current device to the whole 160 KiB, once per
+// (kernel, device): caps of 1 or 2 workgroups per CU reserve more than the default
+// 64 KiB (the attribute used to be set on every such launch).  false
+// if the runtime refuses, and the launch then fails instead of running uncapped
+// under a label it did not get.
+static bool raise_lds_limit(const void* fn) {
+  static std::mutex mu;
+  static std::vector<std::pair<const void*, int>> done;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::lock_guard<std::mutex> g(mu);
+  for (const auto& d : done)
+    if (d.first == fn && d.second == dev) return true;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsPerCu)) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  done.emplace_back(fn, dev);
+  return true;
+}
 
 // Dynamic LDS bytes that cap `fn` at `cap` workgroups per CU (0: none): halfway
 // between 160 KiB / (cap + 1) and 160 KiB / cap, so allocation granularity and any
 // static LDS cannot turn c into c - 1 (160 KiB / cap exactly admitted one fewer:
-// profiles/r05c_ab_same_occ.log, caps 3 / 5 / 6 ran as 2 / 4 / 5).
+// profiles/r05c_ab_same_occ.log, caps 3 / 5 / 6 ran as 2 / 4 / 5).  kLdsRefused when
+// the kernel's LDS limit cannot be raised for the cap.
+constexpr size_t kLdsRefused = ~size_t(0);
 static size_t occ_lds(const void* fn, uint32_t cap) {
   if (cap == 0) return 0;
   const size_t lds = ((kLdsPerCu / cap + kLdsPerCu / (cap + 1)) / 2) & ~size_t(1023);
-  if (lds > 65536) {  // above the default dynamic-LDS limit: raise it for this kernel
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds)) != hipSuccess) {
-      (void)hipGetLastError();
-      return 0;
-    }
-  }
+  if (lds > 65536 && !raise_lds_limit(fn)) return kLdsRefused;  // above the default dynamic-LDS limit
   return lds;
+}
+
+// hipLaunchKernel with an occupancy reservation; false if it cannot be honoured.
+static bool launch_capped(const void* fn, dim3 grid, void** args, size_t lds, hipStream_t s) {
+  if (lds == kLdsRefused) return false;
+  return hipLaunchKernel(fn, grid, dim3(256), args, lds, s) == hipSuccess;
 }
 
 // One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
@@ -1850,12 +1637,11 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
       // against a grid-stride loop over 6 workgroups per CU)
       const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
-      if (hipLaunchKernel(fn, grid, dim3(256), args, occ_lds(fn, cap_of(RS_OCC_CAP_BS)), s) != hipSuccess) return nullptr;
+      if (!launch_capped(fn, grid, args, occ_lds(fn, cap_of(RS_OCC_CAP_BS)), s)) return nullptr;
       return name;
     }
   }
-  if ((per_stripe || (RS_FLAT_UNIFORM && !a.data_inputs)) && !generic && a.out && cols >= 64u &&
-      (cols % 64u != 0u || RS_FLAT_ALIGNED || (a.k == 10 && e >= 2)) &&
+  if (per_stripe && !generic && a.out && cols >= 64u && (cols % 64u != 0u || (a.k == 10 && e >= 2)) &&
       a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
@@ -1866,10 +1652,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 2-erasure; E = M since round 5's segmented kernel: unbounded 2-erasure and
       // mixed batches +3.5 / +3.9 points, r05b_ab_same_flat.log, r05e_ab_same_em.log)
       const uint32_t bpc = blocks_per_cu ? blocks_per_cu : default_blocks_per_cu(a.k, e);
-      const dim3 grid = (!blocks_per_cu && (e <= 2 || RS_FLAT_EM_FULL)) ? full_grid(waves)
+      const dim3 grid = !blocks_per_cu ? full_grid(waves)
                                                                          : grid_for(waves, bpc, cu_count);
       const uint32_t cap = e == 1 ? RS_OCC_CAP_FLAT_E1 : e == 2 ? RS_OCC_CAP_FLAT_E2 : RS_OCC_CAP_FLAT_EM;
-      if (hipLaunchKernel(ff, grid, dim3(256), args, occ_lds(ff, cap_of(cap)), s) != hipSuccess) return nullptr;
+      if (!launch_capped(ff, grid, args, occ_lds(ff, cap_of(cap)), s)) return nullptr;
       return name;
     }
   }
@@ -1895,10 +1681,9 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
     grid = full_grid(waves);
   }
   uint32_t dcap = RS_OCC_CAP_APPLY;
-  if (RS_OCC_CAP_PS_AUTO && dcap == 0u && per_stripe && !generic && e <= 2)
+  if (dcap == 0u && per_stripe && !generic && e <= 2)
     dcap = a.blocks_per_stripe >= 2u ? 4u : (e == 1 ? 5u : 0u);
-  if (hipLaunchKernel(fn, grid, dim3(256), args, generic ? 0 : occ_lds(fn, cap_of(dcap)), s) != hipSuccess)
-    return nullptr;
+  if (!launch_capped(fn, grid, args, generic ? 0 : occ_lds(fn, cap_of(dcap)), s)) return nullptr;
   return name;
 }
 

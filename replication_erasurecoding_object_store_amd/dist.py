@@ -8,7 +8,7 @@ elapsed times, and the AND of per-rank parity checks.
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import List, Tuple
 
 
 def world() -> Tuple[int, int, int]:
@@ -25,11 +25,18 @@ def init(backend: str = "nccl") -> None:
     if ws <= 1 or dist.is_initialized():
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    rdzv = os.environ.get("RSGPU_RDZV_FILE")
+    if rdzv:
+        # bench.py's own launcher: a file store in a fresh directory, so no TCP port is
+        # picked by one process and bound by another later (a port
+        # freed by the launcher could be taken before rank 0 bound it)
+        kw = {"init_method": "file://" + rdzv, "rank": rank, "world_size": ws}
     if backend == "nccl":
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), **kw)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, **kw)
 
 
 def stripe_range(n_stripes: int, rank: int, world_size: int) -> Tuple[int, int]:
@@ -73,6 +80,20 @@ def all_true(flag: bool) -> bool:
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=_device())
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
+
+
+def gather_floats(x: float) -> List[float]:
+    """Every rank's value of x, in rank order (on every rank)."""
+    import torch
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return [x]
+    ws = dist.get_world_size()
+    t = torch.tensor([x], dtype=torch.float64, device=_device())
+    out = [torch.zeros_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
 
 
 def distinct_count(key: int) -> int:

@@ -118,6 +118,16 @@ class Service:
         L = _lib.lib()
         return [L.rs_device_at(self._ctx, i) for i in range(L.rs_device_count(self._ctx))]
 
+    def device_launches(self) -> List[int]:
+        """Codec kernels launched on each engine since creation (rs_device_launches)."""
+        L = _lib.lib()
+        out = []
+        for i in range(L.rs_device_count(self._ctx)):
+            v = ctypes.c_uint64()
+            _check(L.rs_device_launches(self._ctx, i, ctypes.byref(v)))
+            out.append(v.value)
+        return out
+
     def encode_matrix(self) -> List[List[int]]:
         t = self.k + self.m
         out = (ctypes.c_uint8 * (t * self.k))()

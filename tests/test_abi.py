@@ -29,7 +29,7 @@ def test_header_declares_expected_surface():
 
 def test_library_exports_every_header_symbol():
     L = _lib.lib()
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.SHIPPED_LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     exported = set(re.findall(r" T (rs_\w+)", out))
     for f in header_functions():
@@ -39,9 +39,9 @@ def test_library_exports_every_header_symbol():
 
 
 def test_library_is_gfx950_code():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", _lib.LIB_PATH], capture_output=True,
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", _lib.SHIPPED_LIB_PATH], capture_output=True,
                          text=True)
-    blob = open(_lib.LIB_PATH, "rb").read()
+    blob = open(_lib.SHIPPED_LIB_PATH, "rb").read()
     assert b"gfx950" in blob
 
 
@@ -125,9 +125,9 @@ def test_product_never_imports_the_oracle():
             if fn.endswith((".cpp", ".hip", ".hpp", ".h")):
                 src = open(path).read()
                 assert "rs_oracle" not in src and "rso_" not in src, path
-    out = subprocess.run(["nm", "-D", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    out = subprocess.run(["nm", "-D", _lib.SHIPPED_LIB_PATH], capture_output=True, text=True, check=True).stdout
     assert "rso_" not in out
-    ldd = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    ldd = subprocess.run(["ldd", _lib.SHIPPED_LIB_PATH], capture_output=True, text=True).stdout
     assert "rs_oracle" not in ldd
 
 
@@ -156,6 +156,6 @@ def test_no_gpu_mapping_of_caller_memory():
             code = re.sub(r"//[^\n]*|/\*.*?\*/", "", src, flags=re.S)  # comments may name them
             assert "hipHostRegister(" not in code, fn
             assert "getenv(" not in code, fn
-    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.SHIPPED_LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     assert "hipHostRegister" not in out and "getenv" not in out

@@ -1,7 +1,8 @@
 """bench.py's rank launcher on CPU: `--gpus N` with no torchrun environment starts N
 fresh ranks itself (the driver may call `python3 bench.py --gpus 8` directly), a
 WORLD_SIZE that disagrees with --gpus fails loudly, and a failing rank fails the run.
---dry-run keeps every rank off the GPU (gloo control collectives only)."""
+--dry-run keeps every rank off the GPU (gloo control collectives only) and runs the
+per-GPU efficiency arithmetic of the N-rank line on synthetic per-rank times."""
 import json
 import os
 import subprocess
@@ -35,6 +36,12 @@ def test_gpus_flag_spawns_ranks(n):
     assert line["n_gpus"] == n
     assert line["pids_distinct"] == n  # n separate processes
     assert line["ranks_ok"] is True
+    # the per-GPU efficiency fields (solo_times + scaling_fields, the same code the GPU
+    # run uses), on synthetic per-rank times: alone 20 ms each, together 20 ms x (1 + r/10)
+    sc = line["scaling_check"]
+    assert len(sc["per_rank_GiBps"]) == n and len(sc["solo_GiBps"]) == n
+    assert sc["solo_GiBps"] == [round((1 << 20) / 0.02 / (1 << 30), 2)] * n
+    assert sc["per_gpu_efficiency"] == pytest.approx(1 / (1 + (n - 1) / 10), abs=2e-4)
 
 
 @pytest.mark.timeout(60)
@@ -58,3 +65,25 @@ def test_failing_rank_fails_the_run():
     r = _run(["--gpus", "2", "--dry-run"], _env(RSGPU_BENCH_DRY_FAIL_RANK="1"))
     assert r.returncode == 3, (r.returncode, r.stderr)
     assert "rank 1 exited with 3" in r.stderr
+
+
+def test_cpu_baseline_threads_follow_the_cgroup_quota(tmp_path):
+    """cpu_baseline's core count: the cgroup CPU quota (v2 cpu.max
+    or v1 cfs quota / period), capped by the affinity mask; no quota -> the mask."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    affinity = len(os.sched_getaffinity(0))
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert bench.cpu_quota(str(tmp_path)) == (affinity, None, "no cgroup CPU quota: every CPU in the affinity mask")
+    (tmp_path / "cpu.max").write_text("200000 100000\n")
+    th, q, src = bench.cpu_quota(str(tmp_path))
+    assert (th, q) == (min(2, affinity), 2.0) and "cpu.max" in src
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("150000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    th, q, src = bench.cpu_quota(str(v1))
+    assert (th, q) == (1, 1.5) and "cfs_quota_us" in src
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert bench.cpu_quota(str(v1))[:2] == (affinity, None)

@@ -11,7 +11,7 @@ caller's bound, and scrub.  Bytes [0, S) of every shard written equal the oracle
 (oracle/rs_oracle.c, pinned on klauspost's KATs in tests/test_oracle.py), and every
 byte the contract does not let the call write keeps its sentinel: slot padding,
 stripe gaps, present shards, unused output rows, output padding past the 128-B line
-(rs_set_out_pad_writes, on by default, and its guard against the next stripe).
+(rs_set_out_pad_writes, which BatchEngine turns on, and its guard against the next stripe).
 Reference semantics: internal/ec/ec.go:54-61 (Encode / Reconstruct), klauspost
 v1.12.1 reedsolomon.go (first-K survivors, every missing shard filled, Verify).
 """

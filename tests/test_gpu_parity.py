@@ -38,7 +38,7 @@ def eng_for(engines, k, m):
 
 def _pad_end(S, P):
     """First byte of an out-of-place row that is never written: rows end on whole
-    128-B lines within their slot (rs_set_out_pad_writes, on by default)."""
+    128-B lines within their slot (rs_set_out_pad_writes, on in BatchEngine)."""
     return min(P, (S + 127) // 128 * 128)
 
 

@@ -64,7 +64,7 @@ def _codewords(eng, k, m, S, N, seed):
 
 def _pad_end(S, P):
     """First byte of an out-of-place row that is never written: rows end on whole
-    128-B lines within their slot (rs_set_out_pad_writes, on by default)."""
+    128-B lines within their slot (rs_set_out_pad_writes, on in BatchEngine)."""
     return min(P, (S + 127) // 128 * 128)
 
 
@@ -244,7 +244,7 @@ def test_out_pad_writes(engines, k, m, S, bound):
     rows = bound or m
     out = torch.full((N, rows, P), 0xC3, dtype=torch.uint8, device="cuda")
     mdev = torch.from_numpy(masks.view(np.int32)).cuda()
-    eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=bound, shard_pitch=P)  # default: on
+    eng.reconstruct_out(data, parity, out, S, N, masks_dev=mdev, max_missing=bound, shard_pitch=P)  # BatchEngine: on
     eng.sync()
     got = out.cpu().numpy()
     line_end = min(P, (S + 127) // 128 * 128)
@@ -274,7 +274,7 @@ def test_out_pad_writes(engines, k, m, S, bound):
 def test_out_pad_never_crosses_a_stripe_slot(engines, k, m, S):
     """Dense 1-row outputs (bound 1, out stripe pitch = round_up(S, 16), below the
     128-B line end): whole-line rows would overwrite the next stripe's row, so the
-    engine writes them exactly (the guard in launch()) -- with the default on."""
+    engine writes them exactly (the guard in launch()) -- with BatchEngine's padding on."""
     import torch
 
     eng = _engine(engines, k, m)
@@ -298,6 +298,55 @@ def test_out_pad_never_crosses_a_stripe_slot(engines, k, m, S):
         j = [s for s in range(t) if not (masks[i] >> s) & 1][0]
         assert np.array_equal(got[i, :S], full[i, j]), (i, j)
     assert (got[:N, S:] == 0xC3).all(), "a row's padding reached into the next stripe's row"
+
+
+@pytest.mark.parametrize("k,m,S,bound", [(10, 4, 6554, 2), (10, 4, 6554, 0), (4, 2, 1000, 2), (8, 4, 8200, 1)])
+def test_c_abi_default_rows_end_at_byte_s(k, m, S, bound):
+    """a C / Go caller gets exact rows by default.  A context made
+    through the plain C-ABI (no BatchEngine opt-in) writes no byte past S of any
+    output row, so an output buffer that ends exactly at the last row's byte S --
+    (N-1)*out_sp + (e-1)*pitch + S -- is enough: the bytes after it keep their
+    sentinel, and every row equals the erased shard."""
+    import ctypes
+
+    import torch
+
+    from replication_erasurecoding_object_store_amd.ec import Service
+
+    svc = Service(k, m, 0)  # rs_create: the library's defaults
+    try:
+        t, N = k + m, 257
+        P = shard_pitch_for(S)
+        e = bound or m
+        g = torch.Generator(device="cuda").manual_seed(S + 11)
+        data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+        parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+        L = _lib.lib()
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        assert L.rs_encode_batch(svc.ctx, data.data_ptr(), k * P, parity.data_ptr(), m * P, P, S, N,
+                                 _lib.RS_MEM_DEVICE, st) == 0
+        full = torch.cat([data, parity], dim=1)[:, :, :S].cpu().numpy()
+        rng = np.random.default_rng(S + bound)
+        masks = _masks(rng, N, t, e, e)  # every stripe misses e shards: the last row is row e-1
+        out_sp = e * P
+        need = (N - 1) * out_sp + (e - 1) * P + S
+        guard = 4096
+        buf = torch.full((need + guard,), 0xC3, dtype=torch.uint8, device="cuda")
+        mdev = torch.from_numpy(masks.view(np.int32)).cuda()
+        assert L.rs_reconstruct_batch_out_devmask(svc.ctx, data.data_ptr(), k * P, parity.data_ptr(), m * P, P, S,
+                                                  N, mdev.data_ptr(), bound, buf.data_ptr(), out_sp, st) == 0
+        assert L.rs_sync(svc.ctx, st) == 0
+        got = buf.cpu().numpy()
+        assert (got[need:] == 0xC3).all(), "a byte past the last row's byte S was written"
+        for i in range(N):
+            missing = [j for j in range(t) if not (masks[i] >> j) & 1]
+            for r, j in enumerate(missing):
+                o = i * out_sp + r * P
+                assert np.array_equal(got[o:o + S], full[i, j]), (i, r, j)
+                if o + S < need:
+                    assert (got[o + S:min(o + P, need)] == 0xC3).all(), ("row padding written", i, r)
+    finally:
+        svc.close()
     assert (got[N] == 0xC3).all()
 
 

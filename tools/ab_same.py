@@ -43,9 +43,10 @@ SIGS = {
 
 
 class Variant:
-    def __init__(self, name, path, occ_cap=None):
+    def __init__(self, name, path, occ_cap=None, env=None):
         self.name = name
         self.occ_cap = occ_cap
+        self.env = env or {}  # set around this variant's rs_create (engine-creation knobs)
         self.lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
         for fn, (res, args) in SIGS.items():
             f = getattr(self.lib, fn)
@@ -55,7 +56,16 @@ class Variant:
     def ctx_for(self, k, m):
         if (k, m) not in self.ctx:
             c = _vp()
-            rc = self.lib.rs_create(k, m, 0, 0, ctypes.byref(c))
+            saved = {key: os.environ.get(key) for key in self.env}
+            os.environ.update(self.env)
+            try:
+                rc = self.lib.rs_create(k, m, 0, 0, ctypes.byref(c))
+            finally:
+                for key, v in saved.items():
+                    if v is None:
+                        os.environ.pop(key, None)
+                    else:
+                        os.environ[key] = v
             assert rc == 0, f"{self.name}: rs_create {rc}"
             if self.occ_cap is not None:
                 assert self.lib.rs_set_occupancy_cap(c, self.occ_cap) == 0
@@ -80,9 +90,14 @@ def main():
     GiB = 1 << 30
     names = args.variants.split(",")
     # "name@c": abx/name.so with rs_set_occupancy_cap(c) (e.g. a compute-free twin at the
-    # occupancy its real kernel's registers allow)
-    vs = [Variant(n, os.path.join(ROOT, "abx", n.split("@")[0] + ".so"),
-                  int(n.split("@")[1]) if "@" in n else None) for n in names]
+    # occupancy its real kernel's registers allow); "shipped": the in-tree library
+    def variant(n):
+        lib, _, cap = n.partition("@")
+        path = (os.path.join(ROOT, "replication_erasurecoding_object_store_amd", "librsgpu.so") if lib == "shipped"
+                else os.path.join(ROOT, "abx", lib + ".so"))
+        return Variant(n, path, int(cap) if cap else None)
+
+    vs = [variant(n) for n in names]
     print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
     for wl in args.workloads.split(","):
         k, m, S, N, mode = WORKLOADS[wl]
