@@ -234,7 +234,8 @@ class RSWorkload:
     reconstruct 2 erased shards per stripe (seeded per-stripe pattern, device masks)
     out of place -- the reference's semantics (Reconstruct gives missing entries NEW
     slices; the healer writes back only those), include/rsgpu.h's
-    rs_reconstruct_batch_out."""
+    rs_reconstruct_batch_out.  Calls with a caller-known erasure bound b write b
+    rows per stripe, back to back; calls without one, m-row slots."""
 
     def __init__(self, torch, eng, k, m, S, N, rotate_bytes, seed):
         from replication_erasurecoding_object_store_amd.batch import shard_pitch_for
@@ -248,6 +249,10 @@ class RSWorkload:
         # device masks: the engine cannot bound #missing on the host, so outputs
         # have room for m per stripe; the first 2 are written here
         self.outs = [torch.empty((N, m, self.P), dtype=torch.uint8, device="cuda") for _ in range(self.nb)]
+        # a caller that bounds the erasures at b (max_missing) gives each stripe b
+        # output rows, back to back (the healer writes back just those,
+        # poller.go:288-302): dense out stripe pitch b * P (for b = m the slots above)
+        self.outs_b = {m: self.outs}
         rng = np.random.default_rng(0x5EED0003)
         self.masks = [torch.from_numpy(two_erasure_masks(rng, N, t).view(np.int32)).cuda() for _ in range(self.nb)]
         for d, p in self.bufs:  # every batch a codeword before timing
@@ -258,13 +263,24 @@ class RSWorkload:
         d, p = self.bufs[i % self.nb]
         self.eng.encode(d, p, self.S, self.N)
 
-    def rec(self, i, bound=0):
+    def out_for(self, i, bound, dense=True):
+        """Output slots of rotation i for a call bounded at `bound` erasures (0 = m):
+        `bound` rows per stripe back to back, or (dense=False) the m-row slots."""
+        b = bound or self.m
+        if not dense:
+            return self.outs[i % self.nb]
+        if b not in self.outs_b:
+            self.outs_b[b] = [self.torch.empty((self.N, b, self.P), dtype=self.torch.uint8, device="cuda")
+                              for _ in range(self.nb)]
+        return self.outs_b[b][i % self.nb]
+
+    def rec(self, i, bound=0, dense=True):
         """bound: the caller's erasure bound (max_missing; 0 = m)."""
         d, p = self.bufs[i % self.nb]
-        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks[i % self.nb],
-                                 max_missing=bound)
+        self.eng.reconstruct_out(d, p, self.out_for(i, bound, dense), self.S, self.N,
+                                 masks_dev=self.masks[i % self.nb], max_missing=bound)
 
-    def rec1(self, i, bound=0):
+    def rec1(self, i, bound=0, dense=True):
         """1 erased shard per stripe (seeded uniform index, device masks)."""
         if not hasattr(self, "masks1"):
             rng = np.random.default_rng(0x5EED0003 + 1)
@@ -272,8 +288,8 @@ class RSWorkload:
             self.masks1 = [self.torch.from_numpy((full & ~(1 << rng.integers(0, self.k + self.m, self.N)))
                                                  .astype(np.uint32).view(np.int32)).cuda() for _ in range(self.nb)]
         d, p = self.bufs[i % self.nb]
-        self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N, masks_dev=self.masks1[i % self.nb],
-                                 max_missing=bound)
+        self.eng.reconstruct_out(d, p, self.out_for(i, bound, dense), self.S, self.N,
+                                 masks_dev=self.masks1[i % self.nb], max_missing=bound)
 
     def rec_mix(self, i, host=False):
         """0..m erased shards per stripe (seeded, uniform count), no caller bound: a
@@ -378,7 +394,7 @@ class RSWorkload:
         return ok
 
     def close(self):
-        del self.bufs, self.outs, self.masks
+        del self.bufs, self.outs, self.outs_b, self.masks
         self.torch.cuda.empty_cache()
 
 
@@ -826,6 +842,11 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             e2.set_parity_pad_writes(False)
         timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"], solo=True)
         timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+        if mm > 2:
+            # round 5's layout for the same calls: the bounded rows in m-row slots
+            # (rows 1..m-1 of every stripe's slot unused)
+            timed("reconstruct2_mslot_out", lambda i: w.rec(i, bound=2, dense=False), alg["reconstruct"])
+            timed("reconstruct1_mslot_out", lambda i: w.rec1(i, bound=1, dense=False), alg["reconstruct1"])
         if SS % 128:
             # output rows end on whole 128-B lines by default (round 5); the same legs
             # with exact rows (rs_set_out_pad_writes(0): nothing past S written)

@@ -22,6 +22,7 @@ import (
 	"runtime"
 	"sync"
 	"sync/atomic"
+	"time"
 	"unsafe"
 
 	"github.com/klauspost/reedsolomon"
@@ -45,6 +46,13 @@ import (
 // the staged outputs into the callers' slices -- so several reapers share that copy
 // work) and wake their goroutines.  A blocking cgo call would instead hold an OS
 // thread per in-flight request and pay a futex sleep and wake-up per object.
+//
+// Hybrid dispatch (round 6): a call runs on klauspost on its own goroutine instead
+// of the GPU when the object is smaller than gpuMinObject bytes (its staging costs
+// more CPU than encoding it), when gpuMaxInflight calls are already on the GPU (the
+// PCIe link is the limit there, and the CPU codec adds its own throughput), and when
+// the coalescer has no free staging batch (RS_ERR_BUSY) -- a call never waits for
+// the GPU.  Thresholds: tools/run_hybrid.sh, DESIGN.md §6.
 type Service struct {
 	ctx *C.rs_ctx
 	co  *C.rs_coalescer
@@ -55,14 +63,10 @@ type Service struct {
 	nextTag uint64
 	waiting map[uint64]chan int // result codes (Go ints: the tests cannot name cgo types)
 
-	// back-pressure: a submit that finds no free staging batch (RS_ERR_BUSY) waits
-	// for the next reaper round instead of spinning.  Every round bumps epoch and
-	// wakes the waiters, timeouts included: batches also come free without a reap
-	// (rs_co_reconstruct_many's synchronous calls), so a waiter retries at least
-	// every reapTimeoutUs.
-	freeMu   sync.Mutex
-	freeCond *sync.Cond
-	epoch    uint64 // reaper rounds so far (freeMu)
+	inflight   atomic.Int64 // calls submitted to the GPU and not yet completed
+	maxInfl    int64        // gpuMaxInflight (tests may lower it)
+	minGPUData int          // gpuMinObject (tests may change it)
+	reaping    atomic.Int32 // reaper goroutines still in their loop
 
 	// broken: a reaper failed; the calls it left waiting got its error and every
 	// later call runs on klauspost (enc).  Set before waiting is flushed (mu).
@@ -71,17 +75,41 @@ type Service struct {
 	reapers sync.WaitGroup
 }
 
-// errGPUUnavailable: the call was not submitted (the engine is broken); the caller
-// runs it on the CPU codec instead.
+// Hybrid dispatch thresholds, measured on MI355X with a 16-CPU quota
+// (profiles/r06*_hybrid.log, tools/run_hybrid.sh): objects of at least gpuMinObject
+// bytes go to the GPU while fewer than gpuMaxInflight calls are in flight there.
+const (
+	gpuMinObject   = 16 << 10
+	gpuMaxInflight = 64
+)
+
+// errGPUUnavailable: the call was not submitted (the engine is broken, or busy:
+// RS_ERR_BUSY); the caller runs it on the CPU codec instead.
 var errGPUUnavailable = errors.New("EC Driver: GPU engine unavailable")
 
 // reapTimeoutUs bounds one rs_co_reap wait so a reaper notices Close.
 const reapTimeoutUs = 100000
 
-// call runs one asynchronous coalescer call: submit(tag) stages it; the result
-// arrives from a reaper.  The caller keeps its shard buffers pinned until then.
-// errGPUUnavailable means nothing was submitted: run the call on the CPU.
+// useGPU reserves a GPU slot for a call on an object of dataBytes user bytes, or
+// says the call runs on the CPU (hybrid dispatch).  A reserved slot is released by
+// call() when the call completes or is not submitted.
+func (s *Service) useGPU(dataBytes int) bool {
+	if !s.gpu || s.broken.Load() || dataBytes < s.minGPUData {
+		return false
+	}
+	if s.inflight.Add(1) > s.maxInfl {
+		s.inflight.Add(-1)
+		return false
+	}
+	return true
+}
+
+// call runs one asynchronous coalescer call in the GPU slot useGPU reserved:
+// submit(tag) stages it; the result arrives from a reaper.  The caller keeps its
+// shard buffers pinned until then.  errGPUUnavailable means nothing was submitted
+// (engine broken, or no free staging batch): run the call on the CPU.
 func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
+	defer s.inflight.Add(-1)
 	ch := make(chan int, 1) // buffered: a reaper never blocks on a send
 	s.mu.Lock()
 	if s.broken.Load() {
@@ -92,36 +120,17 @@ func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
 	tag := s.nextTag
 	s.waiting[tag] = ch
 	s.mu.Unlock()
-	forget := func() {
-		s.mu.Lock()
-		delete(s.waiting, tag)
-		s.mu.Unlock()
+	rc := submit(C.uint64_t(tag))
+	if rc == C.RS_OK {
+		return toErr(C.int(<-ch)) // a reaper's result, or the error of a reaper that failed
 	}
-	for {
-		s.freeMu.Lock()
-		seen := s.epoch
-		s.freeMu.Unlock()
-		rc := submit(C.uint64_t(tag))
-		if rc == C.RS_OK {
-			return toErr(C.int(<-ch)) // a reaper's result, or the error of a reaper that failed
-		}
-		if rc != C.RS_ERR_BUSY || s.closing.Load() { // rejected: never reaped
-			forget()
-			return toErr(rc)
-		}
-		// no staging batch is free: batches still executing, or finished ones whose
-		// calls are not reaped yet -- sleep until the next reaper round, then submit
-		// again
-		s.freeMu.Lock()
-		for s.epoch == seen && !s.closing.Load() && !s.broken.Load() {
-			s.freeCond.Wait()
-		}
-		s.freeMu.Unlock()
-		if s.broken.Load() {
-			forget()
-			return errGPUUnavailable
-		}
+	s.mu.Lock()
+	delete(s.waiting, tag) // rejected or busy: never reaped
+	s.mu.Unlock()
+	if rc == C.RS_ERR_BUSY && !s.closing.Load() {
+		return errGPUUnavailable // every staging batch executing or unreaped: the CPU takes it
 	}
+	return toErr(rc)
 }
 
 // reap delivers finished calls to their goroutines; several run per Service.
@@ -130,12 +139,13 @@ func (s *Service) call(submit func(tag C.uint64_t) C.int) error {
 // and switches the Service to the CPU codec (fail, never hang a caller).
 func (s *Service) reap() {
 	defer s.reapers.Done()
+	defer s.reaping.Add(-1)
 	const max = 256
 	tags := (*[max]C.uint64_t)(C.malloc(max * C.size_t(unsafe.Sizeof(C.uint64_t(0)))))
 	rcs := (*[max]C.int)(C.malloc(max * C.size_t(unsafe.Sizeof(C.int(0)))))
 	defer C.free(unsafe.Pointer(tags))
 	defer C.free(unsafe.Pointer(rcs))
-	for !s.closing.Load() {
+	for !s.closing.Load() && !s.broken.Load() {
 		n := int(C.rs_co_reap(s.co, &tags[0], &rcs[0], max, reapTimeoutUs))
 		if n < 0 {
 			s.fail(-n)
@@ -150,30 +160,28 @@ func (s *Service) reap() {
 				ch <- int(rcs[i])
 			}
 		}
-		s.tick()
 	}
 }
 
-// tick ends a reaper round: BUSY submitters wake and try again.
-func (s *Service) tick() {
-	s.freeMu.Lock()
-	s.epoch++
-	s.freeCond.Broadcast()
-	s.freeMu.Unlock()
-}
-
 // fail completes every waiting call with rc and sends later calls to the CPU codec.
+// The other reapers stop first (they leave their loop once broken is set, within
+// one reapTimeoutUs), so no reap copies outputs into a failed caller's buffers after
+// it has returned and unpinned them (ADVICE round 5).  Calls whose shards lie in an
+// Arena may still be written by a kernel already queued: their buffers must not be
+// reused before Close, which drains the coalescer.
 func (s *Service) fail(rc int) {
 	log.Printf("EC Driver: rs_co_reap failed: %v; failing %d waiting calls, using klauspost/reedsolomon on the CPU from now on",
 		toErr(C.int(rc)), s.pending())
 	s.broken.Store(true) // before the flush: no call registers after it
+	for s.reaping.Load() > 1 { // the other reapers leave their loop within reapTimeoutUs
+		time.Sleep(time.Millisecond)
+	}
 	s.mu.Lock()
 	for tag, ch := range s.waiting {
 		ch <- rc
 		delete(s.waiting, tag)
 	}
 	s.mu.Unlock()
-	s.tick()
 }
 
 func (s *Service) pending() int {
@@ -189,12 +197,25 @@ func (s *Service) Close() {
 	if !s.gpu || s.closing.Swap(true) {
 		return
 	}
-	s.freeMu.Lock()
-	s.freeCond.Broadcast()
-	s.freeMu.Unlock()
 	s.reapers.Wait()
 	C.rs_coalescer_destroy(s.co)
 	C.rs_destroy(s.ctx)
+}
+
+// gpuLaunches: codec kernels the engine has launched on all its GPUs so far
+// (rs_device_launches; the routing tests read it).
+func (s *Service) gpuLaunches() uint64 {
+	if !s.gpu {
+		return 0
+	}
+	var total uint64
+	for i := 0; i < int(C.rs_device_count(s.ctx)); i++ {
+		var n C.uint64_t
+		if C.rs_device_launches(s.ctx, C.int(i), &n) == C.RS_OK {
+			total += uint64(n)
+		}
+	}
+	return total
 }
 
 // Keep klauspost's exported sentinels so errors.Is and %v output match ec.go.
@@ -247,11 +268,12 @@ func NewService() interfaces.IEcDriver {
 		log.Fatalf("Failed to create Reed-Solomon batch coalescer: %v", toErr(rc))
 	}
 	log.Printf("EC Driver loaded (k=%d, m=%d) on %s\n", config.K, config.M, C.GoString(C.rs_backend(ctx)))
-	s := &Service{ctx: ctx, co: co, enc: enc, gpu: true, waiting: make(map[uint64]chan int)}
-	s.freeCond = sync.NewCond(&s.freeMu)
+	s := &Service{ctx: ctx, co: co, enc: enc, gpu: true, waiting: make(map[uint64]chan int),
+		maxInfl: gpuMaxInflight, minGPUData: gpuMinObject}
 	// reapers share rs_co_reap's output copies: one per 4 Ps, 1..8
 	n := min(max(runtime.GOMAXPROCS(0)/4, 1), 8)
 	s.reapers.Add(n)
+	s.reaping.Store(int32(n))
 	for i := 0; i < n; i++ {
 		go s.reap()
 	}
@@ -284,11 +306,8 @@ func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, fu
 
 // Encode fills shards[K:] in place (ec.go:54-56).
 func (s *Service) Encode(shards [][]byte) error {
-	if !s.gpu || s.broken.Load() {
-		return s.enc.Encode(shards)
-	}
-	if len(shards) != config.K+config.M {
-		return reedsolomon.ErrTooFewShards
+	if len(shards) != config.K+config.M || !s.useGPU(config.K*len(shards[0])) {
+		return s.enc.Encode(shards) // klauspost's own checks and sentinels on the CPU path
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin() // after the call completed: the engine writes parity until then
@@ -304,11 +323,8 @@ func (s *Service) Encode(shards [][]byte) error {
 // Reconstruct fills every empty entry, data and parity (ec.go:59-61;
 // readservice.go:285 and poller.go:282 rely on all nil entries being filled).
 func (s *Service) Reconstruct(shards [][]byte) error {
-	if !s.gpu || s.broken.Load() {
+	if !s.gpu || s.broken.Load() || len(shards) != config.K+config.M {
 		return s.enc.Reconstruct(shards)
-	}
-	if len(shards) != config.K+config.M {
-		return reedsolomon.ErrTooFewShards
 	}
 	size := 0
 	for _, sh := range shards {
@@ -317,8 +333,8 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 			break
 		}
 	}
-	if size == 0 {
-		return reedsolomon.ErrShardNoData
+	if size == 0 || config.K*size < s.minGPUData {
+		return s.enc.Reconstruct(shards) // ErrShardNoData, or an object the CPU takes
 	}
 	missing := 0
 	for i := range shards {
@@ -336,6 +352,9 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 			}
 		}
 		return nil
+	}
+	if !s.useGPU(config.K * size) {
+		return s.enc.Reconstruct(shards) // the GPU has enough in flight: this goroutine computes it
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()

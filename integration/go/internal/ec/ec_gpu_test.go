@@ -9,6 +9,7 @@ package ec
 import (
 	"bytes"
 	"crypto/sha256"
+	"errors"
 	"math/rand"
 	"runtime"
 	"testing"
@@ -236,16 +237,106 @@ func TestArenaInPlaceMatchesKlauspost(t *testing.T) {
 	}
 }
 
-// A healer's ReconstructMany can hold every staging batch with synchronous calls,
-// which free their batches without a reap.  Encode goroutines that got RS_ERR_BUSY
-// meanwhile must still finish: every reaper round (timeouts included) wakes them
-// (ADVICE round 4).  A hang shows up as the test's own deadline.
-func TestBusySubmittersWakeWithoutReaps(t *testing.T) {
+// Hybrid dispatch (VERDICT round 5 item 4): objects below the size threshold, calls
+// beyond the GPU's in-flight limit and calls that find no free staging batch run on
+// klauspost on the caller's goroutine; the rest on the GPU.  Every route gives
+// klauspost's bytes, and the engine's launch counter shows which route ran.
+func TestHybridRouting(t *testing.T) {
 	svc, ok := NewService().(*Service)
 	if !ok || !svc.gpu {
 		t.Skip("needs the GPU engine")
 	}
 	defer svc.Close()
+	ref, _ := reedsolomon.New(config.K, config.M)
+	rng := rand.New(rand.NewSource(11))
+	roundTrip := func(n int) {
+		data := make([]byte, n)
+		rng.Read(data)
+		want, _ := ref.Split(append([]byte(nil), data...))
+		_ = ref.Encode(want)
+		got, _ := svc.Split(append([]byte(nil), data...))
+		if err := svc.Encode(got); err != nil {
+			t.Fatal(err)
+		}
+		got[0], got[config.K] = nil, nil
+		if err := svc.Reconstruct(got); err != nil {
+			t.Fatal(err)
+		}
+		for i := range want {
+			if !bytes.Equal(got[i], want[i]) {
+				t.Fatalf("len %d shard %d differs from klauspost", n, i)
+			}
+		}
+	}
+	// below the size threshold: the CPU, no kernel
+	before := svc.gpuLaunches()
+	roundTrip(gpuMinObject / 2)
+	if svc.gpuLaunches() != before {
+		t.Fatal("an object below gpuMinObject reached the GPU")
+	}
+	// at or above it: the GPU
+	roundTrip(gpuMinObject * 4)
+	if svc.gpuLaunches() == before {
+		t.Fatal("a large object did not reach the GPU")
+	}
+	// the GPU's in-flight limit reached: the CPU
+	svc.maxInfl = 0
+	before = svc.gpuLaunches()
+	roundTrip(gpuMinObject * 4)
+	if svc.gpuLaunches() != before {
+		t.Fatal("a call beyond gpuMaxInflight reached the GPU")
+	}
+	if svc.inflight.Load() != 0 {
+		t.Fatalf("in-flight count leaked: %d", svc.inflight.Load())
+	}
+	svc.maxInfl = gpuMaxInflight
+	// many concurrent callers with a small limit: some calls on each side, every one
+	// right, and the in-flight count back at zero
+	svc.maxInfl = 2
+	done := make(chan error, 64)
+	for g := 0; g < 64; g++ {
+		go func(g int) {
+			for j := 0; j < 50; j++ {
+				data := make([]byte, gpuMinObject*2)
+				data[0], data[1] = byte(g), byte(j)
+				want, _ := ref.Split(append([]byte(nil), data...))
+				_ = ref.Encode(want)
+				got, _ := svc.Split(append([]byte(nil), data...))
+				if err := svc.Encode(got); err != nil {
+					done <- err
+					return
+				}
+				for i := range want {
+					if !bytes.Equal(got[i], want[i]) {
+						done <- errors.New("concurrent hybrid encode differs from klauspost")
+						return
+					}
+				}
+			}
+			done <- nil
+		}(g)
+	}
+	for g := 0; g < 64; g++ {
+		if err := <-done; err != nil {
+			t.Fatal(err)
+		}
+	}
+	if svc.inflight.Load() != 0 {
+		t.Fatalf("in-flight count leaked: %d", svc.inflight.Load())
+	}
+}
+
+// Encode goroutines that find no free staging batch (RS_ERR_BUSY) while
+// ReconstructMany's synchronous calls hold the batches run on the CPU instead of
+// waiting (round 6; round 5 parked them until a reaper round): every call finishes,
+// with klauspost's bytes.  A hang shows up as the test's own deadline.
+func TestBusySubmittersRunOnCPU(t *testing.T) {
+	svc, ok := NewService().(*Service)
+	if !ok || !svc.gpu {
+		t.Skip("needs the GPU engine")
+	}
+	defer svc.Close()
+	svc.minGPUData = 0 // 4 KiB objects on the GPU too, so the batches fill up
 	rng := rand.New(rand.NewSource(7))
 	objects := make([][][]byte, 4096)
 	for i := range objects {
@@ -258,16 +349,26 @@ func TestBusySubmittersWakeWithoutReaps(t *testing.T) {
 		sh[i%6] = nil
 		objects[i] = sh
 	}
+	ref, _ := reedsolomon.New(config.K, config.M)
 	done := make(chan error, 64)
 	for g := 0; g < 64; g++ {
 		go func(g int) {
 			for j := 0; j < 200; j++ {
 				data := make([]byte, 4096)
 				data[0] = byte(g)
+				data[1] = byte(j)
 				sh, _ := svc.Split(data)
 				if err := svc.Encode(sh); err != nil {
 					done <- err
 					return
+				}
+				want, _ := ref.Split(append([]byte(nil), data...))
+				_ = ref.Encode(want)
+				for i := range want {
+					if !bytes.Equal(sh[i], want[i]) {
+						done <- errors.New("encode differs from klauspost")
+						return
+					}
 				}
 			}
 			done <- nil

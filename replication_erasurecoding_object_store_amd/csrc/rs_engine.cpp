@@ -194,10 +194,6 @@ int make_decode_plan(int k, int m, const Matrix& enc, uint64_t present, bool dat
 
 uint64_t full_mask64(int t) { return (t >= 64) ? ~0ull : ((1ull << t) - 1); }
 
-#ifndef RS_MASK_UPLOAD
-#define RS_MASK_UPLOAD 0
-#endif
-
 // ---- buffers -------------------------------------------------------------------
 // A lane serves one synchronous host call at a time.
 struct Lane {
@@ -212,10 +208,9 @@ struct Lane {
 // keeps a second caller off the slot between its upload and its launch.
 struct UploadSlot {
   PinnedBuf host;
-  void* host_dev = nullptr;  // GPU address of host (mask_mode 2)
+  void* host_dev = nullptr;  // GPU address of host (a portable mapping)
   DevBuf dev;
   hipEvent_t done = nullptr;
-  hipEvent_t copied = nullptr;  // the masks' H2D on the engine's upload stream
   bool used = false;
   bool busy = false;
 };
@@ -335,13 +330,6 @@ struct Engine {
   std::condition_variable upload_cv;
   UploadSlot uploads[kUploadSlots];
   size_t upload_next = 0;
-  // Host-mask H2D copies run here, off the caller's stream, which only waits on the
-  // copy's event: the copy overlaps the kernels already queued there (round 4).
-  hipStream_t upload_st = nullptr;
-  // How host masks reach a per-stripe kernel (A/B build switch RS_MASK_UPLOAD):
-  // 0 = H2D on upload_st + cross-stream event, 1 = H2D on the launch stream itself,
-  // 2 = the kernel reads the pinned slot in place (no copy).
-  int mask_mode = RS_MASK_UPLOAD;
 
   std::mutex host_mu;                     // host-resident batches: one at a time per engine
   hipStream_t pipe_st[kHostStreams] = {};
@@ -401,11 +389,8 @@ struct Engine {
     }
     if (worker.joinable()) worker.join();
     (void)hipDeviceSynchronize();
-    for (auto& s : uploads) {
+    for (auto& s : uploads)
       if (s.done) (void)hipEventDestroy(s.done);
-      if (s.copied) (void)hipEventDestroy(s.copied);
-    }
-    if (upload_st) (void)hipStreamDestroy(upload_st);
     for (auto& l : lanes)
       if (l->stream) (void)hipStreamDestroy(l->stream);
     for (auto& s : pipe_st)
@@ -845,7 +830,8 @@ int copy_slots(const Layout& dst, const Layout& src, int k, const std::vector<in
 }
 
 // ---- per-stripe mask uploads ----------------------------------------------------
-// upload_acquire copies n host masks into a free slot and enqueues their H2D on s;
+// upload_acquire copies n host masks into a free slot and enqueues their copy to the
+// slot's device buffer on s;
 // the caller launches the kernel that reads them, then the guard's release records
 // the slot's event on s AFTER that kernel -- the slot (pinned and device buffer)
 // cannot be rewritten or reallocated while any kernel still reads it.
@@ -864,6 +850,16 @@ struct UploadGuard {
   }
 };
 
+// Round 6: the masks are copied into the slot's device buffer by a small kernel on
+// the launch stream itself, which reads the pinned slot over PCIe -- no DMA engine,
+// no second stream, no cross-stream event -- and the slot's `done` event carries no
+// system-scope release (it only tells the host that the kernel stopped reading the
+// slot).  Same-process A/B (profiles/r06b_ab_mask.log, profiles/r06a_ab_mask.log, 64 KiB
+// objects, mixed 0..m erasures per stripe with host masks) against round 5's H2D on
+// an upload stream + cross-stream event + a fenced done event: RS(4+2) 67.9 ->
+// 72.7 %, RS(8+4) 69.1 -> 69.6 %, RS(10+4) 59.4 -> 59.9 % of 8 TB/s.  (An H2D on the
+// launch stream lost 0.9-3.5 points, the kernel reading the pinned masks in place
+// 8-11.)
 int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
                    const uint32_t** dev) {
   UploadSlot* u = nullptr;
@@ -881,41 +877,23 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
       e->upload_cv.wait(lk);
     }
     u->busy = true;
-    if (!e->upload_st && hipStreamCreateWithFlags(&e->upload_st, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      e->upload_st = nullptr;  // the copy then runs on the caller's stream
-    }
   }
   g->e = e;
   g->u = u;
   g->s = s;
-  if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
-  if (!u->copied) RS_HIP(hipEventCreateWithFlags(&u->copied, hipEventDisableTiming));
+  if (!u->done) RS_HIP(hipEventCreateWithFlags(&u->done, hipEventDisableTiming | hipEventDisableSystemFence));
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
   u->host.numa = e->numa;
-  if (e->mask_mode == 2) {
-    const void* before = u->host.p;
-    if (u->host.ensure(n * 4)) return RS_ERR_DEVICE;
-    if (u->host.p != before || !u->host_dev) {
-      void* dp = nullptr;
-      RS_HIP(hipHostGetDevicePointer(&dp, u->host.p, 0));
-      u->host_dev = dp;
-    }
-    std::memcpy(u->host.p, masks, n * 4);
-    *dev = static_cast<const uint32_t*>(u->host_dev);
-    return RS_OK;
-  }
+  const void* before = u->host.p;
   if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
-  std::memcpy(u->host.p, masks, n * 4);
-  if (e->mask_mode == 1) {
-    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
-  } else if (e->upload_st) {
-    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, e->upload_st));
-    RS_HIP(hipEventRecord(u->copied, e->upload_st));
-    RS_HIP(hipStreamWaitEvent(s, u->copied, 0));
-  } else {
-    RS_HIP(hipMemcpyAsync(u->dev.p, u->host.p, n * 4, hipMemcpyHostToDevice, s));
+  if (u->host.p != before || !u->host_dev) {
+    void* dp = nullptr;
+    RS_HIP(hipHostGetDevicePointer(&dp, u->host.p, 0));
+    u->host_dev = dp;
   }
+  std::memcpy(u->host.p, masks, n * 4);
+  if (!rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev), static_cast<uint32_t*>(u->dev.p), n, s))
+    return RS_ERR_DEVICE;
   *dev = static_cast<const uint32_t*>(u->dev.p);
   return RS_OK;
 }

@@ -192,13 +192,6 @@ constexpr int path_cpol() {
 // in place; every other shape level.  K = 10 with E >= 2 would spill to scratch at 4
 // waves and is left alone.
 constexpr int kApplyMinWaves = 4;
-#ifndef RS_EM_INOUT
-#define RS_EM_INOUT 0
-#endif
-#ifndef RS_EM_ROWB
-#define RS_EM_ROWB 0
-#endif
-constexpr bool kEmRowBarrier = RS_EM_ROWB != 0;
 
 // 16-B store at base + off, or nothing at all when !live: a raw buffer
 // store whose offset then fails the range check, so the hardware drops it -- no
@@ -291,7 +284,7 @@ __device__ __forceinline__ uint32_t pop_low(uint32_t& bits) {
 // the accumulator with one 3-input XOR.  The scheduling barrier per input stops the
 // compiler from hoisting every input's tables into SGPRs at once (K*NR*5 dwords,
 // e.g. 100 for RS(10+4) x 2 rows -> SGPR spills through VGPR lanes).
-template <int K, int M, int R0, int NR, bool ROW_BARRIER = false>
+template <int K, int M, int R0, int NR>
 __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K], u32x4 (&y)[NR]) {
   if constexpr (RS_PATTERN_ONLY) {
 #pragma unroll
@@ -330,14 +323,9 @@ __device__ __forceinline__ void gf_rows(const uint8_t* plan, const u32x4 (&x)[K]
           pend[r][d] = prod;
       }
     };
-    // ROW_BARRIER: one row's lookups at a time (the scheduler would otherwise interleave
-    // every row's temporaries of this input for ILP, at the price of registers)
     row(std::integral_constant<int, 0>{});
-    if constexpr (ROW_BARRIER && NR > 1) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 1) row(std::integral_constant<int, 1>{});
-    if constexpr (ROW_BARRIER && NR > 2) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 2) row(std::integral_constant<int, 2>{});
-    if constexpr (ROW_BARRIER && NR > 3) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NR > 3) row(std::integral_constant<int, 3>{});
     if (c + 1 < K) __builtin_amdgcn_sched_barrier(0);
   }
@@ -547,28 +535,14 @@ __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void 
       }
     };
     u32x4 y[E];
-    if constexpr (PER_STRIPE && E > 2 && RS_EM_INOUT >= 2) {
-      // input-outer by the stripe's row count (A/B), as in apply_flat_seg_kernel
-      const uint32_t nrow = pv.n_out();
-      if (nrow <= 1u) {
-        u32x4 yy[1];
-        gf_rows<K, M, 0, 1>(plan, x, yy);
-        emit(std::integral_constant<int, 1>{}, std::integral_constant<int, path_cpol<K, E, 1>()>{}, yy);
-      } else if (nrow == 2u) {
-        u32x4 yy[2];
-        gf_rows<K, M, 0, 2>(plan, x, yy);
-        emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, yy);
-      } else if (E == 3 || nrow == 3u) {
-        u32x4 yy[3];
-        gf_rows<K, M, 0, 3>(plan, x, yy);
-        emit(std::integral_constant<int, 3>{}, std::integral_constant<int, out_cpol<K, E>()>{}, yy);
-      } else {
-        u32x4 yy[E > 3 ? 4 : 3];
-        gf_rows<K, M, 0, (E > 3 ? 4 : 3)>(plan, x, yy);
-        emit(std::integral_constant<int, (E > 3 ? 4 : 3)>{}, std::integral_constant<int, out_cpol<K, E>()>{}, yy);
-      }
-      continue;
-    } else if constexpr (PER_STRIPE && E > 2) {
+    if constexpr (PER_STRIPE && E > 2) {
+      // An intact or skipped stripe: its loads fetched nothing, and it has no row to
+      // compute either (round 6, same-process A/B, profiles/r06c_ab_fast.log: RS(8+4)
+      // 64 KiB mixed 0..4 erasures 71.9 -> 73.9 % of 8 TB/s; it used to compute and
+      // drop one row).
+      if (!work) continue;
+    }
+    if constexpr (PER_STRIPE && E > 2) {
       // every input's chunk indices once, then only the rows this stripe misses
       // (wave-uniform branches): a 1-erasure stripe computes one row, a 2-erasure
       // stripe two.  Round 2: RS(10+4) 64 KiB 1-erasure 63.5-66.9 -> 69.4-70.9 %,
@@ -956,6 +930,18 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
   // (no masks: one erasure pattern for the batch) has the one plan for every stripe
   const bool uni = a.present_masks == nullptr;
   auto plan_of = [&](uint32_t s, uint32_t& m, uint32_t& nout) -> const uint8_t* {
+    if (E > 2 && !uni) {
+      // an intact stripe (a scan's common case; launches sized for m outputs are the
+      // scans'): nothing to do, decided from the mask alone -- no LUT and plan round
+      // trips before the wave can leave (round 6, profiles/r06c_ab_fast.log: RS(10+4)
+      // 64 KiB mixed 0..4 erasures +0.7 points)
+      const uint32_t present = as_const<uint32_t>(a.present_masks)[s] & full;
+      if (present == full) {
+        m = full;
+        nout = 0u;
+        return uniform_ptr(a.plans);
+      }
+    }
     if (uni) {
       const uint8_t* p = uniform_ptr(a.plans);
       const PlanView pv(p, K, M);
@@ -1041,29 +1027,14 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         u32x4 y[E];
         gf_rows<K, M, 0, E>(plan, x, y);
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-      } else if constexpr (RS_EM_INOUT >= 1) {
-        // input-outer by the stripe's row count (A/B): x[K] and NR accumulators live,
-        // every input split once and folded into each of its NR rows as it arrives
-        if (nout <= 1u) {
-          u32x4 y[1];
-          gf_rows<K, M, 0, 1, kEmRowBarrier>(plan, x, y);
-          emit(std::integral_constant<int, 1>{}, std::integral_constant<int, kCpolFlatPath1>{}, y);
-        } else if (nout == 2u) {
-          u32x4 y[2];
-          gf_rows<K, M, 0, 2, kEmRowBarrier>(plan, x, y);
-          emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-        } else if (E == 3 || nout == 3u) {
-          u32x4 y[3];
-          gf_rows<K, M, 0, 3, kEmRowBarrier>(plan, x, y);
-          emit(std::integral_constant<int, 3>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-        } else {
-          u32x4 y[E > 3 ? 4 : 3];
-          gf_rows<K, M, 0, (E > 3 ? 4 : 3), kEmRowBarrier>(plan, x, y);
-          emit(std::integral_constant<int, (E > 3 ? 4 : 3)>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
-        }
       } else {
-        // each row path computes only its rows; stripes missing 3+ shards store each
-        // row as soon as it is computed (one row's accumulators live instead of E)
+        // E > 2 (device masks without a bound, mixed batches): every input split into
+        // chunk indices once, then only the rows the stripe misses, one at a time, in a
+        // wave-uniform branch per row count; stripes missing 3+ shards store each row as
+        // soon as it is computed.  (Rejected, round 6, profiles/r06b_ab_perm.log: the
+        // inputs folded into all of a stripe's rows as they arrive -- mixed +1.1 to
+        // +1.6, 2-erasure -1.5 to -2.7 points; the tasks scattered over the waves so a
+        // CU holds many stripes' erasure counts at once -- -5 to -12.)
         Idx3 ix[K][4];
 #pragma unroll
         for (int c = 0; c < K; ++c)
@@ -1775,6 +1746,25 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
   void* args[] = {const_cast<KernelArgs*>(&a)};
   if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
+}
+
+// Per-stripe host masks into device memory, read straight from the pinned slot over
+// PCIe: one 16-B load per lane (tail words singly), on the launch stream itself.
+__global__ __launch_bounds__(256) void words_copy_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                         uint64_t n) {
+  const uint64_t i = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4u;
+  if (i + 4u <= n) {
+    *reinterpret_cast<u32x4*>(dst + i) = *reinterpret_cast<const u32x4*>(src + i);
+  } else {
+    for (uint64_t j = i; j < n; ++j) dst[j] = src[j];
+  }
+}
+
+bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s) {
+  if (n == 0) return true;
+  const uint64_t blocks = (n + 1023u) / 1024u;
+  hipLaunchKernelGGL(words_copy_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError() == hipSuccess;
 }
 
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s) {

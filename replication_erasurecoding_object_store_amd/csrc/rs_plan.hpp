@@ -133,6 +133,9 @@ uint32_t default_blocks_per_cu(int k, int e);
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s, int occ_cap = -1);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
+// n uint32 words from src (pinned host memory the GPU maps, or device memory) to dst
+// (device memory), on s: per-stripe host masks staged by a kernel on the launch stream.
+bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.
 // Per-stripe plans (masks -> LUT) over a table of shard addresses instead of a

@@ -298,6 +298,7 @@ def test_out_pad_never_crosses_a_stripe_slot(engines, k, m, S):
         j = [s for s in range(t) if not (masks[i] >> s) & 1][0]
         assert np.array_equal(got[i, :S], full[i, j]), (i, j)
     assert (got[:N, S:] == 0xC3).all(), "a row's padding reached into the next stripe's row"
+    assert (got[N] == 0xC3).all()
 
 
 @pytest.mark.parametrize("k,m,S,bound", [(10, 4, 6554, 2), (10, 4, 6554, 0), (4, 2, 1000, 2), (8, 4, 8200, 1)])
@@ -347,7 +348,6 @@ def test_c_abi_default_rows_end_at_byte_s(k, m, S, bound):
                     assert (got[o + S:min(o + P, need)] == 0xC3).all(), ("row padding written", i, r)
     finally:
         svc.close()
-    assert (got[N] == 0xC3).all()
 
 
 @pytest.mark.parametrize("nbytes", [16, 4080, 4096, 4112, (1 << 20) + 16, 201326592])

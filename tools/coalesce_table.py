@@ -25,18 +25,21 @@ def main():
             key = f"GPU coalesced, {r['threads']} blocking callers{where}"
         elif mode == "async":
             key = f"GPU async, {r['threads']} loops x {r['depth']} in flight{where}"
+        elif mode == "hybrid":
+            key = f"hybrid, GPU limit {r['gpu_limit']}" + (f", GPU from {r['min_obj']} B" if r.get("min_obj") else "")
         else:
             key = f"{mode} {r['threads']}{where}"
         if key not in cols:
             cols.append(key)
-        rows[r["obj_bytes"]][key] = (r["user_GiBps"], r["calls_per_s"])
+        rows[r["obj_bytes"]][key] = (r["user_GiBps"], r["calls_per_s"], r.get("cpu_share"))
     print("| object | " + " | ".join(cols) + " |")
     print("|---|" + "---|" * len(cols))
     for obj in sorted(rows):
         cells = []
         for c in cols:
             v = rows[obj].get(c)
-            cells.append(f"{v[0]:.1f} GiB/s ({v[1] / 1e3:.0f} K/s)" if v else "")
+            share = f", {v[2] * 100:.0f} % on CPU" if v and v[2] is not None and "hybrid" in c else ""
+            cells.append(f"{v[0]:.1f} GiB/s ({v[1] / 1e3:.0f} K/s{share})" if v else "")
         size = f"{obj // 1024} KiB" if obj % 1024 == 0 else f"{obj / 1024:.0f} KiB"
         print(f"| {size} | " + " | ".join(cells) + " |")
 

@@ -19,7 +19,7 @@ import sys
 HBM_PEAK_GBS = 8000.0
 SHAPES = {"rs42_64KiB": (4, 2, 16384), "rs84_64KiB": (8, 4, 8192), "rs104_64KiB": (10, 4, 6554)}
 E_OF = {"encode": None, "encode_parity_pad": None, "reconstruct2": 2, "reconstruct1": 1,
-        "reconstruct2_out_pad": 2, "reconstruct1_out_pad": 1, "reconstruct2_exact_rows": 2, "reconstruct1_exact_rows": 1,
+        "reconstruct2_mslot_out": 2, "reconstruct1_mslot_out": 1, "reconstruct2_out_pad": 2, "reconstruct1_out_pad": 1, "reconstruct2_exact_rows": 2, "reconstruct1_exact_rows": 1,
         "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1,
         "reconstruct_mixed_unbounded": "mix", "reconstruct_mixed_host": "mix"}
 CONFIG3 = {"rec1_per_stripe_out": 1, "rec_0_1_uniform_out": 2, "rec_0_4_uniform_out": 2,
