@@ -256,7 +256,7 @@ int rs_co_encode_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards
  * thousands of values per launch (rs_co_encode_hash_many on a bulk load,
  * rs_sha256_batch).  Per-object writers should hash on the CPU while rs_co_encode
  * runs, as the Go shim's EncodeHash does: measured per object, this call moves
- * 0.5 GiB/s against 4-40 GiB/s for rs_co_encode. */
+ * 0.5 GiB/s against 4-40 GiB/s for rs_co_encode (`HISTORY.md` §A.4). */
 int rs_co_encode_hash(rs_coalescer *co, uint8_t *const *shards, const size_t *lens, size_t value_len,
                       uint8_t *digest);
 int rs_co_encode_hash_many(rs_coalescer *co, size_t n_objects, uint8_t *const *shards, const size_t *lens,
@@ -335,7 +335,7 @@ int rs_host_free(rs_ctx *ctx, void *ptr);
  * pins, maps or addresses caller memory in place (round 4).  amdgpu maps
  * hipHostRegister'ed pageable memory as a user-pointer range whose pages may still
  * be migrated, compacted or collapsed into huge pages while a kernel runs, which is
- * how in-place writes into it were lost.  Calls on registered
+ * how in-place writes into it were lost (`HISTORY.md` §A.1).  Calls on registered
  * buffers are staged like any pageable buffer; use rs_host_alloc for in-place
  * work.  Kept for ABI compatibility: RS_ERR_INVALID_ARG for a range overlapping a
  * known one; rs_host_unregister(ptr) forgets the range starting at ptr

@@ -48,11 +48,15 @@ import (
 // thread per in-flight request and pay a futex sleep and wake-up per object.
 //
 // Hybrid dispatch (round 6): a call runs on klauspost on its own goroutine instead
-// of the GPU when the object is smaller than gpuMinObject bytes (its staging costs
-// more CPU than encoding it), when gpuMaxInflight calls are already on the GPU (the
-// PCIe link is the limit there, and the CPU codec adds its own throughput), and when
-// the coalescer has no free staging batch (RS_ERR_BUSY) -- a call never waits for
-// the GPU.  Thresholds: tools/run_hybrid.sh, DESIGN.md §6.
+// of the GPU unless its shards all lie in one of the Service's Arenas (in place: the
+// kernel reads and writes them over PCIe with no staging copy) and the object is at
+// least gpuMinObject bytes, and fewer than gpuMaxInflight calls are on the GPU; a call
+// that finds no free staging batch (RS_ERR_BUSY) runs on the CPU as well -- a call
+// never waits for the GPU.  Measured per object on a 16-CPU quota
+// (profiles/r06*_hybrid.log, DESIGN.md §6): a staged call (Go heap shards) costs the
+// CPU more in staging copies than klauspost's GFNI kernels spend encoding it, so
+// routing those to the GPU lowers throughput at every size, while arena calls of
+// >= 100 KiB add the GPU's PCIe-bound rate to the CPU's (800 KiB: 72 -> 91 GiB/s).
 type Service struct {
 	ctx *C.rs_ctx
 	co  *C.rs_coalescer
@@ -66,7 +70,11 @@ type Service struct {
 	inflight   atomic.Int64 // calls submitted to the GPU and not yet completed
 	maxInfl    int64        // gpuMaxInflight (tests may lower it)
 	minGPUData int          // gpuMinObject (tests may change it)
+	stagedGPU  bool         // tests: staged (non-arena) calls may use the GPU too
 	reaping    atomic.Int32 // reaper goroutines still in their loop
+
+	arenaMu sync.RWMutex
+	arenas  []*Arena // live arenas: calls on their memory run in place
 
 	// broken: a reaper failed; the calls it left waiting got its error and every
 	// later call runs on klauspost (enc).  Set before waiting is flushed (mu).
@@ -79,7 +87,7 @@ type Service struct {
 // (profiles/r06*_hybrid.log, tools/run_hybrid.sh): objects of at least gpuMinObject
 // bytes go to the GPU while fewer than gpuMaxInflight calls are in flight there.
 const (
-	gpuMinObject   = 16 << 10
+	gpuMinObject   = 64 << 10
 	gpuMaxInflight = 64
 )
 
@@ -90,11 +98,11 @@ var errGPUUnavailable = errors.New("EC Driver: GPU engine unavailable")
 // reapTimeoutUs bounds one rs_co_reap wait so a reaper notices Close.
 const reapTimeoutUs = 100000
 
-// useGPU reserves a GPU slot for a call on an object of dataBytes user bytes, or
-// says the call runs on the CPU (hybrid dispatch).  A reserved slot is released by
-// call() when the call completes or is not submitted.
-func (s *Service) useGPU(dataBytes int) bool {
-	if !s.gpu || s.broken.Load() || dataBytes < s.minGPUData {
+// useGPU reserves a GPU slot for a call on an object of dataBytes user bytes whose
+// shards are `shards`, or says the call runs on the CPU (hybrid dispatch).  A
+// reserved slot is released by call() when the call completes or is not submitted.
+func (s *Service) useGPU(dataBytes int, shards [][]byte) bool {
+	if !s.gpu || s.broken.Load() || dataBytes < s.minGPUData || (!s.stagedGPU && !s.inArena(shards)) {
 		return false
 	}
 	if s.inflight.Add(1) > s.maxInfl {
@@ -202,6 +210,33 @@ func (s *Service) Close() {
 	C.rs_destroy(s.ctx)
 }
 
+// inArena: every shard's storage (len or, for a missing shard, cap) lies inside one
+// live Arena of this Service -- the calls the engine runs in place.
+func (s *Service) inArena(shards [][]byte) bool {
+	s.arenaMu.RLock()
+	defer s.arenaMu.RUnlock()
+	for _, a := range s.arenas {
+		lo := uintptr(a.base)
+		hi := lo + uintptr(a.size)
+		all := true
+		for _, sh := range shards {
+			if cap(sh) == 0 {
+				all = false
+				break
+			}
+			p := uintptr(unsafe.Pointer(&sh[:cap(sh)][0]))
+			if p < lo || p+uintptr(cap(sh)) > hi {
+				all = false
+				break
+			}
+		}
+		if all {
+			return true
+		}
+	}
+	return false
+}
+
 // gpuLaunches: codec kernels the engine has launched on all its GPUs so far
 // (rs_device_launches; the routing tests read it).
 func (s *Service) gpuLaunches() uint64 {
@@ -306,7 +341,7 @@ func shardArgs(shards [][]byte, pin *runtime.Pinner) (**C.uint8_t, *C.size_t, fu
 
 // Encode fills shards[K:] in place (ec.go:54-56).
 func (s *Service) Encode(shards [][]byte) error {
-	if len(shards) != config.K+config.M || !s.useGPU(config.K*len(shards[0])) {
+	if len(shards) != config.K+config.M || !s.useGPU(config.K*len(shards[0]), shards) {
 		return s.enc.Encode(shards) // klauspost's own checks and sentinels on the CPU path
 	}
 	var pin runtime.Pinner
@@ -353,7 +388,7 @@ func (s *Service) Reconstruct(shards [][]byte) error {
 		}
 		return nil
 	}
-	if !s.useGPU(config.K * size) {
+	if !s.useGPU(config.K*size, shards) {
 		return s.enc.Reconstruct(shards) // the GPU has enough in flight: this goroutine computes it
 	}
 	var pin runtime.Pinner
@@ -501,6 +536,7 @@ func (s *Service) ReconstructMany(objects [][][]byte) (errs []error) {
 // A bump allocator: Alloc until full, Reset when none of its slices is in use.
 // Nil on a GPU-less host (the CPU codec needs no arena).
 type Arena struct {
+	svc  *Service
 	ctx  *C.rs_ctx
 	base unsafe.Pointer
 	size int
@@ -518,7 +554,11 @@ func (s *Service) NewArena(size int) (*Arena, error) {
 	if rc := C.rs_host_alloc(s.ctx, C.size_t(n), &p); rc != C.RS_OK {
 		return nil, toErr(rc)
 	}
-	return &Arena{ctx: s.ctx, base: p, size: n}, nil
+	a := &Arena{svc: s, ctx: s.ctx, base: p, size: n}
+	s.arenaMu.Lock()
+	s.arenas = append(s.arenas, a)
+	s.arenaMu.Unlock()
+	return a, nil
 }
 
 // Alloc returns n bytes (16-B aligned, len = cap = n) or nil when the arena is full.
@@ -548,6 +588,14 @@ func (a *Arena) Reset() {
 // Close frees the arena (no call may be using it).
 func (a *Arena) Close() {
 	if a != nil && a.base != nil {
+		a.svc.arenaMu.Lock()
+		for i, x := range a.svc.arenas {
+			if x == a {
+				a.svc.arenas = append(a.svc.arenas[:i], a.svc.arenas[i+1:]...)
+				break
+			}
+		}
+		a.svc.arenaMu.Unlock()
 		C.rs_host_free(a.ctx, a.base)
 		a.base = nil
 	}

@@ -237,10 +237,11 @@ func TestArenaInPlaceMatchesKlauspost(t *testing.T) {
 	}
 }
 
-// Hybrid dispatch (VERDICT round 5 item 4): objects below the size threshold, calls
-// beyond the GPU's in-flight limit and calls that find no free staging batch run on
-// klauspost on the caller's goroutine; the rest on the GPU.  Every route gives
-// klauspost's bytes, and the engine's launch counter shows which route ran.
+// Hybrid dispatch (VERDICT round 5 item 4): staged objects (Go heap shards), objects
+// below the size threshold, calls beyond the GPU's in-flight limit and calls that find
+// no free staging batch run on klauspost on the caller's goroutine; large objects in
+// an Arena on the GPU, in place.  Every route gives klauspost's bytes, and the
+// engine's launch counter shows which route ran.
 func TestHybridRouting(t *testing.T) {
 	svc, ok := NewService().(*Service)
 	if !ok || !svc.gpu {
@@ -249,49 +250,74 @@ func TestHybridRouting(t *testing.T) {
 	defer svc.Close()
 	ref, _ := reedsolomon.New(config.K, config.M)
 	rng := rand.New(rand.NewSource(11))
-	roundTrip := func(n int) {
+	arena, err := svc.NewArena(64 << 20)
+	if err != nil {
+		t.Fatal(err)
+	}
+	defer arena.Close()
+	// inArena: the object's data and all K+M shard buffers carved from the arena
+	roundTrip := func(n int, inArena bool) {
 		data := make([]byte, n)
 		rng.Read(data)
 		want, _ := ref.Split(append([]byte(nil), data...))
 		_ = ref.Encode(want)
-		got, _ := svc.Split(append([]byte(nil), data...))
+		var got [][]byte
+		if inArena {
+			arena.Reset()
+			per := len(want[0])
+			got = make([][]byte, len(want))
+			for i := range got {
+				got[i] = arena.Alloc(per)
+				if i < config.K {
+					copy(got[i], want[i])
+				}
+			}
+		} else {
+			got, _ = svc.Split(append([]byte(nil), data...))
+		}
 		if err := svc.Encode(got); err != nil {
 			t.Fatal(err)
 		}
-		got[0], got[config.K] = nil, nil
+		got[0], got[config.K] = got[0][:0], got[config.K][:0]
 		if err := svc.Reconstruct(got); err != nil {
 			t.Fatal(err)
 		}
 		for i := range want {
 			if !bytes.Equal(got[i], want[i]) {
-				t.Fatalf("len %d shard %d differs from klauspost", n, i)
+				t.Fatalf("len %d (arena %v) shard %d differs from klauspost", n, inArena, i)
 			}
 		}
 	}
-	// below the size threshold: the CPU, no kernel
+	// staged (Go heap) objects of any size: the CPU, no kernel
 	before := svc.gpuLaunches()
-	roundTrip(gpuMinObject / 2)
+	roundTrip(gpuMinObject*4, false)
+	if svc.gpuLaunches() != before {
+		t.Fatal("a staged object reached the GPU")
+	}
+	// an arena object below the size threshold: the CPU
+	roundTrip(gpuMinObject/2, true)
 	if svc.gpuLaunches() != before {
 		t.Fatal("an object below gpuMinObject reached the GPU")
 	}
-	// at or above it: the GPU
-	roundTrip(gpuMinObject * 4)
+	// at or above it, in an arena: the GPU
+	roundTrip(gpuMinObject*4, true)
 	if svc.gpuLaunches() == before {
-		t.Fatal("a large object did not reach the GPU")
+		t.Fatal("a large arena object did not reach the GPU")
 	}
 	// the GPU's in-flight limit reached: the CPU
 	svc.maxInfl = 0
 	before = svc.gpuLaunches()
-	roundTrip(gpuMinObject * 4)
+	roundTrip(gpuMinObject*4, true)
 	if svc.gpuLaunches() != before {
 		t.Fatal("a call beyond gpuMaxInflight reached the GPU")
 	}
 	if svc.inflight.Load() != 0 {
 		t.Fatalf("in-flight count leaked: %d", svc.inflight.Load())
 	}
-	svc.maxInfl = gpuMaxInflight
-	// many concurrent callers with a small limit: some calls on each side, every one
-	// right, and the in-flight count back at zero
+	// many concurrent callers with a small limit (staged calls allowed on the GPU for
+	// the test): some calls on each side, every one right, and the in-flight count
+	// back at zero
+	svc.stagedGPU = true
 	svc.maxInfl = 2
 	done := make(chan error, 64)
 	for g := 0; g < 64; g++ {
@@ -336,7 +362,8 @@ func TestBusySubmittersRunOnCPU(t *testing.T) {
 		t.Skip("needs the GPU engine")
 	}
 	defer svc.Close()
-	svc.minGPUData = 0 // 4 KiB objects on the GPU too, so the batches fill up
+	svc.minGPUData = 0    // 4 KiB objects on the GPU too, so the batches fill up
+	svc.stagedGPU = true // (Go heap shards)
 	rng := rand.New(rand.NewSource(7))
 	objects := make([][][]byte, 4096)
 	for i := range objects {

@@ -859,7 +859,8 @@ struct UploadGuard {
 // an upload stream + cross-stream event + a fenced done event: RS(4+2) 67.9 ->
 // 72.7 %, RS(8+4) 69.1 -> 69.6 %, RS(10+4) 59.4 -> 59.9 % of 8 TB/s.  (An H2D on the
 // launch stream lost 0.9-3.5 points, the kernel reading the pinned masks in place
-// 8-11.)
+// 8-11; the copy kernel on a second stream, overlapping the previous kernel, with a
+// fence-free event: level, profiles/r06f_ab_side.log.)
 int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
                    const uint32_t** dev) {
   UploadSlot* u = nullptr;
@@ -910,7 +911,7 @@ int ensure_pipe_stream(Engine* e, int i) {
 // must move every slot a stripe might use).  Memory the library does not own --
 // pageable, rs_host_register'ed or pinned by someone else -- never qualifies: a
 // kernel never reads or writes pages whose lifetime and placement the library does
-// not control.  Returns RS_ERR_NOT_SUPPORTED when the batch does
+// not control (`HISTORY.md` §A.1).  Returns RS_ERR_NOT_SUPPORTED when the batch does
 // not qualify.
 int host_zero_copy(Engine* e, const Layout& hl, size_t S, size_t N, const uint8_t* plan_dev,
                    const uint32_t* masks_host, int e_out, uint32_t* bad_host) {
@@ -1869,7 +1870,7 @@ bool reg_erase(rs_ctx* c, void* ptr, bool owned) {
 // hipHostRegister'ed pageable memory as a user-pointer range whose pages the kernel
 // may still migrate, compact or collapse into huge pages under a running kernel;
 // the round-3 records show lost in-place writes and a late-reported illegal address
-// right after the only tests that ran GPU work on such ranges.  So no
+// right after the only tests that ran GPU work on such ranges (`HISTORY.md` §A.1).  So no
 // kernel and no DMA of this library touches caller pages in place: calls on
 // registered buffers are staged through the library's own page-locked memory, and
 // in-place work needs rs_host_alloc.

@@ -387,7 +387,7 @@ __device__ __forceinline__ u32x4 gf_row_ix(const uint8_t* plan, const Idx3 (&ix)
 // max_missing bound) is skipped and flagged (status bit 1).
 // Every trip issues the same loads; the wave-uniform branches differ only in VALU
 // work and in how many stores end the trip, so the compiler's vmcnt bookkeeping
-// stays exact (a branch around the loads does not: DESIGN.md Appendix A.5).
+// stays exact (a branch around the loads does not: `HISTORY.md` §A.5).
 template <int K, int M, int E, bool PER_STRIPE>
 __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void apply_kernel(
     const KernelArgs a) {
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void 
       // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
       // (profiles/r02c_ab_ix_rows.log).  Input-outer passes of <= 2 rows instead
       // (round 4) lost 9-10 points on 4-erasure and mixed batches
-      // (profiles/r04g_ab_twopass.log).
+      // (profiles/r04g_ab_twopass.log, `HISTORY.md` §A.5).
       Idx3 ix[K][4];
 #pragma unroll
       for (int c = 0; c < K; ++c)

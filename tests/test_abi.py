@@ -142,7 +142,7 @@ def test_single_hip_runtime_per_process():
 
 
 def test_no_gpu_mapping_of_caller_memory():
-    """DESIGN.md Appendix A.1 (round 4): the library never creates a GPU mapping of memory it
+    """`HISTORY.md` §A.1 (round 4): the library never creates a GPU mapping of memory it
     does not own -- no hipHostRegister (userptr ranges whose pages the host kernel may
     move under a running kernel) and no environment-controlled switches.  In-place
     kernels address only rs_host_alloc'ed (hipHostMalloc) memory."""

@@ -636,7 +636,7 @@ def test_host_alloc_batches_zero_copy(engines):
 
 
 def test_host_path_routing(engines):
-    """Which host memory a kernel may address in place: only the
+    """Which host memory a kernel may address in place (`HISTORY.md` §A.1): only the
     context's own page-locked memory (rs_host_alloc) runs zero-copy.  Pageable,
     rs_host_register'ed and torch-pinned memory -- pages whose placement the library
     does not control -- are staged, and the bytes are the same either way."""

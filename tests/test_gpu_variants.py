@@ -175,7 +175,7 @@ def test_devmask_bound_flags_and_skips_excess(engines, k, m, S, bound):
 
 # Sporadic-corruption guard for the output stores: every kernel stores with one
 # cache policy (out_cpol); a per-lane mix of policies once returned wrong 64-B
-# halves of rows on a few stripes per run (profiles/r03n_ab_cpol.log).
+# halves of rows on a few stripes per run (`HISTORY.md` §A.1 / §A.5, profiles/r03n_ab_cpol.log).
 # Larger batches than the parity tests, two pattern draws each, every output row
 # and every unused output slot compared (vectorised).
 @pytest.mark.parametrize("k,m,S,bound", [(8, 4, 6554, 1), (10, 4, 6554, 2), (8, 4, 6554, 4), (8, 4, 8192, 1),

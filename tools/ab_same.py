@@ -1,7 +1,7 @@
 """Same-process A/B of librsgpu variants (abx/<name>.so from tools/build_ab.sh).
 
 tools/run_ab.sh runs each variant in its own process, and an allocation's physical
-pages move a leg by up to 2 points from process to process (the
+pages move a leg by up to 2 points from process to process (`HISTORY.md` §A.5: the
 spread is fixed per allocation).  Here every variant library is loaded into ONE
 process (ctypes, RTLD_LOCAL: each keeps its own kernels and context) and they
 take turns on the SAME device buffers, in an order that rotates every round, each

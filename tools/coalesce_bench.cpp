@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <string>
 #include <thread>
@@ -102,8 +103,6 @@ int main(int argc, char** argv) {
   std::atomic<int> ready{0};  // threads done building their objects: the clock starts after all
   std::atomic<uint64_t> ops{0}, bad{0}, busy{0}, cpu_ops{0};
   std::atomic<long> gpu_inflight{0};  // hybrid: calls submitted and not yet reaped (all threads)
-  std::unique_ptr<std::atomic<int>[]> done_word(new std::atomic<int>[static_cast<size_t>(T) * depth]);
-  for (size_t i = 0; i < static_cast<size_t>(T) * depth; ++i) done_word[i].store(0);
   std::vector<std::thread> ts;
   // One object's k+m shards; the reference parity comes from a direct call, and
   // before every call the shards it must write are scribbled, so a call that writes
@@ -122,8 +121,14 @@ int main(int argc, char** argv) {
   const int reg_mode = std::getenv("REGISTER") ? std::atoi(std::getenv("REGISTER")) : 0;
   const bool reg = reg_mode != 0;
   const size_t SP = (S + 63) / 64 * 64;
-  const size_t per_thread = async_mode ? static_cast<size_t>(depth)
-                                       : std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
+  // objects per thread: blocking and hybrid threads cycle through their share of
+  // ROTATE_MB (DRAM-resident calls); an asynchronous GPU loop holds `depth` in flight
+  const size_t rot_share = std::max<size_t>(1, rotate_bytes / (static_cast<size_t>(T) * (k + m) * S));
+  const size_t per_thread = hybrid_mode  ? std::max<size_t>(static_cast<size_t>(depth), rot_share)
+                            : async_mode ? static_cast<size_t>(depth)
+                                         : rot_share;
+  std::unique_ptr<std::atomic<int>[]> done_word(new std::atomic<int>[static_cast<size_t>(T) * per_thread]);
+  for (size_t i = 0; i < static_cast<size_t>(T) * per_thread; ++i) done_word[i].store(0);
   uint8_t* arena = nullptr;
   size_t arena_bytes = 0;
   if (reg) {
@@ -221,20 +226,24 @@ int main(int argc, char** argv) {
         // may reap any call, as the Go shim's single reaper goroutine does), so a
         // reaped tag = (thread << 32 | object) is routed to its owner through a
         // completion word; each loop then handles its own completed objects.
+        const int npool = static_cast<int>(per_thread);
         std::vector<Obj> objs;
-        for (int d = 0; d < depth; ++d) objs.push_back(make_obj(static_cast<uint64_t>(t) * depth + d, static_cast<size_t>(t) * per_thread + d));
-        std::vector<int> idle;
-        for (int d = depth - 1; d >= 0; --d) idle.push_back(d);
+        for (int d = 0; d < npool; ++d)
+          objs.push_back(make_obj(static_cast<uint64_t>(t) * npool + d, static_cast<size_t>(t) * per_thread + d));
+        std::deque<int> idle;  // in rotation order: the least recently used object first
+        for (int d = 0; d < npool; ++d) idle.push_back(d);
+        std::vector<int> flying;  // submitted, not yet completed
+        auto last_reap = std::chrono::steady_clock::now();
         std::vector<uint64_t> tags(256);
         std::vector<int> rcs(256);
-        std::atomic<int>* mine_done = &done_word[static_cast<size_t>(t) * depth];
+        std::atomic<int>* mine_done = &done_word[static_cast<size_t>(t) * per_thread];
         ++ready;
         while (!start.load()) std::this_thread::yield();
         uint64_t mine = 0, nb = 0, e = 0, inflight = 0, on_cpu = 0;
         while (!stop.load(std::memory_order_relaxed) || inflight) {
           bool cpu_ran = false;
           while (!idle.empty() && !stop.load(std::memory_order_relaxed)) {
-            const int d = idle.back();
+            const int d = idle.front();
             Obj& o = objs[d];
             const int lost = prep(o);
             bool to_gpu = true;
@@ -257,6 +266,8 @@ int main(int argc, char** argv) {
               ++mine;
               ++on_cpu;
               cpu_ran = true;
+              idle.pop_front();
+              idle.push_back(d);  // to the back of the rotation
               break;  // one CPU call, then reap what the GPU finished meanwhile
             }
             if (rc == RS_ERR_BUSY) {
@@ -267,18 +278,32 @@ int main(int argc, char** argv) {
               ++e;
               break;
             }
-            idle.pop_back();
+            idle.pop_front();
+            flying.push_back(d);
             ++inflight;
           }
           if (!inflight) continue;
+          if (cpu_ran) {
+            // between CPU calls, poll the GPU's completions at most every 20 us: a reap
+            // costs about as much as a 4 KiB CPU call
+            const auto now = std::chrono::steady_clock::now();
+            if (now - last_reap < std::chrono::microseconds(20)) continue;
+            last_reap = now;
+          }
           const int got = rs_co_reap(co, tags.data(), rcs.data(), 256, cpu_ran ? 0 : 50);
           if (hybrid_mode && got > 0) gpu_inflight.fetch_sub(got, std::memory_order_relaxed);
           for (int g = 0; g < got; ++g)
-            done_word[(tags[g] >> 32) * static_cast<uint64_t>(depth) + (tags[g] & 0xFFFFFFFFu)].store(
+            done_word[(tags[g] >> 32) * static_cast<uint64_t>(per_thread) + (tags[g] & 0xFFFFFFFFu)].store(
                 rcs[g] + 1, std::memory_order_release);
-          for (int d = 0; d < depth; ++d) {
+          for (size_t q = 0; q < flying.size();) {  // this loop's calls in flight
+            const int d = flying[q];
             const int v = mine_done[d].load(std::memory_order_acquire);
-            if (!v) continue;
+            if (!v) {
+              ++q;
+              continue;
+            }
+            flying[q] = flying.back();
+            flying.pop_back();
             mine_done[d].store(0, std::memory_order_relaxed);
             if (v - 1 != RS_OK) ++e;
             e += check(objs[d]);

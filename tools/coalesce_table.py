@@ -26,7 +26,8 @@ def main():
         elif mode == "async":
             key = f"GPU async, {r['threads']} loops x {r['depth']} in flight{where}"
         elif mode == "hybrid":
-            key = f"hybrid, GPU limit {r['gpu_limit']}" + (f", GPU from {r['min_obj']} B" if r.get("min_obj") else "")
+            key = (f"hybrid, GPU limit {r['gpu_limit']}" + (f", GPU from {r['min_obj']} B" if r.get("min_obj") else "")
+                   + where)
         else:
             key = f"{mode} {r['threads']}{where}"
         if key not in cols:

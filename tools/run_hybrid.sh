@@ -16,7 +16,7 @@
 set -o pipefail
 B=tools/coalesce_bench
 run() {  # each run under its own limit; a limit, kill or fault (>= 124) ends the sweep
-  echo "# GPU_LIMIT=${GPU_LIMIT:-} MIN_OBJ=${MIN_OBJ:-} $*" >&2
+  echo "# REGISTER=${REGISTER:-0} GPU_LIMIT=${GPU_LIMIT:-} MIN_OBJ=${MIN_OBJ:-} $*" >&2
   timeout -k 5 60 "$@"
   local rc=$?
   if [ $rc -ne 0 ]; then echo "# rc=$rc" >&2; fi
@@ -29,11 +29,15 @@ Q=${Q:-16}
 CPUS=$(tools/gpu_local_cpus.sh $Q)
 PIN="taskset -c $CPUS"
 echo "# callers on cpus $CPUS, quota $Q" >&2
+# REGISTER=2: the objects live in an rs_host_alloc arena, so GPU calls run in place
+# (no staging copy on the CPU); the CPU codec works on the same memory
 for OBJ in ${SIZES:-4096 10240 102400 819200 1536000}; do
   run $PIN $B $Q $SECS mix cpu 0 0 $OBJ
-  run $PIN $B $Q $SECS mix async 0 0 $OBJ 0 0 0 64
-  for L in ${LIMITS:-16 64 256}; do
-    D=$(( L / Q + 2 ))
-    GPU_LIMIT=$L MIN_OBJ=${MIN_OBJ:-0} run $PIN $B $Q $SECS mix hybrid 0 0 $OBJ 0 0 0 $D
+  for R in ${REGS:-0 2}; do
+    REGISTER=$R run $PIN $B $Q $SECS mix async 0 0 $OBJ 0 0 0 64
+    for L in ${LIMITS:-16 64}; do
+      D=$(( L / Q + 2 ))
+      REGISTER=$R GPU_LIMIT=$L MIN_OBJ=${MIN_OBJ:-0} run $PIN $B $Q $SECS mix hybrid 0 0 $OBJ 0 0 0 $D
+    done
   done
 done
