@@ -1034,7 +1034,9 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         // soon as it is computed.  (Rejected, round 6, profiles/r06b_ab_perm.log: the
         // inputs folded into all of a stripe's rows as they arrive -- mixed +1.1 to
         // +1.6, 2-erasure -1.5 to -2.7 points; the tasks scattered over the waves so a
-        // CU holds many stripes' erasure counts at once -- -5 to -12.)
+        // CU holds many stripes' erasure counts at once -- -5 to -12; the survivors of
+        // a task 512-4096 tasks ahead fetched into L2 by LDS-DMA loads while the own
+        // inputs load, -15 to -22, profiles/r06h_ab_prefetch.log.)
         Idx3 ix[K][4];
 #pragma unroll
         for (int c = 0; c < K; ++c)
