@@ -100,6 +100,9 @@ def main():
     vs = [variant(n) for n in names]
     print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
     for wl in args.workloads.split(","):
+        # "<workload>@dense": bounded calls write `bound` rows per stripe back to back;
+        # "@densepad": the same with the out stripe pitch 256 B longer; default: m-row slots
+        wl, _, layout = wl.partition("@")
         k, m, S, N, mode = WORKLOADS[wl]
         t = k + m
         P = (S + 255) // 256 * 256
@@ -107,7 +110,9 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1)
         bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
                  torch.empty((N, m, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
-        outs = [torch.empty((N, m, P), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+        out_rows = {"rec1pb_out": 1, "rec2pb_out": 2}.get(mode, m) if layout else m
+        osp = out_rows * P + (256 if layout == "densepad" else 0)
+        outs = [torch.empty((N, osp), dtype=torch.uint8, device="cuda") for _ in range(nb)]
         rng = np.random.default_rng(3)
         full = (1 << t) - 1
         if mode in ("rec1pb_out", "rec1p_out"):
@@ -171,7 +176,7 @@ def main():
                                                         md.data_ptr(), None)
             elif bound:
                 rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
-                                                            md.data_ptr(), bound, outs[i % nb].data_ptr(), m * P,
+                                                            md.data_ptr(), bound, outs[i % nb].data_ptr(), osp,
                                                             None)
             elif mode == "recmixh_out":
                 rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
@@ -213,7 +218,7 @@ def main():
             kname = v.lib.rs_last_kernel(v.ctx_for(k, m)).decode()
             base = np.array(res[vs[0].name])
             mine = np.array(res[v.name])
-            print(f"{wl:24s} {v.name:10s} median {np.median(mine) * 100:5.1f}%  min {mine.min() * 100:5.1f}  "
+            print(f"{wl + ('@' + layout if layout else ''):24s} {v.name:10s} median {np.median(mine) * 100:5.1f}%  min {mine.min() * 100:5.1f}  "
                   f"max {mine.max() * 100:5.1f}  paired diff vs {vs[0].name}: {np.median(mine - base) * 100:+5.2f} "
                   f"points  {kname}", flush=True)
         agree = len(set(digests.values())) == 1

@@ -5,6 +5,7 @@ number there is taken from the committed profiles of that tree:
   profiles/<tag>_sweep_trace.json      the bench's K/M-sweep windows under rocprofv3
   profiles/<tag>_pattern_ceilings.json compute-free twins (ceiling_probe.sh)
   profiles/<tag>_drop_in.log           tools/run_drop_in.sh
+  profiles/<tag>_bench_gpus2.json      bench.py --gpus 2 with gloo on one GPU (final_validate.sh b)
 Usage: python tools/design_tables.py <tag>   (prints markdown sections)
 """
 import json
@@ -83,6 +84,38 @@ def main():
                        f"**{e.get('zero-copy')} GiB/s** ({hm['e2e_objects_per_s'].get('zero-copy') / 1e6:.1f} M "
                        f"objects/s), staged **{e.get('staged')} GiB/s**; device-resident {hm['device_GiBps']:,.0f} GiB/s; "
                        f"sample ok {hm['ok_sample']} |")
+        mc = ex.get("multi_ctx")
+        if mc:
+            out.append(f"| one context over every visible GPU (`rs_create_multi(4, 2, 0)`, devices {mc['devices']}) | "
+                       f"host batch of {mc['objects']:,} × {mc['object_bytes'] // 1024} KiB through `fan_out`: "
+                       f"zero-copy encode {mc['zero-copy']['encode_GiBps']} / 1-erasure "
+                       f"{mc['zero-copy']['reconstruct1_GiBps']} GiB/s, staged {mc['staged']['encode_GiBps']} / "
+                       f"{mc['staged']['reconstruct1_GiBps']} GiB/s; coalesced burst of {mc['coalesced_burst']['objects']:,} "
+                       f"× {mc['coalesced_burst']['object_bytes'] // 1024} KiB in {mc['coalesced_burst']['batches']} "
+                       f"batches; launches per device {mc['zero-copy']['launches_per_device']} / "
+                       f"{mc['staged']['launches_per_device']} / {mc['coalesced_burst']['launches_per_device']}; "
+                       f"ok {mc['ok']} |")
+    g2 = load(f"{tag}_bench_gpus2.json")
+    if g2:
+        out.append("")
+        out.append(f"### The N-rank line, rehearsed with 2 ranks on one GPU (`profiles/{tag}_bench_gpus2.json`)\n")
+        out.append(f"`n_gpus` {g2['n_gpus']}, `physical_gpus` {g2['physical_gpus']}, `value` {g2['value']:,.0f} GiB/s, "
+                   f"parity {g2['parity_check_full_size']}. Both ranks share the chip, so each rank alone runs at the "
+                   f"GPU's rate and together at half of it: the efficiency fields read about 0.5 here and measure "
+                   f"the real thing on distinct GPUs.\n")
+        out.append("| leg | per rank concurrent (GiB/s) | per rank alone (GiB/s) | per-GPU efficiency |\n|---|---|---|---|")
+        sc = g2.get("scaling_check")
+        if sc:
+            out.append(f"| headline step ({sc['steps']} steps) | {sc['per_rank_GiBps']} | {sc['solo_GiBps']} | "
+                       f"{sc['per_gpu_efficiency']} |")
+        for shape, ent in g2.get("extras", {}).get("kmsweep_64KiB_device", {}).items():
+            for key in ("encode", "reconstruct2"):
+                if f"{key}_per_gpu_efficiency" in ent:
+                    out.append(f"| {shape} {key} | {ent[f'{key}_per_rank_GiBps']} | {ent[f'{key}_solo_GiBps']} | "
+                               f"{ent[f'{key}_per_gpu_efficiency']} |")
+        for path, v in g2.get("extras", {}).get("healer_mix_config5", {}).get("e2e_scaling_check", {}).items():
+            out.append(f"| config 5 e2e, {path} | {v['per_rank_GiBps']} | {v['solo_GiBps']} | "
+                       f"{v['per_gpu_efficiency']} |")
     if sw:
         out.append("")
         out.append(f"### K/M sweep and config 3 (`profiles/{tag}_sweep_trace.md`"

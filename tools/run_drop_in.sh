@@ -8,7 +8,8 @@
 #     one call per thread: 1 core, and the box's CPU quota;
 #   * the coalesced GPU drop-in on caller memory (staged): 64 blocking callers, and
 #     one event loop per quota core with 64 asynchronous calls in flight;
-#   * the same two in place, objects in an rs_host_alloc arena (REGISTER=2).
+#   * the same two in place, objects in an rs_host_alloc arena (REGISTER=2);
+#   * the Go shim's hybrid dispatch on arena objects (tools/run_hybrid.sh sweeps it).
 # Callers are pinned to the quota's cores on the GPU's NUMA node.  One JSON line per
 # run (tools/coalesce_bench.cpp); tools/coalesce_table.py makes the table.
 # Usage: tools/run_drop_in.sh     (SIZES, SECS, ROTATE_MB override the defaults)
@@ -36,4 +37,8 @@ for OBJ in ${SIZES:-4096 10240 102400 819200 1536000}; do
     REGISTER=$R run $PIN $B 64 $SECS mix co 0 0 $OBJ
     REGISTER=$R run $PIN $B $Q $SECS mix async 0 0 $OBJ 0 0 0 64
   done
+  # the Go shim's hybrid dispatch on arena objects: the GPU for objects of >= 64 KiB
+  # while fewer than 64 calls are there, the CPU codec for everything else
+  # (integration/go/internal/ec/ec_gpu.go gpuMinObject / gpuMaxInflight)
+  REGISTER=2 GPU_LIMIT=64 MIN_OBJ=65536 run $PIN $B $Q $SECS mix hybrid 0 0 $OBJ 0 0 0 6
 done

@@ -21,7 +21,7 @@ def main():
     for ln in open(sys.argv[1]):
         m = re.match(r"(\S+)\s+\S+\s+median\s+([\d.]+)%", ln)
         if m:
-            got[m.group(1)] = float(m.group(2)) / 100
+            got[m.group(1).split("@")[0]] = float(m.group(2)) / 100  # "@dense": the output-row layout
     print("| shape | " + " | ".join(LABEL[md] for md in SURVEY_MODES) + " |")
     print("|---" * (len(SURVEY_MODES) + 1) + "|")
     for sh in _SURVEY_SHAPES:
