@@ -179,6 +179,24 @@ int rs_reconstruct_batch_out_devmask(rs_ctx *ctx, const uint8_t *data, size_t da
                                      size_t shard_pitch, size_t shard_len, size_t n_stripes,
                                      const uint32_t *present_masks_dev, int max_missing, uint8_t *out,
                                      size_t out_stripe_pitch, void *stream);
+/* Packed out-of-place reconstruct (RS_MEM_DEVICE only, k+m <= 16), for scans whose
+ * stripes miss 0..m shards each (the healer's audit of a batch of objects,
+ * poller.go:227-309): the missing shards of the whole batch are written back to
+ * back, stripe i's r-th missing shard (index order, data before parity) at
+ *   out + (row_offsets[i] + r) * shard_pitch,
+ * where row_offsets (a device array of n_stripes + 1 uint32 the call fills) is the
+ * exclusive prefix sum of the stripes' erasure counts and row_offsets[n_stripes] the
+ * batch's total -- so out needs total * shard_pitch bytes, not n_stripes * m rows
+ * (intact stripes take none, a stripe with < k present none either: at most
+ * n_stripes * m rows).  present_masks: host (n_stripes) or, with masks_on_device != 0,
+ * device (errors deferred to rs_sync: a stripe with < k present is reported and
+ * skipped).  Whole-line rows follow rs_set_out_pad_writes (each row
+ * owns one shard_pitch).  Streams faster than the m-row slots of
+ * rs_reconstruct_batch_out on scans. */
+int rs_reconstruct_batch_out_packed(rs_ctx *ctx, const uint8_t *data, size_t data_stripe_pitch,
+                                    const uint8_t *parity, size_t parity_stripe_pitch, size_t shard_pitch,
+                                    size_t shard_len, size_t n_stripes, const uint32_t *present_masks,
+                                    int masks_on_device, uint8_t *out, uint32_t *row_offsets, void *stream);
 /* Batched parity verify / bit-rot scrub ([upstream reedsolomon.go Verify], per
  * object: rs_verify).  Recomputes every parity shard from the data shards and
  * compares it with the stored one: bad[i] = bitmask of stripe i's parity shards

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rs_reconstruct_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _u32p, _sz, _i, _vp]),
     "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
     "rs_reconstruct_batch_out": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _sz, _i, _vp, _sz, _vp]),
+    "rs_reconstruct_batch_out_packed": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _vp, _vp]),
     "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
     "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
     "rs_sync": (_i, [_vp, _vp]),

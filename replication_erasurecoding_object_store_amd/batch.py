@@ -112,6 +112,26 @@ class BatchEngine(Service):
                                                    out.data_ptr(), osp, _stream_handle(stream)))
         del keep
 
+    def reconstruct_packed(self, data, parity, out, row_offsets, shard_len: int, n_stripes: int,
+                           present_masks=None, masks_dev=None, shard_pitch: Optional[int] = None,
+                           stream=None) -> None:
+        """Packed out-of-place reconstruct (rs_reconstruct_batch_out_packed): the missing
+        shards of the batch back to back, stripe i's r-th at row row_offsets[i] + r of
+        `out` (rows of shard_pitch bytes); row_offsets: int32/uint32 device tensor of
+        n_stripes + 1, filled by the call.  Masks: host array or device tensor."""
+        P = shard_pitch or data.shape[-1]
+        if masks_dev is not None:
+            mptr, on_dev, keep = ctypes.c_void_p(masks_dev.data_ptr()), 1, None
+        else:
+            keep = _masks(present_masks)
+            if keep.size != n_stripes:
+                raise ValueError("present_masks: one per stripe")
+            mptr, on_dev = ctypes.c_void_p(keep.ctypes.data), 0
+        _check(_lib.lib().rs_reconstruct_batch_out_packed(
+            self.ctx, data.data_ptr(), self.k * P, parity.data_ptr(), self.m * P, P, shard_len, n_stripes, mptr,
+            on_dev, out.data_ptr(), row_offsets.data_ptr(), _stream_handle(stream)))
+        del keep
+
     def verify(self, data, parity, bad, shard_len: int, n_stripes: int, shard_pitch: Optional[int] = None,
                stream=None) -> None:
         """Scrub: bad [N] int32/uint32 device tensor <- bitmask of mismatching parity

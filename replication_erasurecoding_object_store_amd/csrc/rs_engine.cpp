@@ -861,8 +861,11 @@ struct UploadGuard {
 // launch stream lost 0.9-3.5 points, the kernel reading the pinned masks in place
 // 8-11; the copy kernel on a second stream, overlapping the previous kernel, with a
 // fence-free event: level, profiles/r06f_ab_side.log.)
+// extra (optional): extra_n more host words copied the same way straight into
+// extra_dst (device memory the caller owns), e.g. a packed batch's row offsets.
 int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, UploadGuard* g,
-                   const uint32_t** dev) {
+                   const uint32_t** dev, const uint32_t* extra = nullptr, size_t extra_n = 0,
+                   uint32_t* extra_dst = nullptr) {
   UploadSlot* u = nullptr;
   {
     std::unique_lock<std::mutex> lk(e->upload_mu);
@@ -886,14 +889,17 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   if (u->used) RS_HIP(hipEventSynchronize(u->done));  // the last kernel that read this slot is done
   u->host.numa = e->numa;
   const void* before = u->host.p;
-  if (u->host.ensure(n * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
+  if (u->host.ensure((n + extra_n) * 4) || u->dev.ensure(n * 4)) return RS_ERR_DEVICE;
   if (u->host.p != before || !u->host_dev) {
     void* dp = nullptr;
     RS_HIP(hipHostGetDevicePointer(&dp, u->host.p, 0));
     u->host_dev = dp;
   }
   std::memcpy(u->host.p, masks, n * 4);
+  if (extra_n) std::memcpy(static_cast<uint32_t*>(u->host.p) + n, extra, extra_n * 4);
   if (!rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev), static_cast<uint32_t*>(u->dev.p), n, s))
+    return RS_ERR_DEVICE;
+  if (extra_n && !rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev) + n, extra_dst, extra_n, s))
     return RS_ERR_DEVICE;
   *dev = static_cast<const uint32_t*>(u->dev.p);
   return RS_OK;
@@ -1387,6 +1393,55 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
   return launch(e, a, most, true, s);
 }
 
+// Packed out-of-place reconstruct: the missing shards of the whole batch back to back,
+// stripe i's from row row_offsets[i] (an exclusive prefix sum of the erasure counts,
+// written here: N + 1 device words; a stripe with < k present takes none, so the batch
+// needs at most N * m rows).  Device masks: a one-workgroup scan kernel ahead
+// of the reconstruct on s; host masks: the offsets summed on the host and copied with
+// the masks.
+int engine_reconstruct_batch_packed(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                    size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
+                                    int masks_on_device, uint8_t* out, uint32_t* row_offsets, hipStream_t s) {
+  if (N == 0) return RS_OK;
+  if (S == 0) return RS_ERR_SHARD_NO_DATA;
+  if (!batch_sizes_ok(S, N, pitch) || N >= 0xFFFFFFFFull / 32u) return RS_ERR_INVALID_ARG;
+  const Layout L{const_cast<uint8_t*>(data), data_sp, const_cast<uint8_t*>(parity), parity_sp, pitch};
+  if (!device_layout_ok(L, e->m, S) || reinterpret_cast<uintptr_t>(out) % 16 ||
+      reinterpret_cast<uintptr_t>(row_offsets) % 4)
+    return RS_ERR_INVALID_ARG;
+  if (!e->have_lut) return RS_ERR_NOT_SUPPORTED;
+  const int t = e->k + e->m;
+  const uint32_t full = static_cast<uint32_t>(full_mask64(t));
+  rs::KernelArgs a = make_args(e, L, S, N);
+  a.out = out;
+  a.out_sp = pitch;  // each row owns one pitch: whole-line rows stay inside it
+  a.row_offsets = row_offsets;
+  a.plans = static_cast<const uint8_t*>(e->d_plans.p);
+  if (masks_on_device) {
+    if (!rs::launch_row_offsets(masks, full, static_cast<uint32_t>(e->m), row_offsets, N, s)) return RS_ERR_DEVICE;
+    a.present_masks = masks;
+    return launch(e, a, e->m, true, s);
+  }
+  int most = 0;
+  std::vector<uint32_t> offs(N + 1);
+  uint32_t rows = 0;
+  for (size_t i = 0; i < N; ++i) {
+    const int np = __builtin_popcount(masks[i] & full);
+    if (np < e->k) return RS_ERR_TOO_FEW_SHARDS;
+    offs[i] = rows;
+    rows += static_cast<uint32_t>(t - np);
+    most = std::max(most, t - np);
+  }
+  offs[N] = rows;
+  UploadGuard ug;
+  const uint32_t* dm = nullptr;
+  int rc = upload_acquire(e, masks, N, s, &ug, &dm, offs.data(), N + 1, row_offsets);
+  if (rc) return rc;
+  if (most == 0) return RS_OK;  // the offsets are all 0 (copied above), nothing to compute
+  a.present_masks = dm;
+  return launch(e, a, most, true, s);
+}
+
 int engine_plan_for(Engine* e, uint64_t present, bool data_only, const uint8_t** plan) {
   DeviceScope ds(e->device);
   if (!ds.ok()) return RS_ERR_DEVICE;
@@ -1740,6 +1795,18 @@ int rs_reconstruct_batch_out_devmask(rs_ctx* c, const uint8_t* data, size_t data
   DeviceScope ds(e->device);
   return rs::engine_reconstruct_batch_out(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, masks_dev, N, 1,
                                           max_missing, out, out_sp, as_stream(stream));
+}
+
+int rs_reconstruct_batch_out_packed(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                    size_t parity_sp, size_t shard_pitch, size_t S, size_t N, const uint32_t* masks,
+                                    int masks_on_device, uint8_t* out, uint32_t* row_offsets, void* stream) {
+  if (!c || !data || (c->m > 0 && !parity) || !masks || !out || !row_offsets) return RS_ERR_INVALID_ARG;
+  if (N == 0) return RS_OK;
+  Engine* e = engine_for_stream(c, as_stream(stream));
+  if (!e) return RS_ERR_INVALID_ARG;
+  DeviceScope ds(e->device);
+  return rs::engine_reconstruct_batch_packed(e, data, data_sp, parity, parity_sp, shard_pitch, S, N, masks,
+                                             masks_on_device, out, row_offsets, as_stream(stream));
 }
 
 int rs_verify_batch(rs_ctx* c, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,

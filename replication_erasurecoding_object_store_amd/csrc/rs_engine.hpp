@@ -58,6 +58,9 @@ int engine_reconstruct_batch_out(Engine* e, const uint8_t* data, size_t data_sp,
                                  size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
                                  size_t n_masks, int masks_on_device, int max_missing, uint8_t* out, size_t out_sp,
                                  hipStream_t s);
+int engine_reconstruct_batch_packed(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity,
+                                    size_t parity_sp, size_t pitch, size_t S, size_t N, const uint32_t* masks,
+                                    int masks_on_device, uint8_t* out, uint32_t* row_offsets, hipStream_t s);
 int engine_verify_batch(Engine* e, const uint8_t* data, size_t data_sp, const uint8_t* parity, size_t parity_sp,
                         size_t pitch, size_t S, size_t N, uint32_t* bad_dev, hipStream_t s);
 // Device address of the plan for one pattern on this engine (cached; thread-safe):

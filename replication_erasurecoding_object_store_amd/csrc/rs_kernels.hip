@@ -266,6 +266,8 @@ __device__ __forceinline__ uint8_t* slot_ptr(const KernelArgs& a, int k, uint32_
 
 // r-th output of stripe i: in place (its shard slot) or out of place.
 __device__ __forceinline__ uint8_t* out_ptr(const KernelArgs& a, int k, uint32_t stripe, uint32_t r, uint32_t slot) {
+  if (a.out && a.row_offsets)  // packed: the stripe's rows start at its row offset
+    return a.out + (static_cast<uint64_t>(as_const<uint32_t>(a.row_offsets)[stripe]) + r) * a.shard_pitch;
   return a.out ? a.out + static_cast<uint64_t>(stripe) * a.out_sp + static_cast<uint64_t>(r) * a.shard_pitch
                : slot_ptr(a, k, stripe, slot);
 }
@@ -982,16 +984,23 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
     const bool lb = live && inB;      // B lanes are addressed off stripe s0's base
     const uint32_t offD = (lb ? static_cast<uint32_t>(a.data_sp) : 0u) + col * 16u;
     const uint32_t offP = (lb ? static_cast<uint32_t>(a.parity_sp) : 0u) + col * 16u;
-    const uint32_t offO = (lb ? static_cast<uint32_t>(a.out_sp) : 0u) + col * 16u;
+    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P,
+    // or packed at out + (row_offsets[s] + r)*P
+    uint64_t obase = static_cast<uint64_t>(s0) * a.out_sp;
+    uint32_t osp = static_cast<uint32_t>(a.out_sp);
+    if (a.row_offsets) {  // wave-uniform
+      const uint32_t r0 = as_const<uint32_t>(a.row_offsets)[s0];
+      obase = static_cast<uint64_t>(r0) * pitch;
+      osp = straddle ? (as_const<uint32_t>(a.row_offsets)[s0 + 1u] - r0) * pitch : 0u;
+    }
+    const uint32_t offO = (lb ? osp : 0u) + col * 16u;
     const bool fullc = live && colr < a.full_cols;
     const bool part = nb != 0u && live && colr == a.full_cols;
     const auto din = __builtin_amdgcn_make_buffer_rsrc(a.data + static_cast<uint64_t>(s0) * a.data_sp, 0,
                                                        0x7FFFFFFF, 0x00020000);
     const auto pin = __builtin_amdgcn_make_buffer_rsrc(a.parity + static_cast<uint64_t>(s0) * a.parity_sp, 0,
                                                        0x7FFFFFFF, 0x00020000);
-    // out of place: the r-th missing shard of the lane's stripe at out + s*out_sp + r*P
-    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + static_cast<uint64_t>(s0) * a.out_sp, 0,
-                                                        0x7FFFFFFF, 0x00020000);
+    const auto oout = __builtin_amdgcn_make_buffer_rsrc(a.out + obase, 0, 0x7FFFFFFF, 0x00020000);
     for (uint32_t seg = 0; seg < (two ? 2u : 1u); ++seg) {
       const bool sb = seg != 0u;
       const uint8_t* plan = sb ? planB : planA;
@@ -1748,6 +1757,60 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
   void* args[] = {const_cast<KernelArgs*>(&a)};
   if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
   return name;
+}
+
+// Row offsets of a packed out-of-place batch: an exclusive prefix sum of the
+// stripes' erasure counts, by one workgroup of 1024 threads walking the masks in
+// chunks of 16 384 (16 per thread, each thread's in a run), a running total carried
+// from chunk to chunk.  Tiny next to the reconstruct it precedes (one mask word per
+// 64 KiB object); dst[n] = the batch's total row count.  A stripe missing more than
+// max_rows shards (fewer than k present: never rebuilt) takes no rows.
+__global__ __launch_bounds__(1024) void row_offsets_kernel(const uint32_t* __restrict__ masks, uint32_t full,
+                                                           uint32_t max_rows, uint32_t* __restrict__ dst,
+                                                           uint64_t n) {
+  constexpr uint32_t kPer = 16, kChunk = 1024u * kPer;
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  if (tid == 0) carry = 0u;
+  __syncthreads();
+  for (uint64_t base = 0; base < n; base += kChunk) {
+    const uint64_t i0 = base + static_cast<uint64_t>(tid) * kPer;
+    uint32_t cnt[kPer], sum = 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      const uint32_t c = i0 + j < n ? static_cast<uint32_t>(__builtin_popcount(~masks[i0 + j] & full)) : 0u;
+      cnt[j] = c > max_rows ? 0u : c;
+      sum += cnt[j];
+    }
+    // inclusive scan of the threads' sums within the wave, then across the 16 waves
+    uint32_t inc = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t v = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += v;
+    }
+    if (lane == 63u) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t before = carry;
+    for (uint32_t w = 0; w < wid; ++w) before += wsum[w];
+    uint32_t run = before + inc - sum;  // exclusive start of this thread's run
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      if (i0 + j < n) dst[i0 + j] = run;
+      run += cnt[j];
+    }
+    __syncthreads();
+    if (tid == 1023u) carry = run;  // the last thread's run ends the chunk
+    __syncthreads();
+  }
+  if (tid == 0) dst[n] = carry;
+}
+
+bool launch_row_offsets(const uint32_t* masks, uint32_t full, uint32_t max_rows, uint32_t* dst, uint64_t n,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(row_offsets_kernel, dim3(1), dim3(1024), 0, s, masks, full, max_rows, dst, n);
+  return hipGetLastError() == hipSuccess;
 }
 
 // Per-stripe host masks into device memory, read straight from the pinned slot over

@@ -112,6 +112,9 @@ struct KernelArgs {
   const uint64_t* shard_ptrs;      // pointer-table launches: stripe i's shard s at device address
                                    //   shard_ptrs[i*(k+m) + s] (inputs: present shards; outputs:
                                    //   the missing shards' buffers), each S bytes, 16-B aligned
+  const uint32_t* row_offsets;     // packed outputs (out != null): the r-th missing shard of stripe
+                                   //   i at out + (row_offsets[i] + r) * shard_pitch (N+1 entries,
+                                   //   an exclusive prefix sum of the stripes' erasure counts)
 };
 
 // Parity rows the generated bitsliced encode program of (k, m) was derived from
@@ -136,6 +139,11 @@ void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_block
 // n uint32 words from src (pinned host memory the GPU maps, or device memory) to dst
 // (device memory), on s: per-stripe host masks staged by a kernel on the launch stream.
 bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s);
+// dst[i] = sum over j < i of popcount(~masks[j] & full) for i <= n (dst has n + 1 words):
+// the output row of stripe i's first missing shard in a packed batch; a stripe missing
+// more than max_rows counts 0.  One workgroup walks the masks in chunks on s.
+bool launch_row_offsets(const uint32_t* masks, uint32_t full, uint32_t max_rows, uint32_t* dst, uint64_t n,
+                        hipStream_t s);
 // Verify: recompute parity from the data shards (uniform encode plan) and compare
 // with the stored parity; a.bad[i] |= bit r for every mismatching parity shard r.
 // Per-stripe plans (masks -> LUT) over a table of shard addresses instead of a

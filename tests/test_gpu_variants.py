@@ -350,6 +350,60 @@ def test_c_abi_default_rows_end_at_byte_s(k, m, S, bound):
         svc.close()
 
 
+@pytest.mark.parametrize("k,m,S,N", [(10, 4, 6554, 2049), (8, 4, 8192, 2049), (4, 2, 1024, 2049), (10, 4, 413, 2049),
+                                     (6, 3, 1000, 777), (4, 2, 16384, 1025), (4, 2, 100, 40000)])
+@pytest.mark.parametrize("where", ["dev", "host"])
+def test_packed_rows_match_oracle(engines, k, m, S, N, where):
+    """rs_reconstruct_batch_out_packed: stripes missing 0..m shards (scan batches);
+    row_offsets = the exclusive prefix sum of the erasure counts (stripes with < k
+    present take none), stripe i's r-th missing shard at row row_offsets[i] + r,
+    equal to the encoded shard; bytes past each row's 128-B line and rows past the
+    total stay untouched.  N = 40000 walks the scan kernel's 16384-mask chunks."""
+    import torch
+
+    eng = _engine(engines, k, m)
+    t, P = k + m, shard_pitch_for(S)
+    g = torch.Generator(device="cuda").manual_seed(S * 3 + N)
+    data = torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g)
+    parity = torch.empty((N, m, P), dtype=torch.uint8, device="cuda")
+    eng.encode(data, parity, S, N)
+    ref = torch.cat([data, parity], dim=1)[:, :, :S].cpu().numpy()
+    rng = np.random.default_rng(S + N + (where == "dev"))
+    masks = _masks(rng, N, t, 0, m)
+    invalid = [7, 64, 65, N - 1] if where == "dev" else []
+    for i in invalid:  # fewer than k present: reported by rs_sync, no rows
+        masks[i] = (1 << (k - 1)) - 1
+    nmiss = np.array([bin(int(x) ^ ((1 << t) - 1)).count("1") for x in masks])
+    cnt = np.where(nmiss > m, 0, nmiss)
+    want = np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32)
+    out = torch.full((N * m + 2, P), 0xC3, dtype=torch.uint8, device="cuda")
+    roffs = torch.full((N + 1,), -1, dtype=torch.int32, device="cuda")
+    if where == "dev":
+        eng.reconstruct_packed(data, parity, out, roffs, S, N, masks_dev=torch.from_numpy(masks.view(np.int32)).cuda())
+        with pytest.raises(ECError) as ei:
+            eng.sync()
+        assert ei.value.code == _lib.RS_ERR_TOO_FEW_SHARDS
+    else:
+        eng.reconstruct_packed(data, parity, out, roffs, S, N, present_masks=masks)
+    torch.cuda.synchronize()
+    assert np.array_equal(roffs.cpu().numpy().view(np.uint32), want)
+    got = out.cpu().numpy()
+    rows = np.concatenate([want[i] + np.arange(cnt[i]) for i in range(N)]).astype(np.int64)
+    src = np.concatenate([[(i, j) for j in range(t) if not (int(masks[i]) >> j) & 1] if cnt[i] else
+                          np.zeros((0, 2), np.int64) for i in range(N)]).astype(np.int64)
+    assert len(rows) == len(src) == int(want[N])
+    bad = np.nonzero((got[rows, :S] != ref[src[:, 0], src[:, 1]]).any(axis=1))[0]
+    assert len(bad) == 0, rows[bad][:8].tolist()
+    assert (got[int(want[N]):] == 0xC3).all(), "a row past the batch's total was written"
+    assert (got[:, _pad_end(S, P):] == 0xC3).all(), "row padding past the line written"
+    # host masks with a stripe below k: refused before anything runs
+    if where == "host":
+        masks[3] = (1 << (k - 1)) - 1
+        with pytest.raises(ECError) as ei:
+            eng.reconstruct_packed(data, parity, out, roffs, S, N, present_masks=masks)
+        assert ei.value.code == _lib.RS_ERR_TOO_FEW_SHARDS
+
+
 @pytest.mark.parametrize("nbytes", [16, 4080, 4096, 4112, (1 << 20) + 16, 201326592])
 def test_device_copy_exact(engines, nbytes):
     """rs_device_copy (the bench's HBM yardstick): 4 KiB wave tasks whose descriptors

@@ -106,6 +106,14 @@ WORKLOADS = {
     "rs84_64K_recmix_out": (8, 4, 8192, 16384, "recmix_out"),
     "rs84_64K_recmixh_out": (8, 4, 8192, 16384, "recmixh_out"),
     "rs42_64K_recmixh_out": (4, 2, 16384, 16384, "recmixh_out"),
+    # the same scans with packed output rows (rs_reconstruct_batch_out_packed)
+    "rs104_64K_recmixp_out": (10, 4, 6554, 16384, "recmixp_out"),
+    "rs104_64K_recmixph_out": (10, 4, 6554, 16384, "recmixph_out"),
+    "rs84_64K_recmixp_out": (8, 4, 8192, 16384, "recmixp_out"),
+    "rs84_64K_recmixph_out": (8, 4, 8192, 16384, "recmixph_out"),
+    "rs42_64K_recmixp_out": (4, 2, 16384, 16384, "recmixp_out"),
+    "rs42_64K_recmixph_out": (4, 2, 16384, 16384, "recmixph_out"),
+    "rs104_80K_recmixp_out": (10, 4, 8192, 16384, "recmixp_out"),
     # mixed 1..m erasures: no intact stripe (what the intact stripes' holes cost)
     "rs104_64K_recmix1_out": (10, 4, 6554, 16384, "recmix1_out"),
     "rs84_64K_recmix1_out": (8, 4, 8192, 16384, "recmix1_out"),

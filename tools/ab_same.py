@@ -35,6 +35,7 @@ SIGS = {
     "rs_reconstruct_batch_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _vp]),
     "rs_verify_batch": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp]),
     "rs_reconstruct_batch_out_devmask": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _sz, _vp]),
+    "rs_reconstruct_batch_out_packed": (_i, [_vp, _vp, _sz, _vp, _sz, _sz, _sz, _sz, _vp, _i, _vp, _vp, _vp]),
     "rs_last_kernel": (ctypes.c_char_p, [_vp]),
     "rs_set_out_pad_writes": (_i, [_vp, _i]),
     "rs_set_occupancy_cap": (_i, [_vp, _i]),
@@ -49,8 +50,11 @@ class Variant:
         self.env = env or {}  # set around this variant's rs_create (engine-creation knobs)
         self.lib = ctypes.CDLL(path, mode=os.RTLD_LOCAL | os.RTLD_NOW)
         for fn, (res, args) in SIGS.items():
+            if fn == "rs_reconstruct_batch_out_packed" and not hasattr(self.lib, fn):
+                continue  # variants built before the packed entry point
             f = getattr(self.lib, fn)
             f.restype, f.argtypes = res, args
+        self.packed = False  # "+packed": the mixed scans through rs_reconstruct_batch_out_packed
         self.ctx = {}
 
     def ctx_for(self, k, m):
@@ -90,12 +94,17 @@ def main():
     GiB = 1 << 30
     names = args.variants.split(",")
     # "name@c": abx/name.so with rs_set_occupancy_cap(c) (e.g. a compute-free twin at the
-    # occupancy its real kernel's registers allow); "shipped": the in-tree library
+    # occupancy its real kernel's registers allow); "shipped": the in-tree library;
+    # "name+packed": the mixed scans (recmix_out / recmixh_out) with packed output rows,
+    # so "shipped,shipped+packed" pairs the two layouts (their digests differ by layout)
     def variant(n):
         lib, _, cap = n.partition("@")
+        lib, _, opt = lib.partition("+")
         path = (os.path.join(ROOT, "replication_erasurecoding_object_store_amd", "librsgpu.so") if lib == "shipped"
                 else os.path.join(ROOT, "abx", lib + ".so"))
-        return Variant(n, path, int(cap) if cap else None)
+        v = Variant(n, path, int(cap) if cap else None)
+        v.packed = opt == "packed"
+        return v
 
     vs = [variant(n) for n in names]
     print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
@@ -134,7 +143,7 @@ def main():
             mk = np.array([full & ~sum(1 << int(j) for j in rng.choice(t, size=min(4, m), replace=False))
                            for _ in range(N)])
             bound = 0
-        elif mode in ("recmix_out", "recmix1_out", "recmixh_out"):
+        elif mode in ("recmix_out", "recmix1_out", "recmixh_out", "recmixp_out", "recmixph_out"):
             lo = 1 if mode == "recmix1_out" else 0
             mk = np.full(N, full)
             for i, ne in enumerate(rng.integers(lo, m + 1, N)):
@@ -146,10 +155,11 @@ def main():
         else:
             raise SystemExit(f"{wl}: mode {mode} not supported here")
         bad = torch.zeros(N, dtype=torch.int32, device="cuda")
+        roffs = torch.zeros(N + 1, dtype=torch.int32, device="cuda")  # packed modes' row offsets
         alg = alg_bytes(wl)
         if mk is not None:
             mk = mk.astype(np.uint32)
-            if mode in ("recmix_out", "recmix1_out", "recmixh_out"):
+            if mode in ("recmix_out", "recmix1_out", "recmixh_out", "recmixp_out", "recmixph_out"):
                 nmiss = np.array([bin(int(x) ^ full).count("1") for x in mk])
                 alg = int(S * (k * np.count_nonzero(nmiss) + nmiss.sum()))
             md = torch.from_numpy(mk.view(np.int32)).cuda()
@@ -178,6 +188,11 @@ def main():
                 rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
                                                             md.data_ptr(), bound, outs[i % nb].data_ptr(), osp,
                                                             None)
+            elif mode in ("recmixp_out", "recmixph_out") or (v.packed and mode in ("recmix_out", "recmixh_out")):
+                dev = mode in ("recmixp_out", "recmix_out")  # packed rows (rs_reconstruct_batch_out_packed)
+                rc = v.lib.rs_reconstruct_batch_out_packed(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                                                           md.data_ptr() if dev else mh.ctypes.data, 1 if dev else 0,
+                                                           outs[i % nb].data_ptr(), roffs.data_ptr(), None)
             elif mode == "recmixh_out":
                 rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
                                                     mh.ctypes.data, N, 0, outs[i % nb].data_ptr(), m * P, None)
