@@ -291,10 +291,12 @@ class RSWorkload:
         self.eng.reconstruct_out(d, p, self.out_for(i, bound, dense), self.S, self.N,
                                  masks_dev=self.masks1[i % self.nb], max_missing=bound)
 
-    def rec_mix(self, i, host=False):
+    def rec_mix(self, i, host=False, packed=False):
         """0..m erased shards per stripe (seeded, uniform count), no caller bound: a
         scan's mix of intact and damaged stripes.  host: the masks come from host
-        memory (rs_reconstruct_batch_out with per-stripe host masks)."""
+        memory (rs_reconstruct_batch_out with per-stripe host masks).  packed: the
+        missing shards back to back (rs_reconstruct_batch_out_packed, row offsets
+        filled by the call) instead of m-row slots."""
         if not hasattr(self, "masks_mix"):
             rng = np.random.default_rng(0x5EED0003 + 2)
             t = self.k + self.m
@@ -307,7 +309,13 @@ class RSWorkload:
                 self.masks_mix_np.append(mk)
             self.masks_mix = [self.torch.from_numpy(mk.view(np.int32)).cuda() for mk in self.masks_mix_np]
         d, p = self.bufs[i % self.nb]
-        if host:
+        if packed:
+            if not hasattr(self, "roffs"):
+                self.roffs = self.torch.empty(self.N + 1, dtype=self.torch.int32, device="cuda")
+            kw = ({"present_masks": self.masks_mix_np[i % self.nb]} if host else
+                  {"masks_dev": self.masks_mix[i % self.nb]})
+            self.eng.reconstruct_packed(d, p, self.outs[i % self.nb], self.roffs, self.S, self.N, **kw)
+        elif host:
             self.eng.reconstruct_out(d, p, self.outs[i % self.nb], self.S, self.N,
                                      present_masks=self.masks_mix_np[i % self.nb])
         else:
@@ -842,11 +850,11 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             e2.set_parity_pad_writes(False)
         timed("reconstruct2", lambda i: w.rec(i, bound=2), alg["reconstruct"], solo=True)
         timed("reconstruct1", lambda i: w.rec1(i, bound=1), alg["reconstruct1"])
+        # round 5's layout for the same calls: the bounded rows in m-row slots (the
+        # rows past the bound unused in every stripe's slot)
         if mm > 2:
-            # round 5's layout for the same calls: the bounded rows in m-row slots
-            # (rows 1..m-1 of every stripe's slot unused)
             timed("reconstruct2_mslot_out", lambda i: w.rec(i, bound=2, dense=False), alg["reconstruct"])
-            timed("reconstruct1_mslot_out", lambda i: w.rec1(i, bound=1, dense=False), alg["reconstruct1"])
+        timed("reconstruct1_mslot_out", lambda i: w.rec1(i, bound=1, dense=False), alg["reconstruct1"])
         if SS % 128:
             # output rows end on whole 128-B lines by default (round 5); the same legs
             # with exact rows (rs_set_out_pad_writes(0): nothing past S written)
@@ -864,6 +872,9 @@ def kmsweep(torch, rdist, rotate, min_ms=100.0):
             timed("reconstruct1_unbounded", w.rec1, alg["reconstruct1"])
         timed("reconstruct_mixed_unbounded", w.rec_mix, mix)
         timed("reconstruct_mixed_host", lambda i: w.rec_mix(i, host=True), mix)
+        # the same scans with packed output rows (rs_reconstruct_batch_out_packed)
+        timed("reconstruct_mixed_packed", lambda i: w.rec_mix(i, packed=True), mix)
+        timed("reconstruct_mixed_packed_host", lambda i: w.rec_mix(i, host=True, packed=True), mix)
         ent["ok"] = rdist.all_true(w.check())
         ent["kernels"] = kern
         w.close()
