@@ -6,7 +6,9 @@ PMC passes (FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024, MI355X_MICROARCH.md §HBM
 A leg's timed window is the reps + 2 dispatches of its kernel that follow an idle gap
 of >= 2 ms (bench.py idles 3 ms before each window; kernel_ms_events issues two
 warm-up launches, then the timed ones), the first such after the previous leg's
-window.  The timed ones are the last reps.
+window.  The timed ones are the last reps.  The packed device-mask leg's row-offset
+scan kernel (one per reconstruct) is left out of the windows: its bench fraction
+includes the scan, its rocprof average does not.
 
 Usage: python tools/sweep_trace_summary.py gpurun_out/sweep_<tag> <tag>
 """
@@ -21,7 +23,8 @@ SHAPES = {"rs42_64KiB": (4, 2, 16384), "rs84_64KiB": (8, 4, 8192), "rs104_64KiB"
 E_OF = {"encode": None, "encode_parity_pad": None, "reconstruct2": 2, "reconstruct1": 1,
         "reconstruct2_mslot_out": 2, "reconstruct1_mslot_out": 1, "reconstruct2_out_pad": 2, "reconstruct1_out_pad": 1, "reconstruct2_exact_rows": 2, "reconstruct1_exact_rows": 1,
         "reconstruct2_unbounded": 2, "reconstruct1_unbounded": 1,
-        "reconstruct_mixed_unbounded": "mix", "reconstruct_mixed_host": "mix"}
+        "reconstruct_mixed_unbounded": "mix", "reconstruct_mixed_host": "mix",
+        "reconstruct_mixed_packed": "mix", "reconstruct_mixed_packed_host": "mix"}
 CONFIG3 = {"rec1_per_stripe_out": 1, "rec_0_1_uniform_out": 2, "rec_0_4_uniform_out": 2,
            "rec_4_5_uniform_out": 2, "soa_encode": 2}
 
@@ -58,7 +61,7 @@ def windows(trace_csv, want):
     """Dispatches of each leg's timed window: reps + 2 dispatches of the leg's kernel
     starting right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each
     window); the first two are kernel_ms_events' warm-up launches."""
-    ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"]]
+    ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"] and "row_offsets_kernel" not in r["Kernel_Name"]]
     ds.sort(key=lambda r: int(r["Start_Timestamp"]))
     res, pos = [], 0
     for label, kern, reps, alg, frac in want:
