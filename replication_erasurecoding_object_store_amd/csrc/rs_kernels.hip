@@ -1581,17 +1581,67 @@ static bool raise_lds_limit(const void* fn) {
 // profiles/r05c_ab_same_occ.log, caps 3 / 5 / 6 ran as 2 / 4 / 5).  kLdsRefused when
 // the kernel's LDS limit cannot be raised for the cap.
 constexpr size_t kLdsRefused = ~size_t(0);
-static size_t occ_lds(const void* fn, uint32_t cap) {
+static size_t occ_lds(const void* fn, uint32_t cap, uint32_t wg_per_wave_slot = 1) {
   if (cap == 0) return 0;
-  const size_t lds = ((kLdsPerCu / cap + kLdsPerCu / (cap + 1)) / 2) & ~size_t(1023);
+  cap *= wg_per_wave_slot;  // workgroups of fewer than 4 waves: more of them per CU
+  const size_t lds = ((kLdsPerCu / cap + kLdsPerCu / (cap + 1)) / 2) & ~size_t(wg_per_wave_slot == 1 ? 1023 : 255);
   if (lds > 65536 && !raise_lds_limit(fn)) return kLdsRefused;  // above the default dynamic-LDS limit
   return lds;
 }
 
-// hipLaunchKernel with an occupancy reservation; false if it cannot be honoured.
-static bool launch_capped(const void* fn, dim3 grid, void** args, size_t lds, hipStream_t s) {
+// Waves per workgroup of each launch: 4 (256 threads, one wave per SIMD) or 1 (64
+// threads).  Every kernel here is wave-independent (no LDS, no barriers), so the
+// choice only changes how the dispatcher refills a CU: a 4-wave workgroup frees its
+// slots when its slowest wave ends, a 1-wave workgroup as soon as it ends -- which
+// pays when the waves of one workgroup do unequal work (the per-stripe erasure counts
+// of a mixed scan, the two passes of a task straddling two stripes, stores draining
+// behind loads).  Same-process A/B per class (round 6, profiles/r06k_ab_wpw.log, 4
+// rounds; points of 8 TB/s, one wave against four):
+//   flat E = m reconstruct (scans)      RS(10+4) 64 KiB mixed 0..4 +9.2 (host masks
+//                                       +8.4, r06k_ab_wg64.log), 4-erasure +6.8,
+//                                       unbounded 2-erasure +1.8            -> 1
+//   flat E <= 2                         RS(10+4) bounded 1 / 2: -1.8 / -5.7   -> 4
+//   stripe-aligned per-stripe E = m     RS(8+4) mixed +4.3, unbounded 2-erasure +2.0;
+//                                       RS(8+4) in place -1.0, RS(6+3) mixed -1.1
+//                                                   -> 1 out of place for k >= 8
+//   stripe-aligned per-stripe E <= 2    RS(8+4) bounded 1 / 2 +5.1 / +1.7, RS(4+2)
+//                                       4 KiB bounded 2 (the headline) +1.2, 1 +1.6,
+//                                       16 KiB 1 +4.8; stripes of > 4 tasks (RS(4+2)
+//                                       64 KiB / 1 MiB, r06l_ab_pslong.log): 1-erasure
+//                                       +2.6 / +3.4, in place +2.0 / +0.8, 2-erasure
+//                                       out of place -0.3 to -1.4   -> 1 but for those
+//   uniform (encode, one-pattern)       RS(4+2) encode 4 / 64 KiB +1.0 / +4.2,
+//                                       one-pattern out of place / in place +1.2 /
+//                                       +3.5; RS(6+3) encode -2.4     -> 1 for k <= 4
+//   bitsliced encode                    RS(8+4) +1.7, RS(10+4) -1.2 -> 1 for (8, 4)
+//   verify                              RS(10+4) -6.5, RS(4+2) +0.4            -> 4
+// RS_WPW_FORCE=4 (or 1) builds every launch with that many (A/B builds).
+enum class Wpw { kFlatEm, kFlat, kPsEm, kPs, kUni, kBs, kVerify };
+#ifndef RS_WPW_FORCE
+#define RS_WPW_FORCE 0
+#endif
+static uint32_t wpw_for(Wpw cls, const KernelArgs& a) {
+  if (RS_WPW_FORCE) return RS_WPW_FORCE;
+  switch (cls) {
+    case Wpw::kFlatEm: return 1u;
+    case Wpw::kPsEm: return a.out && a.k >= 8 ? 1u : 4u;
+    case Wpw::kPs:
+      return a.k >= 8 || a.blocks_per_stripe <= 4u || a.max_out == 1u || !a.out ? 1u : 4u;
+    case Wpw::kUni: return a.k <= 4 ? 1u : 4u;
+    case Wpw::kBs: return a.k == 8 && a.m == 4 ? 1u : 4u;
+    default: return 4u;
+  }
+}
+
+// hipLaunchKernel of `grid` 4-wave workgroups' worth of waves in workgroups of wpw
+// waves, at most `cap` waves per SIMD (0: uncapped; kLdsRefused-style failure if the
+// reservation cannot be honoured).  false if the launch fails.
+static bool launch_capped(const void* fn, dim3 grid, void** args, uint32_t cap, hipStream_t s, uint32_t wpw = 4) {
+  const size_t lds = occ_lds(fn, cap, 4u / wpw);
   if (lds == kLdsRefused) return false;
-  return hipLaunchKernel(fn, grid, dim3(256), args, lds, s) == hipSuccess;
+  uint64_t g = static_cast<uint64_t>(grid.x) * (4u / wpw);
+  if (g > 0x7FFFFFFFull) g = 0x7FFFFFFFull - (0x7FFFFFFFull % (4u / wpw));  // kernels grid-stride past it
+  return hipLaunchKernel(fn, dim3(static_cast<uint32_t>(g)), dim3(64u * wpw), args, lds, s) == hipSuccess;
 }
 
 // One launch over columns [0, a.shard_len) of every shard (a.shard_len < 2 GiB:
@@ -1619,7 +1669,7 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
       // against a grid-stride loop over 6 workgroups per CU)
       const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
-      if (!launch_capped(fn, grid, args, occ_lds(fn, cap_of(RS_OCC_CAP_BS)), s)) return nullptr;
+      if (!launch_capped(fn, grid, args, cap_of(RS_OCC_CAP_BS), s, wpw_for(Wpw::kBs, a))) return nullptr;
       return name;
     }
   }
@@ -1637,7 +1687,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       const dim3 grid = !blocks_per_cu ? full_grid(waves)
                                                                          : grid_for(waves, bpc, cu_count);
       const uint32_t cap = e == 1 ? RS_OCC_CAP_FLAT_E1 : e == 2 ? RS_OCC_CAP_FLAT_E2 : RS_OCC_CAP_FLAT_EM;
-      if (!launch_capped(ff, grid, args, occ_lds(ff, cap_of(cap)), s)) return nullptr;
+      if (!launch_capped(ff, grid, args, cap_of(cap), s, wpw_for(e > 2 ? Wpw::kFlatEm : Wpw::kFlat, a)))
+        return nullptr;
       return name;
     }
   }
@@ -1665,7 +1716,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   uint32_t dcap = RS_OCC_CAP_APPLY;
   if (dcap == 0u && per_stripe && !generic && e <= 2)
     dcap = a.blocks_per_stripe >= 2u ? 4u : (e == 1 ? 5u : 0u);
-  if (!launch_capped(fn, grid, args, generic ? 0 : occ_lds(fn, cap_of(dcap)), s)) return nullptr;
+  const uint32_t wpw = generic ? 4u : wpw_for(!per_stripe ? Wpw::kUni : e > 2 ? Wpw::kPsEm : Wpw::kPs, a);
+  if (!launch_capped(fn, grid, args, generic ? 0u : cap_of(dcap), s, wpw)) return nullptr;
   return name;
 }
 
@@ -1751,11 +1803,9 @@ const char* launch_verify(const KernelArgs& a, uint32_t blocks_per_cu, uint32_t 
     }
   }
   if (waves == 0) return name;
-  const uint64_t cap = static_cast<uint64_t>(cu_count) * blocks_per_cu;
-  const uint64_t need = (waves + 3) / 4;
-  const uint32_t grid = static_cast<uint32_t>(need < cap ? need : cap);
   void* args[] = {const_cast<KernelArgs*>(&a)};
-  if (hipLaunchKernel(fn, dim3(grid > 0 ? grid : 1), dim3(256), args, 0, s) != hipSuccess) return nullptr;
+  if (!launch_capped(fn, grid_for(waves, blocks_per_cu, cu_count), args, 0u, s, wpw_for(Wpw::kVerify, a)))
+    return nullptr;
   return name;
 }
 
