@@ -1669,7 +1669,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
       // against a grid-stride loop over 6 workgroups per CU)
       const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
-      if (!launch_capped(fn, grid, args, cap_of(RS_OCC_CAP_BS), s, wpw_for(Wpw::kBs, a))) return nullptr;
+      // RS(8+4) in one-wave workgroups: 3 waves per SIMD, +1.1 points over its register
+      // limit (round 6, profiles/r06m_ab_caps.log)
+      const uint32_t bcap = RS_OCC_CAP_BS == 0 && a.k == 8 && a.m == 4 ? 3u : RS_OCC_CAP_BS;
+      if (!launch_capped(fn, grid, args, cap_of(bcap), s, wpw_for(Wpw::kBs, a))) return nullptr;
       return name;
     }
   }
@@ -1715,7 +1718,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   }
   uint32_t dcap = RS_OCC_CAP_APPLY;
   if (dcap == 0u && per_stripe && !generic && e <= 2)
-    dcap = a.blocks_per_stripe >= 2u ? 4u : (e == 1 ? 5u : 0u);
+    dcap = a.k >= 8 && e == 1 ? 3u : a.blocks_per_stripe >= 2u ? 4u : (e == 1 ? 5u : 0u);  // k >= 8, e = 1:
+        // 3 in one-wave workgroups, RS(8+4) 64 KiB bounded 1-erasure +1.6 (r06m_ab_caps.log)
   const uint32_t wpw = generic ? 4u : wpw_for(!per_stripe ? Wpw::kUni : e > 2 ? Wpw::kPsEm : Wpw::kPs, a);
   if (!launch_capped(fn, grid, args, generic ? 0u : cap_of(dcap), s, wpw)) return nullptr;
   return name;
