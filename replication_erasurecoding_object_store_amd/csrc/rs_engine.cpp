@@ -839,9 +839,11 @@ struct UploadGuard {
   Engine* e = nullptr;
   UploadSlot* u = nullptr;
   hipStream_t s = nullptr;
+  bool ev_set = false;  // the kernel launch itself updated u->done (rs::set_stop_event)
   ~UploadGuard() {
     if (!u) return;
-    const bool rec = hipEventRecord(u->done, s) == hipSuccess;
+    rs::set_stop_event(nullptr, nullptr);
+    const bool rec = ev_set || hipEventRecord(u->done, s) == hipSuccess;
     std::lock_guard<std::mutex> g(e->upload_mu);
     u->used = rec;
     if (!rec) (void)hipStreamSynchronize(s);  // no event: make the slot safe the slow way
@@ -902,6 +904,10 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   if (extra_n && !rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev) + n, extra_dst, extra_n, s))
     return RS_ERR_DEVICE;
   *dev = static_cast<const uint32_t*>(u->dev.p);
+  // the reading kernel's own completion updates the slot's event (no marker packet
+  // after it: host-mask launches +1.0 / +2.6 / +2.0 points for RS(10+4) / RS(8+4) /
+  // RS(4+2) 64 KiB mixed scans without the marker, profiles/r06n_ab_hostdiag.log)
+  rs::set_stop_event(u->done, &g->ev_set);
   return RS_OK;
 }
 

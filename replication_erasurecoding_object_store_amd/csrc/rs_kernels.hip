@@ -37,6 +37,7 @@
 // The flat-task kernels (bitsliced encode, scrub, per-stripe out-of-place
 // reconstruct) instead cut the batch's columns -- each stripe rounded up to whole
 // 128-B lines -- into tasks that may straddle two stripes (round 2).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -1633,6 +1634,20 @@ static uint32_t wpw_for(Wpw cls, const KernelArgs& a) {
   }
 }
 
+// Stop event of the next launches on this thread (set_stop_event): the kernel's own
+// completion signal updates it (hipExtLaunchKernel), instead of a marker packet the
+// stream processes after the kernel.
+#ifndef RS_STOP_EVENT_LAUNCH
+#define RS_STOP_EVENT_LAUNCH 1
+#endif
+static thread_local hipEvent_t t_stop_event = nullptr;
+static thread_local bool* t_stop_used = nullptr;
+
+void set_stop_event(hipEvent_t ev, bool* used) {
+  t_stop_event = RS_STOP_EVENT_LAUNCH ? ev : nullptr;
+  t_stop_used = RS_STOP_EVENT_LAUNCH ? used : nullptr;
+}
+
 // hipLaunchKernel of `grid` 4-wave workgroups' worth of waves in workgroups of wpw
 // waves, at most `cap` waves per SIMD (0: uncapped; kLdsRefused-style failure if the
 // reservation cannot be honoured).  false if the launch fails.
@@ -1641,6 +1656,13 @@ static bool launch_capped(const void* fn, dim3 grid, void** args, uint32_t cap, 
   if (lds == kLdsRefused) return false;
   uint64_t g = static_cast<uint64_t>(grid.x) * (4u / wpw);
   if (g > 0x7FFFFFFFull) g = 0x7FFFFFFFull - (0x7FFFFFFFull % (4u / wpw));  // kernels grid-stride past it
+  if (t_stop_event) {
+    if (hipExtLaunchKernel(fn, dim3(static_cast<uint32_t>(g)), dim3(64u * wpw), args, lds, s, nullptr, t_stop_event,
+                           0) != hipSuccess)
+      return false;
+    *t_stop_used = true;
+    return true;
+  }
   return hipLaunchKernel(fn, dim3(static_cast<uint32_t>(g)), dim3(64u * wpw), args, lds, s) == hipSuccess;
 }
 

@@ -136,6 +136,10 @@ uint32_t default_blocks_per_cu(int k, int e);
 const char* launch_apply(const KernelArgs& a, int e, bool per_stripe, uint32_t blocks_per_cu,
                          uint32_t cu_count, hipStream_t s, int occ_cap = -1);
 void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_blocks, hipStream_t s);
+// The main kernel launches that follow on this thread also update `ev` as they
+// complete (the kernel's own completion signal, hipExtLaunchKernel) and set *used;
+// set_stop_event(nullptr, nullptr) ends it.  Launches that bypass it leave *used alone.
+void set_stop_event(hipEvent_t ev, bool* used);
 // n uint32 words from src (pinned host memory the GPU maps, or device memory) to dst
 // (device memory), on s: per-stripe host masks staged by a kernel on the launch stream.
 bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s);
