@@ -573,8 +573,13 @@ uint32_t* status_word(Engine* e, hipStream_t s) {
     if (!e->status_chunks[idx / kStatusChunk]) {
       auto ch = std::make_unique<StatusChunk>();
       ch->host.numa = e->numa;
+      // zeroed to completion before any kernel can use a word of it: hipMemset may
+      // return before the fill has run, and a kernel on a non-blocking stream does not
+      // wait for the null stream -- its deferred error then landed before the zeroing
+      // and was lost (a fresh process's first per-stripe launch, round 6)
       if (ch->dev.ensure(kStatusChunk * 4) || ch->host.ensure(kStatusChunk * 4) ||
-          hipMemset(ch->dev.p, 0, kStatusChunk * 4) != hipSuccess) {
+          hipMemsetAsync(ch->dev.p, 0, kStatusChunk * 4, nullptr) != hipSuccess ||
+          hipStreamSynchronize(nullptr) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
       }
