@@ -509,7 +509,9 @@ __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void 
       }
     } else {
       // E <= 2 per-stripe launches run one task per wave (a full grid), so a task of an
-      // intact (or skipped) stripe ends its wave here: no loads, no stores.  RS(4+2)
+      // intact (or skipped) stripe ends its wave here: no loads, no stores.  (Rejected,
+      // round 6, profiles/r06p_ab_mslots.log: the input slots taken from the mask so
+      // the loads issue before the LUT -> plan chain returns -- level, -0.6 to +0.7.)  RS(4+2)
       // device masks without a bound are this kernel (E = M = 2), and a scan's mixed
       // batch had every intact stripe read for nothing.
       if constexpr (PER_STRIPE) {

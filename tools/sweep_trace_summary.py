@@ -8,7 +8,9 @@ of >= 2 ms (bench.py idles 3 ms before each window; kernel_ms_events issues two
 warm-up launches, then the timed ones), the first such after the previous leg's
 window.  The timed ones are the last reps.  The packed device-mask leg's row-offset
 scan kernel (one per reconstruct) is left out of the windows: its bench fraction
-includes the scan, its rocprof average does not.
+includes the scan, its rocprof average does not; likewise the host-mask legs' mask
+copy kernel (round 6: the masks reach the device through a copy kernel on the launch
+stream).
 
 Usage: python tools/sweep_trace_summary.py gpurun_out/sweep_<tag> <tag>
 """
@@ -61,7 +63,8 @@ def windows(trace_csv, want):
     """Dispatches of each leg's timed window: reps + 2 dispatches of the leg's kernel
     starting right after an idle gap of >= 2 ms (bench.py sleeps 3 ms before each
     window); the first two are kernel_ms_events' warm-up launches."""
-    ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"] and "row_offsets_kernel" not in r["Kernel_Name"]]
+    aux = ("row_offsets_kernel", "words_copy_kernel")  # a call's helper launches, not legs
+    ds = [r for r in rows(trace_csv) if "rs::" in r["Kernel_Name"] and not any(x in r["Kernel_Name"] for x in aux)]
     ds.sort(key=lambda r: int(r["Start_Timestamp"]))
     res, pos = [], 0
     for label, kern, reps, alg, frac in want:
