@@ -554,7 +554,9 @@ __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void 
       // 2-erasure 62.9-65.1 -> 65.9-67.1 %, 4-erasure 47.5-48.7 -> 57.3-57.9 %
       // (profiles/r02c_ab_ix_rows.log).  Input-outer passes of <= 2 rows instead
       // (round 4) lost 9-10 points on 4-erasure and mixed batches
-      // (profiles/r04g_ab_twopass.log, `HISTORY.md` §A.5).
+      // (profiles/r04g_ab_twopass.log, `HISTORY.md` §A.5); input-outer per row count,
+      // as the flat kernel does since round 6, lost 8-14 here (166 VGPRs, 252 SGPR
+      // spills in this grid-stride loop, profiles/r06r_ab_psinout.log).
       Idx3 ix[K][4];
 #pragma unroll
       for (int c = 0; c < K; ++c)
@@ -1040,40 +1042,33 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
         gf_rows<K, M, 0, E>(plan, x, y);
         emit(std::integral_constant<int, E>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
       } else {
-        // E > 2 (device masks without a bound, mixed batches): every input split into
-        // chunk indices once, then only the rows the stripe misses, one at a time, in a
-        // wave-uniform branch per row count; stripes missing 3+ shards store each row as
-        // soon as it is computed.  (Rejected, round 6, profiles/r06b_ab_perm.log: the
-        // inputs folded into all of a stripe's rows as they arrive -- mixed +1.1 to
-        // +1.6, 2-erasure -1.5 to -2.7 points; the tasks scattered over the waves so a
-        // CU holds many stripes' erasure counts at once -- -5 to -12; the survivors of
-        // a task 512-4096 tasks ahead fetched into L2 by LDS-DMA loads while the own
-        // inputs load, -15 to -22, profiles/r06h_ab_prefetch.log.)
-        Idx3 ix[K][4];
-#pragma unroll
-        for (int c = 0; c < K; ++c)
-#pragma unroll
-          for (int d = 0; d < 4; ++d) ix[c][d] = split3(x[c][d]);
+        // E > 2 (device masks without a bound, mixed batches): input-outer over only the
+        // rows the stripe misses, one specialisation per row count, in wave-uniform
+        // branches (round 6, profiles/r06r_ab_inout.log, same process under one-wave
+        // workgroups: RS(10+4) 64 KiB mixed 0..4 +1.8, 4-erasure +2.2, unbounded
+        // 2-erasure +1.9, 1-erasure -0.5, 80 KiB mixed +1.8 points against round 5's
+        // chunk-index array computed once and read per row -- 144 VGPRs instead of 165;
+        // forced down to 4 waves per SIMD (128 VGPRs, scratch spills) it lost 10).
+        // (Rejected, round 6: the tasks scattered over the waves so a CU holds many
+        // stripes' erasure counts at once -- -5 to -12, profiles/r06b_ab_perm.log; the
+        // survivors of a task 512-4096 tasks ahead fetched into L2 by LDS-DMA loads
+        // while the own inputs load, -15 to -22, profiles/r06h_ab_prefetch.log.)
         if (nout <= 1u) {
           u32x4 y[1];
-          y[0] = gf_row_ix<K, M>(plan, ix, 0);
+          gf_rows<K, M, 0, 1>(plan, x, y);
           emit(std::integral_constant<int, 1>{}, std::integral_constant<int, kCpolFlatPath1>{}, y);
         } else if (nout == 2u) {
           u32x4 y[2];
-          y[0] = gf_row_ix<K, M>(plan, ix, 0);
-          y[1] = gf_row_ix<K, M>(plan, ix, 1);
+          gf_rows<K, M, 0, 2>(plan, x, y);
           emit(std::integral_constant<int, 2>{}, std::integral_constant<int, path_cpol<K, E, 2>()>{}, y);
-        } else {
-          constexpr int CPOL = out_cpol<K, E>();
-          const bool anypart = __builtin_amdgcn_ballot_w64(part) != 0u;  // wave-uniform
-#pragma unroll
-          for (int r = 0; r < E; ++r) {
-            if (static_cast<uint32_t>(r) < nout) {
-              const u32x4 yr = gf_row_ix<K, M>(plan, ix, r);
-              __builtin_amdgcn_raw_buffer_store_b128(yr, oout, fullc && mine ? offO : kDropOffset, r * pitch, CPOL);
-              if (anypart) store_part_rsrc<CPOL>(oout, offO, r * pitch, part && mine, yr, nb);
-            }
-          }
+        } else if (E < 4 || nout == 3u) {
+          u32x4 y[3];
+          gf_rows<K, M, 0, 3>(plan, x, y);
+          emit(std::integral_constant<int, 3>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
+        } else if constexpr (E >= 4) {
+          u32x4 y[4];
+          gf_rows<K, M, 0, 4>(plan, x, y);
+          emit(std::integral_constant<int, 4>{}, std::integral_constant<int, out_cpol<K, E>()>{}, y);
         }
       }
     }
