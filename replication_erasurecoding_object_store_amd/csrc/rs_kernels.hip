@@ -1688,9 +1688,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       // 64 KiB encode RS(8+4) 74.4 -> 80.3 %, RS(10+4) 68.0 -> 76.3 % of 8 TB/s
       // against a grid-stride loop over 6 workgroups per CU)
       const dim3 grid = blocks_per_cu ? grid_for(waves, blocks_per_cu, cu_count) : full_grid(waves);
-      // RS(8+4) in one-wave workgroups: 3 waves per SIMD, +1.1 points over its register
-      // limit (round 6, profiles/r06m_ab_caps.log)
-      const uint32_t bcap = RS_OCC_CAP_BS == 0 && a.k == 8 && a.m == 4 ? 3u : RS_OCC_CAP_BS;
+      // 3 waves per SIMD over the register limit (round 6): RS(8+4) in one-wave
+      // workgroups +1.1 points (profiles/r06m_ab_caps.log), RS(10+4) +4.3 / +2.7 at
+      // 64 / 80 KiB objects (profiles/r06t_ab_caps2.log)
+      const uint32_t bcap = RS_OCC_CAP_BS == 0 ? 3u : RS_OCC_CAP_BS;
       if (!launch_capped(fn, grid, args, cap_of(bcap), s, wpw_for(Wpw::kBs, a))) return nullptr;
       return name;
     }
