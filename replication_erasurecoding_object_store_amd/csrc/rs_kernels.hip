@@ -580,7 +580,18 @@ __global__ __launch_bounds__(256, (K <= 8 && E <= 2) ? kApplyMinWaves : 1) void 
       }
     } else if constexpr (kDefer) {
       flush();  // the previous task's stores, behind this task's loads
-      gf_rows<K, M, 0, E>(plan, x, y);
+      if (E == 2 && n_out <= 1u) {
+        // wave-uniform: a 1-erasure stripe of a scan computes one row, not two (round
+        // 6, profiles/r06u_ab_nout1.log: RS(4+2) mixed 0..2 erasures at 4 KiB / 64 KiB
+        // / 1 MiB +2.0 / +2.7 / +1.3 points, host masks +2.2; the same branch in the
+        // k >= 8 kernels cost RS(8+4) bounded 2-erasure 1.9)
+        u32x4 y1[1];
+        gf_rows<K, M, 0, 1>(plan, x, y1);
+#pragma unroll
+        for (int r = 0; r < E; ++r) y[r] = y1[0];
+      } else {
+        gf_rows<K, M, 0, E>(plan, x, y);
+      }
       const bool part = col == a.full_cols;
 #pragma unroll
       for (int r = 0; r < E; ++r) {
