@@ -1737,7 +1737,10 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
   uint32_t bpc = blocks_per_cu;
   if (!bpc) bpc = (per_stripe && !generic && e > 2) ? kEmBlocksPerCu : default_blocks_per_cu(a.k, e);
   dim3 grid = grid_for(waves, bpc, cu_count);
-  if (!blocks_per_cu && !generic && !(per_stripe && e > 2)) {
+  // (per-stripe E = M for k < 8 too, round 6, profiles/r06v_ab_emfull.log: RS(6+3)
+  // mixed / unbounded 2-erasure +2.1 / +2.3 points under one-wave workgroups; RS(8+4)
+  // keeps the capped grid: mixed -1.4, 1-erasure -2.2 with a full one)
+  if (!blocks_per_cu && !generic && (a.k < 8 || !(per_stripe && e > 2))) {
     // The specialised E <= 2 and encode kernels run one task per wave: a grid over
     // every task instead of a grid-stride loop over 2 workgroups per CU (round 4,
     // profiles/r04zf_bpc_bounded.log, >= 100 ms per point, 3 rounds): RS(4+2) 4 KiB
