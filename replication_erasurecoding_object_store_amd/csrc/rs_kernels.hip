@@ -1621,7 +1621,11 @@ static size_t occ_lds(const void* fn, uint32_t cap, uint32_t wg_per_wave_slot = 
 //                                       out of place -0.3 to -1.4   -> 1 but for those
 //   uniform (encode, one-pattern)       RS(4+2) encode 4 / 64 KiB +1.0 / +4.2,
 //                                       one-pattern out of place / in place +1.2 /
-//                                       +3.5; RS(6+3) encode -2.4     -> 1 for k <= 4
+//                                       +3.5; RS(6+3) encode -2.4; one-pattern
+//                                       reconstructs (r06x_ab_uni.log) RS(10+4)
+//                                       +3.4 / +2.6, RS(6+3) +2.7 / +3.6, RS(8+4)
+//                                       -0.6 / 0   -> 1 for k <= 4, and for one-pattern
+//                                       reconstructs but RS(8+4)'s
 //   bitsliced encode                    RS(8+4) +1.7, RS(10+4) -1.2 -> 1 for (8, 4)
 //   verify                              RS(10+4) -6.5, RS(4+2) +0.4            -> 4
 // RS_WPW_FORCE=4 (or 1) builds every launch with that many (A/B builds).
@@ -1636,7 +1640,7 @@ static uint32_t wpw_for(Wpw cls, const KernelArgs& a) {
     case Wpw::kPsEm: return a.out && a.k >= 8 ? 1u : 4u;
     case Wpw::kPs:
       return a.k >= 8 || a.blocks_per_stripe <= 4u || a.max_out == 1u || !a.out ? 1u : 4u;
-    case Wpw::kUni: return a.k <= 4 ? 1u : 4u;
+    case Wpw::kUni: return a.k <= 4 || (!a.data_inputs && a.k != 8) ? 1u : 4u;
     case Wpw::kBs: return a.k == 8 && a.m == 4 ? 1u : 4u;
     default: return 4u;
   }
