@@ -15,6 +15,8 @@ stripe gaps, present shards, unused output rows, output padding past the 128-B l
 Reference semantics: internal/ec/ec.go:54-61 (Encode / Reconstruct), klauspost
 v1.12.1 reedsolomon.go (first-K survivors, every missing shard filled, Verify).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -28,7 +30,7 @@ CODES = [(4, 2), (8, 4), (10, 4), (6, 3), (2, 1), (3, 3), (5, 2), (12, 4), (7, 5
 LENGTHS = [1, 7, 15, 16, 17, 100, 413, 1000, 1023, 1024, 1025, 4095, 4096, 6554, 8192, 8205, 9000]
 OPS = ["encode", "rec_one", "rec_host", "rec_dev", "out_host", "out_dev", "out_bound", "verify"]
 SENT = 0xA5
-N_CASES = 256
+N_CASES = int(os.environ.get("RSGPU_FUZZ_CASES", "256"))  # more for a soak run
 MAX_BYTES = 3 << 20  # user bytes per case: keeps the index arithmetic small
 
 
