@@ -1033,10 +1033,32 @@ __global__ __launch_bounds__(256) void apply_flat_seg_kernel(const KernelArgs a)
                                             : bload16(pin, oP, (s - static_cast<uint32_t>(K)) * pitch);
       }
       const uint32_t nl = mine ? nout : 0u;
+      const uint32_t miss = ~(sb ? mB : mA) & full;  // in place: the rows' own slots
       // stores rows [0, NR) with cache policy CPOL, dropped per lane past its stripe's outputs
       auto emit = [&](auto nr_tag, auto cpol_tag, const auto& yy) {
         constexpr int NR = decltype(nr_tag)::value;
         constexpr int CPOL = decltype(cpol_tag)::value;
+        if (!a.out) {
+          // in place (round 6): row r into the stripe's r-th missing slot, through the
+          // inputs' own descriptors (RS(10+4) 80 KiB objects, per-stripe device masks,
+          // +3.9 points over the stripe-aligned kernel; at 64 KiB, where tasks straddle
+          // stripes, -0.9, so ragged in-place batches stay stripe-aligned,
+          // profiles/r06ac_ab_inplace.log)
+          uint32_t mb = miss;
+          const bool anyp = __builtin_amdgcn_ballot_w64(part) != 0u;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+            const uint32_t sl = pop_low(mb);
+            const bool isd = sl < static_cast<uint32_t>(K);
+            const uint32_t so = (isd ? sl : sl - static_cast<uint32_t>(K)) * pitch;
+            const uint32_t vo = isd ? oD : oP;
+            __builtin_amdgcn_raw_buffer_store_b128(yy[r], isd ? din : pin,
+                                                   fullc && static_cast<uint32_t>(r) < nl ? vo : kDropOffset, so,
+                                                   CPOL);
+            if (anyp) store_part_rsrc<CPOL>(isd ? din : pin, vo, so, part && static_cast<uint32_t>(r) < nl, yy[r], nb);
+          }
+          return;
+        }
 #pragma unroll
         for (int r = 0; r < NR; ++r)
           __builtin_amdgcn_raw_buffer_store_b128(yy[r], oout,
@@ -1711,7 +1733,8 @@ static const char* launch_window(const KernelArgs& a, int e, bool per_stripe, ui
       return name;
     }
   }
-  if (per_stripe && !generic && a.out && cols >= 64u && (cols % 64u != 0u || (a.k == 10 && e >= 2)) &&
+  if (per_stripe && !generic && (a.out || cols % 64u == 0u) && cols >= 64u &&
+      (cols % 64u != 0u || (a.k == 10 && e >= 2)) &&
       a.data_sp + span < (1ull << 31) &&
       a.parity_sp + span < (1ull << 31) && a.out_sp + span < (1ull << 31)) {
     // ragged shard lengths: per-stripe reconstruct over flat 64-column tasks
