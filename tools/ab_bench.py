@@ -55,6 +55,13 @@ WORKLOADS = {
     "rs104_64K_rec2pb_out": (10, 4, 6554, 16384, "rec2pb_out"),
     "rs84_64K_rec1pb_out": (8, 4, 8192, 16384, "rec1pb_out"),
     "rs84_64K_rec2pb_out": (8, 4, 8192, 16384, "rec2pb_out"),
+    # the same bounded 2-erasure calls with ONE pattern on every stripe (data 0 and 1
+    # lost), still through per-stripe device masks: the access pattern of a one-pattern
+    # batch on the per-stripe kernels
+    "rs104_64K_rec2sb_out": (10, 4, 6554, 16384, "rec2sb_out"),
+    "rs104_80K_rec2sb_out": (10, 4, 8192, 16384, "rec2sb_out"),
+    "rs84_64K_rec2sb_out": (8, 4, 8192, 16384, "rec2sb_out"),
+    "rs42_64K_rec2sb_out": (4, 2, 16384, 16384, "rec2sb_out"),
     "rs84_64K_rec1p_out": (8, 4, 8192, 16384, "rec1p_out"),
     "rs42_4K_rec04u_out": (4, 2, 1024, 65536, "rec04u_out"),
     "rs42_4K_rec04p_out": (4, 2, 1024, 65536, "rec04p_out"),    # devmask, all stripes miss {0,4}

@@ -119,7 +119,7 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1)
         bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
                  torch.empty((N, m, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
-        out_rows = {"rec1pb_out": 1, "rec2pb_out": 2}.get(mode, m) if layout else m
+        out_rows = {"rec1pb_out": 1, "rec2pb_out": 2, "rec2sb_out": 2}.get(mode, m) if layout else m
         osp = out_rows * P + (256 if layout == "densepad" else 0)
         outs = [torch.empty((N, osp), dtype=torch.uint8, device="cuda") for _ in range(nb)]
         rng = np.random.default_rng(3)
@@ -132,6 +132,9 @@ def main():
             bound = 0
         elif mode == "ver":
             mk, bound = None, 0
+        elif mode == "rec2sb_out":  # one pattern on every stripe, per-stripe device masks, bound 2
+            mk = np.full(N, full & ~0b11)
+            bound = 2
         elif mode in ("rec2pb_out", "rec2p_out", "rec2p"):
             import itertools
 
