@@ -110,16 +110,22 @@ def main():
     print(f"variants (one process): {names}; rounds {args.rounds}; >= {args.min_ms} ms per point", flush=True)
     for wl in args.workloads.split(","):
         # "<workload>@dense": bounded calls write `bound` rows per stripe back to back;
-        # "@densepad": the same with the out stripe pitch 256 B longer; default: m-row slots
+        # "@densepad": the same with the out stripe pitch 256 B longer; default: m-row slots;
+        # "@spad" / "@densespad": the input stripe pitches 256 B longer (below)
         wl, _, layout = wl.partition("@")
         k, m, S, N, mode = WORKLOADS[wl]
         t = k + m
         P = (S + 255) // 256 * 256
         nb = max(2, int(np.ceil(2.2 * GiB / (N * t * P))))
         g = torch.Generator(device="cuda").manual_seed(1)
-        bufs = [(torch.randint(0, 256, (N, k, P), dtype=torch.uint8, device="cuda", generator=g),
-                 torch.empty((N, m, P), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
-        out_rows = {"rec1pb_out": 1, "rec2pb_out": 2, "rec2sb_out": 2}.get(mode, m) if layout else m
+        # "@spad": 256 B more between stripes in the data and parity regions (stripe
+        # pitches k*P + 256 / m*P + 256), other layouts the packed k*P / m*P
+        spad = 256 if layout.endswith("spad") else 0
+        DSP, PSP = k * P + spad, m * P + spad
+        bufs = [(torch.randint(0, 256, (N, DSP), dtype=torch.uint8, device="cuda", generator=g),
+                 torch.empty((N, PSP), dtype=torch.uint8, device="cuda")) for _ in range(nb)]
+        out_rows = ({"rec1pb_out": 1, "rec2pb_out": 2, "rec2sb_out": 2}.get(mode, m)
+                    if layout in ("dense", "densepad", "densespad") else m)
         osp = out_rows * P + (256 if layout == "densepad" else 0)
         outs = [torch.empty((N, osp), dtype=torch.uint8, device="cuda") for _ in range(nb)]
         rng = np.random.default_rng(3)
@@ -174,39 +180,39 @@ def main():
             c = v.ctx_for(k, m)
             d, p = bufs[i % nb]
             if mode == "enc":
-                rc = v.lib.rs_encode_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, 0, None)
+                rc = v.lib.rs_encode_batch(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N, 0, None)
             elif mode == "ver":
-                rc = v.lib.rs_verify_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, bad.data_ptr(), 0,
+                rc = v.lib.rs_verify_batch(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N, bad.data_ptr(), 0,
                                            None)
             elif mode == "rec2u":  # in place: rewrites the lost shards with their own bytes
-                rc = v.lib.rs_reconstruct_batch(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, mh.ctypes.data,
+                rc = v.lib.rs_reconstruct_batch(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N, mh.ctypes.data,
                                                 1, 0, None)
             elif mode == "rec2u_out":
-                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                     mh.ctypes.data, 1, 0, outs[i % nb].data_ptr(), m * P, None)
             elif mode == "rec2p":  # in place, per-stripe device masks
-                rc = v.lib.rs_reconstruct_batch_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_devmask(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                         md.data_ptr(), None)
             elif bound:
-                rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_out_devmask(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                             md.data_ptr(), bound, outs[i % nb].data_ptr(), osp,
                                                             None)
             elif mode in ("recmixp_out", "recmixph_out") or (v.packed and mode in ("recmix_out", "recmixh_out")):
                 dev = mode in ("recmixp_out", "recmix_out")  # packed rows (rs_reconstruct_batch_out_packed)
-                rc = v.lib.rs_reconstruct_batch_out_packed(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_out_packed(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                            md.data_ptr() if dev else mh.ctypes.data, 1 if dev else 0,
                                                            outs[i % nb].data_ptr(), roffs.data_ptr(), None)
             elif mode == "recmixh_out":
-                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                     mh.ctypes.data, N, 0, outs[i % nb].data_ptr(), m * P, None)
             else:
-                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N,
+                rc = v.lib.rs_reconstruct_batch_out(c, d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N,
                                                     md.data_ptr(), N, 1, outs[i % nb].data_ptr(), m * P, None)
             assert rc == 0, (v.name, rc)
 
         for v in vs:  # every batch a codeword; warm each variant's kernels
             for d, p in bufs:
-                v.lib.rs_encode_batch(v.ctx_for(k, m), d.data_ptr(), k * P, p.data_ptr(), m * P, P, S, N, 0, None)
+                v.lib.rs_encode_batch(v.ctx_for(k, m), d.data_ptr(), DSP, p.data_ptr(), PSP, P, S, N, 0, None)
             run(v, 0)
         torch.cuda.synchronize()
         res = {v.name: [] for v in vs}
