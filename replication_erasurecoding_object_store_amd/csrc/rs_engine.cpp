@@ -904,9 +904,8 @@ int upload_acquire(Engine* e, const uint32_t* masks, size_t n, hipStream_t s, Up
   }
   std::memcpy(u->host.p, masks, n * 4);
   if (extra_n) std::memcpy(static_cast<uint32_t*>(u->host.p) + n, extra, extra_n * 4);
-  if (!rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev), static_cast<uint32_t*>(u->dev.p), n, s))
-    return RS_ERR_DEVICE;
-  if (extra_n && !rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev) + n, extra_dst, extra_n, s))
+  if (!rs::launch_words_copy(static_cast<const uint32_t*>(u->host_dev), static_cast<uint32_t*>(u->dev.p), n, s,
+                             extra_n ? extra_dst : nullptr, extra_n))
     return RS_ERR_DEVICE;
   *dev = static_cast<const uint32_t*>(u->dev.p);
   // the reading kernel's own completion updates the slot's event (no marker packet

@@ -1930,20 +1930,30 @@ bool launch_row_offsets(const uint32_t* masks, uint32_t full, uint32_t max_rows,
 
 // Per-stripe host masks into device memory, read straight from the pinned slot over
 // PCIe: one 16-B load per lane (tail words singly), on the launch stream itself.
+// Words [0, n) of src to dst, then words [n, n + n2) of src to dst2 (a second array
+// staged behind the first in the same pinned slot: a packed batch's row offsets) --
+// one launch for both.
 __global__ __launch_bounds__(256) void words_copy_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                                         uint64_t n) {
+                                                         uint64_t n, uint32_t* __restrict__ dst2, uint64_t n2) {
   const uint64_t i = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4u;
   if (i + 4u <= n) {
     *reinterpret_cast<u32x4*>(dst + i) = *reinterpret_cast<const u32x4*>(src + i);
-  } else {
-    for (uint64_t j = i; j < n; ++j) dst[j] = src[j];
+    return;
+  }
+  const uint64_t end = n + n2;
+  for (uint64_t j = i; j < i + 4u && j < end; ++j) {
+    const uint32_t w = src[j];
+    if (j < n)
+      dst[j] = w;
+    else
+      dst2[j - n] = w;
   }
 }
 
-bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s) {
-  if (n == 0) return true;
-  const uint64_t blocks = (n + 1023u) / 1024u;
-  hipLaunchKernelGGL(words_copy_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, src, dst, n);
+bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s, uint32_t* dst2, uint64_t n2) {
+  if (n + n2 == 0) return true;
+  const uint64_t blocks = (n + n2 + 1023u) / 1024u;
+  hipLaunchKernelGGL(words_copy_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, src, dst, n, dst2, n2);
   return hipGetLastError() == hipSuccess;
 }
 

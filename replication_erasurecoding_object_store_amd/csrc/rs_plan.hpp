@@ -142,7 +142,9 @@ void launch_copy(const void* src, void* dst, uint64_t bytes, uint32_t grid_block
 void set_stop_event(hipEvent_t ev, bool* used);
 // n uint32 words from src (pinned host memory the GPU maps, or device memory) to dst
 // (device memory), on s: per-stripe host masks staged by a kernel on the launch stream.
-bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s);
+// n2 > 0: the next n2 words of src go to dst2 in the same launch.
+bool launch_words_copy(const uint32_t* src, uint32_t* dst, uint64_t n, hipStream_t s, uint32_t* dst2 = nullptr,
+                       uint64_t n2 = 0);
 // dst[i] = sum over j < i of popcount(~masks[j] & full) for i <= n (dst has n + 1 words):
 // the output row of stripe i's first missing shard in a packed batch; a stripe missing
 // more than max_rows counts 0.  One workgroup walks the masks in chunks on s.
